@@ -1,0 +1,289 @@
+#!/usr/bin/env python3
+"""bench.py — fp32 SGEMM (M=N=K=4096) on MI355X via libtensorium_hip.so, plus
+YOLOv3-416 conv-forward images/s, per BASELINE.json's metric.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N ... bench.py --gpus N      (one process per GPU)
+
+A "step" is one pass of the hot path over one batch of synthetic input: one
+NN SGEMM 4096^3 (alpha=1, beta=0; BASELINE configs[1]) on operands already
+resident in HBM.  With N GPUs every rank runs its own independent GEMM per
+step (independent units, no data-path collective — SURVEY §8e), so scaling is
+weak and `value` = total FLOP of all ranks / max-over-ranks time.
+
+Extra fields on the single JSON line:
+  roofline     — dominant kernel (sgemm_mfma) vs the fp32 MFMA peak, its
+                 duration taken live with HIP events on the stream the kernel
+                 is launched on; `traffic` from the committed PMC pass
+                 (profiles/, FETCH_SIZE doubled per the gfx950 guide) or null.
+  cpu_baseline — the oracle's restated sgemm_nn (reference: ntensors.pas
+                 cblas_sgemm -> sgemm_nn -> saxpy_avx2) on the host cores, rank
+                 0 at N=1 only, on a bounded sample of rows of the same product.
+  yolo         — YOLOv3-416 conv forward, batch 8 per GPU, 75 conv layers
+                 (BASELINE configs[2]); images/s over all ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+PEAK_F32_TFLOPS = 157.3   # MI355X fp32 MFMA (= vector) peak, MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--yolo-steps", type=int, default=5)
+    ap.add_argument("--no-yolo", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target CPU-baseline sample duration")
+    return ap.parse_args()
+
+
+def dist_setup(n_gpus):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+        return dist, rank, world, local
+    torch.cuda.set_device(0)
+    return None, 0, 1, 0
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def synthetic(torch, shape, seed, lo=-1.0, hi=1.0):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    return torch.rand(shape, generator=g, device="cuda", dtype=torch.float32) * (hi - lo) + lo
+
+
+def bench_sgemm(torch, hip, dist, rank, n, steps, warmup):
+    A = synthetic(torch, (n, n), 2 * 1000 + rank)
+    B = synthetic(torch, (n, n), 2 * 1000 + 500 + rank)
+    Cm = torch.zeros((n, n), device="cuda", dtype=torch.float32)
+
+    def step():
+        hip.gemm(False, False, n, n, n, 1.0, A, 0, n, B, 0, n, 0.0, Cm, 0, n)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    # per-launch kernel duration with HIP events on the kernel's own stream
+    # (TNNHip attaches torch's current stream, so torch.cuda.Event records there)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    barrier(dist)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        ev[i][0].record()
+        step()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    barrier(dist)
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    return wall, float(np.mean(kern_ms)), float(np.min(kern_ms))
+
+
+def bench_yolo(torch, hip, dist, rank, steps, warmup=1):
+    from tensorium_amd.yolo import yolov3_conv_table
+    specs = yolov3_conv_table()
+    batch = 8
+    layers = []
+    max_ws = 0
+    for s in specs:
+        x = synthetic(torch, (batch, s.c, s.h, s.h), 3 * 100000 + rank * 1000 + s.index, 0.0, 1.0)
+        sc = float(np.sqrt(2.0 / (s.size * s.size * s.c)))
+        w = synthetic(torch, (s.filters, s.K), 3 * 200000 + s.index, -sc, sc)
+        b = synthetic(torch, (s.filters,), 3 * 300000 + s.index, -0.1, 0.1)
+        out = torch.empty((batch, s.filters, s.out_h, s.out_h), device="cuda")
+        layers.append((s, x, w, b, out))
+        max_ws = max(max_ws, batch * s.col_elems)
+    ws = torch.empty(max(max_ws, 1), device="cuda")
+
+    def step():
+        for s, x, w, b, out in layers:
+            hip.convForward(batch, s.c, s.h, s.h, x, w, b, s.filters, s.size, s.stride, s.pad, 1,
+                            s.activation, ws, out, fused=True)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(dist)
+    wall = (time.perf_counter() - t0) / steps
+    # per-op split with telemetry (synchronous per op, separate pass)
+    hip.setTelemetry(True)
+    step()
+    from tensorium_amd._abi import TNS_OP_GEMM, TNS_OP_IM2COL
+    gemm_ms, i2c_ms = hip.opMs(TNS_OP_GEMM), hip.opMs(TNS_OP_IM2COL)
+    hip.setTelemetry(False)
+    gflop = sum(s.flops for s in specs) * batch / 1e9
+    col_bytes = sum(s.col_elems for s in specs) * batch * 4
+    in_bytes = sum(s.c * s.h * s.h for s in specs if s.needs_im2col) * batch * 4
+    return {
+        "batch_per_gpu": batch, "ms_per_batch": wall * 1e3, "gflop_per_batch": gflop,
+        "gemm_ms": gemm_ms, "im2col_ms": i2c_ms,
+        "gemm_tflops": gflop / gemm_ms if gemm_ms > 0 else None,
+        "im2col_gbs": (col_bytes + in_bytes) / (i2c_ms * 1e6) if i2c_ms > 0 else None,
+    }
+
+
+def cpu_baseline(n, target_s):
+    """Oracle sgemm_nn (port of the reference CPU path) on a row sample."""
+    from oracle import oracle as ora
+    threads = int(os.environ.get("TNS_ORACLE_THREADS") or os.environ.get("OMP_NUM_THREADS") or
+                  min(os.cpu_count() or 4, 16))
+    ora.set_threads(threads)
+    A = ora.uniform(n * n, 2, 0).reshape(n, n)
+    B = ora.uniform(n * n, 2, 1).reshape(n, n)
+    C = np.zeros((n, n), np.float32)
+    rows = max(threads, 16)
+    t0 = time.perf_counter()
+    ora.sgemm_rows(False, False, 0, rows, n, n, n, 1.0, A, n, B, n, 0.0, C, n)
+    dt = time.perf_counter() - t0
+    more = int(rows * max(target_s - dt, 0.0) / max(dt, 1e-9))
+    more = min(more, n - rows)
+    more -= more % threads if more > threads else 0
+    if more > 0:
+        t1 = time.perf_counter()
+        ora.sgemm_rows(False, False, rows, rows + more, n, n, n, 1.0, A, n, B, n, 0.0, C, n)
+        dt2 = time.perf_counter() - t1
+        rows_t, secs = more, dt2
+    else:
+        rows_t, secs = rows, dt
+    gflops = 2.0 * rows_t * n * n / secs / 1e9
+    return {"value": round(gflops, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+            "sample": f"{rows_t} of {n} rows of the {n}^3 NN product "
+                      f"(restated sgemm_nn/saxpy_avx2 FMA chain, {secs:.1f} s)"}
+
+
+def traffic_from_profiles(n):
+    """HBM bytes per sgemm launch from the committed rocprofv3 PMC pass."""
+    cands = sorted(ROOT.glob("profiles/*sgemm_traffic*.json"))
+    if not cands:
+        return None, None
+    try:
+        d = json.loads(cands[-1].read_text())
+        if int(d.get("size", 0)) == n and d.get("bytes_per_launch"):
+            return float(d["bytes_per_launch"]), str(cands[-1].relative_to(ROOT))
+    except Exception:
+        pass
+    return None, None
+
+
+def main():
+    args = parse()
+    import torch
+    dist, rank, world, local = dist_setup(args.gpus)
+    from tensorium_amd.nnhip import TNNHip
+    hip = TNNHip(local)
+    n = args.size
+
+    wall, kern_ms, kern_min = bench_sgemm(torch, hip, dist, rank, n, args.steps, args.warmup)
+    wall = max_over_ranks(dist, wall)
+    flop = 2.0 * n * n * n
+    ms_per_step = wall / args.steps * 1e3
+    value = world * flop / (ms_per_step / 1e3) / 1e9   # GFLOP/s, whole job
+    achieved = flop / (kern_ms * 1e-3) / 1e12            # TFLOP/s, per launch
+    traffic, traffic_src = traffic_from_profiles(n)
+
+    yolo = None
+    if not args.no_yolo and args.yolo_steps > 0:
+        y = bench_yolo(torch, hip, dist, rank, args.yolo_steps)
+        ms = max_over_ranks(dist, y["ms_per_batch"])
+        y["ms_per_batch"] = ms
+        y["images_per_s"] = world * y["batch_per_gpu"] / (ms / 1e3)
+        yolo = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in y.items()}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            cpu = cpu_baseline(n, args.cpu_seconds)
+        except Exception as e:  # the baseline is reported, never required
+            cpu = {"value": None, "error": str(e)}
+
+    if rank == 0:
+        line = {
+            "metric": "fp32 SGEMM GFLOP/s (M=N=K=4096) + YOLOv3 conv-fwd images/s",
+            "value": round(value, 2),
+            "unit": "GFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic U[-1,1) operands generated on device (torch RNG), resident in HBM",
+            "config": {"workload": f"sgemm_nn_{n}x{n}x{n}", "M": n, "N": n, "K": n,
+                       "alpha": 1.0, "beta": 0.0, "gemms_per_gpu_per_step": 1,
+                       "parallelism": f"{world} independent replicas, one process per GPU, "
+                                      "no data-path collective"},
+            "roofline": {"bound": "mfma", "kernel": "sgemm_mfma_kernel<NN>",
+                         "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel_ms_mean": round(kern_ms, 4), "kernel_ms_min": round(kern_min, 4),
+                         "algorithmic_flop_per_launch": flop},
+            "cpu_baseline": cpu,
+            "yolo": yolo,
+        }
+        print(json.dumps(line), flush=True)
+    hip.finish()
+    hip.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,268 @@
+/*
+ * tns.h — C ABI of libtensorium_hip.so, the MI355X (gfx950) backend for
+ * Tensorium's fp32 SGEMM + im2col-convolution hot path.
+ *
+ * Two boundaries, both plain cdecl (SysV x86-64), no C++ or torch types:
+ *
+ *  A. Op-table drop-ins (host pointers).  Each function has exactly the
+ *     parameter list of one TTensor<Single> class-var procedure pointer
+ *     (source/ntensors.pas:345-385, bound in TTensorOps.initSingle,
+ *     ntensors.pas:12651-12758).  A Pascal maintainer assigns e.g.
+ *       TSingleTensor.gemm := @tns_cblas_sgemm;
+ *     after initSingle, exactly like the USE_OPENBLAS / USE_MKL overrides at
+ *     ntensors.pas:12735-12756.  These return void (the Pascal pointer types
+ *     have no status channel): a failure is recorded in a thread-local error
+ *     string read with tns_last_error(); an optional fatal hook
+ *     (tns_set_error_hook) lets the binding raise like SAFE_CALL does
+ *     (nncuda.pas:216-275).  The shim stages host buffers through device
+ *     scratch that it owns; results are complete when the call returns.
+ *
+ *  B. Device-resident backend (device pointers + element offsets), the HIP
+ *     twin of TNNCuda<T> (source/nncuda.pas:35-157) / TNNOpenCL<T>
+ *     (source/nnopencl.pas:222-319).  Calls are stream-ordered and
+ *     asynchronous on the context's stream; tns_hip_finish() synchronises,
+ *     as TNNCuda.finish does (nncuda.pas:1575).  Every call returns a status
+ *     (0 = TNS_OK); tns_last_error() carries the message.
+ *
+ * Enumerations keep the reference's ordinal values: CBLAS_LAYOUT /
+ * CBLAS_TRANSPOSE (ntensors.pas:106-128, {$Z4} => 4-byte enums) and
+ * TActivationType (ntypes.pas:66-71).
+ */
+#ifndef TNS_H
+#define TNS_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TNS_ABI_VERSION 1
+
+/* ---- enums (reference ordinals) ---------------------------------------- */
+enum { TNS_CblasRowMajor = 101, TNS_CblasColMajor = 102 };           /* ntensors.pas:106-107 */
+enum { TNS_CblasNoTrans = 111, TNS_CblasTrans = 112 };               /* ntensors.pas:119-120 */
+
+/* TActivationType, ntypes.pas:66-71 */
+enum {
+  TNS_acLOGISTIC = 0, TNS_acRELU = 1, TNS_acRELU6 = 2, TNS_acRELIE = 3,
+  TNS_acLINEAR = 4, TNS_acRAMP = 5, TNS_acTANH = 6, TNS_acPLSE = 7,
+  TNS_acREVLEAKY = 8, TNS_acLEAKY = 9, TNS_acELU = 10, TNS_acLOGGY = 11,
+  TNS_acSTAIR = 12, TNS_acHARDTAN = 13, TNS_acLHTAN = 14, TNS_acSELU = 15
+};
+
+/* status codes (boundary B) */
+enum {
+  TNS_OK = 0,
+  TNS_ERR_ARG = 1,        /* invalid argument (shape, enum, null pointer) */
+  TNS_ERR_HIP = 2,        /* a HIP runtime call failed                    */
+  TNS_ERR_NOMEM = 3,      /* device allocation failed                     */
+  TNS_ERR_UNSUPPORTED = 4 /* enum value the backend does not implement    */
+};
+
+/* ---- library / error channel ------------------------------------------- */
+int         tns_abi_version(void);
+const char* tns_last_error(void);          /* thread-local, "" when none   */
+void        tns_clear_error(void);
+typedef void (*tns_error_hook_t)(int code, const char* msg);
+void        tns_set_error_hook(tns_error_hook_t hook);
+int         tns_device_count(void);
+
+/* =========================================================================
+ * A. Op-table drop-ins (host pointers)
+ * ========================================================================= */
+
+/* TTensor<Single>.gemm  — ntensors.pas:345-347, CPU impl cblas_sgemm
+ * ntensors.pas:2231-2286.  Row-major only (Order is accepted and ignored,
+ * as the reference ignores it).  beta<>1 pre-scales C (beta=0 => 0*C, so
+ * NaN/Inf in C propagate, ntensors.pas:2259-2261). */
+void tns_cblas_sgemm(int32_t Order, int32_t TransA, int32_t TransB,
+                     int64_t M, int64_t N, int64_t K, float ALPHA,
+                     const float* A, int64_t lda, const float* B, int64_t ldb,
+                     float BETA, float* C, int64_t ldc);
+
+/* TTensor<Single>.gemmStridedBatched — ntensors.pas:348-351, CPU impl
+ * cblas_sgemm_batch_strided ntensors.pas:2288-2304. */
+void tns_cblas_sgemm_batch_strided(int32_t Layout, int32_t TransA, int32_t TransB,
+                                   int64_t M, int64_t N, int64_t K, float alpha,
+                                   const float* A, int64_t lda, int64_t strideA,
+                                   const float* B, int64_t ldb, int64_t strideB,
+                                   float beta, float* C, int64_t ldc, int64_t strideC,
+                                   int64_t batch_size);
+
+/* TTensor<Single>.im2Colvv — ntensors.pas:362-366, CPU impl sim2Col
+ * ntensors.pas:11415-11491.  multiThread is a Pascal boolean (1 byte). */
+void tns_im2col(int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight,
+                int64_t padWidth, int64_t strideY, int64_t strideX,
+                int64_t dilationY, int64_t dilationX,
+                const float* inData, int64_t inOffset,
+                float* outData, int64_t outOffset, uint8_t multiThread);
+
+/* TTensor<Single>.col2imvv — ntensors.pas:367-371, CPU impl scol2im
+ * ntensors.pas:11717-11763 (accumulates into im; never zeroes it). */
+void tns_col2im(int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight,
+                int64_t padWidth, int64_t strideY, int64_t strideX,
+                int64_t dilationY, int64_t dilationX,
+                const float* inData, int64_t inOffset,
+                float* outData, int64_t outOffset, int64_t batch,
+                uint8_t multiThread);
+
+/* TTensor<Single>.im2colStridedBatchedvv — ntensors.pas:372-378, CPU impl
+ * sim2colStridedBatched ntensors.pas:11493-11532. */
+void tns_im2col_strided_batched(int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                                int64_t kernelHeight, int64_t kernelWidth,
+                                int64_t padHeight, int64_t padWidth,
+                                int64_t strideY, int64_t strideX,
+                                int64_t dilationY, int64_t dilationX,
+                                const float* im, int64_t imStride, int64_t imOffset,
+                                float* col, int64_t colStride, int64_t colOffset,
+                                int64_t batchCount);
+
+/* TTensor<Single>.col2imStridedBatchedvv — ntensors.pas:379-385, CPU impl
+ * scol2imStridedBatched ntensors.pas:11833-11879. */
+void tns_col2im_strided_batched(int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                                int64_t kernelHeight, int64_t kernelWidth,
+                                int64_t padHeight, int64_t padWidth,
+                                int64_t strideY, int64_t strideX,
+                                int64_t dilationY, int64_t dilationX,
+                                const float* inData, int64_t inStride, int64_t inOffset,
+                                float* outData, int64_t outStride, int64_t outOffset,
+                                int64_t batchCount);
+
+/* =========================================================================
+ * B. Device-resident backend (TNNCuda<T> twin).  Pointers are device
+ *    pointers (hipMalloc / torch); offsets are in ELEMENTS, as TCUMem+offset.
+ * ========================================================================= */
+typedef struct tns_ctx tns_ctx;
+
+/* TNNCuda.Create(deviceIndex) — nncuda.pas:448-467.  Creates its own
+ * non-blocking stream unless one is attached with tns_hip_set_stream. */
+int  tns_hip_create(int32_t deviceIndex, tns_ctx** out);
+int  tns_hip_destroy(tns_ctx* ctx);
+int  tns_hip_set_stream(tns_ctx* ctx, void* hipStream);   /* hipStream_t */
+void* tns_hip_get_stream(tns_ctx* ctx);
+int  tns_hip_finish(tns_ctx* ctx);                         /* nncuda.pas:1575 */
+
+/* createDeviceBuffer / freeDeviceBuffer / writeBuffer / readBuffer —
+ * nncuda.pas:104-107 (sizes in BYTES for copies, as the reference). */
+int  tns_hip_malloc(tns_ctx* ctx, int64_t nElements, float** out);
+int  tns_hip_free(tns_ctx* ctx, float* p);
+int  tns_hip_write_buffer(tns_ctx* ctx, float* dev, int64_t bytes, const void* host);
+int  tns_hip_read_buffer(tns_ctx* ctx, const float* dev, int64_t bytes, void* host);
+
+/* TNNCuda.gemm — nncuda.pas:624-725.  Same semantics as cblas_sgemm. */
+int tns_hip_gemm(tns_ctx* ctx, uint8_t transA, uint8_t transB,
+                 int64_t M, int64_t N, int64_t K, float ALPHA,
+                 const float* A, int64_t aOffset, int64_t lda,
+                 const float* B, int64_t bOffset, int64_t ldb,
+                 float BETA, float* C, int64_t cOffset, int64_t ldc);
+
+/* TNNCuda.gemmStridedBatched — nncuda.pas:809.  strideA = 0 shares A
+ * (conv weights, nConvolutionLayer.pas:1078). */
+int tns_hip_gemm_strided_batched(tns_ctx* ctx, uint8_t transA, uint8_t transB,
+                                 int64_t M, int64_t N, int64_t K, float ALPHA,
+                                 const float* A, int64_t aOffset, int64_t lda, int64_t strideA,
+                                 const float* B, int64_t bOffset, int64_t ldb, int64_t strideB,
+                                 float BETA, float* C, int64_t cOffset, int64_t ldc, int64_t strideC,
+                                 int64_t batchCount);
+
+/* TNNCuda.im2col — nncuda.pas:1144 (output layout = CPU sim2Col). */
+int tns_hip_im2col(tns_ctx* ctx, int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                   int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight, int64_t padWidth,
+                   int64_t strideY, int64_t strideX, int64_t dilationY, int64_t dilationX,
+                   const float* im, int64_t imOffset, float* col, int64_t colOffset);
+
+/* Strided-batched im2col (one launch for the whole batch). */
+int tns_hip_im2col_strided_batched(tns_ctx* ctx, int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                   int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight, int64_t padWidth,
+                   int64_t strideY, int64_t strideX, int64_t dilationY, int64_t dilationX,
+                   const float* im, int64_t imStride, int64_t imOffset,
+                   float* col, int64_t colStride, int64_t colOffset, int64_t batchCount);
+
+/* TNNCuda.col2im — nncuda.pas:1212.  Race-free gather; per-pixel sum in the
+ * CPU scol2im's ascending kernel-index order (ntensors.pas:11650-11715),
+ * including its dilation formula (input_row := (kernel_row-pad)*dil). */
+int tns_hip_col2im(tns_ctx* ctx, int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                   int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight, int64_t padWidth,
+                   int64_t strideY, int64_t strideX, int64_t dilationY, int64_t dilationX,
+                   const float* col, int64_t colOffset, float* im, int64_t imOffset);
+
+int tns_hip_col2im_strided_batched(tns_ctx* ctx, int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                   int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight, int64_t padWidth,
+                   int64_t strideY, int64_t strideX, int64_t dilationY, int64_t dilationX,
+                   const float* col, int64_t colStride, int64_t colOffset,
+                   float* im, int64_t imStride, int64_t imOffset, int64_t batchCount);
+
+/* TNNCuda.forwardBias — nncuda.pas:582.  dst[(b*srcSize+i)*bs + j] += src[i*incb],
+ * bs = dstSize/(srcSize*batch)  (vsAddB, ntensors.pas:4066-4093). */
+int tns_hip_forward_bias(tns_ctx* ctx, int64_t dstSize, float* dst, int64_t offset,
+                         int64_t srcSize, const float* src, int64_t incb, int64_t batch);
+
+/* TNNCuda.backwardBias — dst[i] += sum_b sum_j src[(b*dstSize+i)*bs + j]
+ * (addSums, ntensors.pas:7729-7781). */
+int tns_hip_backward_bias(tns_ctx* ctx, int64_t dstSize, float* dst, int64_t srcSize,
+                          const float* src, int64_t srcOffset, int64_t incb, int64_t batch);
+
+/* TNNCuda.ActivateArray / DeriveArray — nncuda.pas:524, 562; formulas
+ * nactivation.pas:272-501, 508-717. */
+int tns_hip_activate_array(tns_ctx* ctx, int64_t N, float* x, int64_t offset, int32_t activation);
+int tns_hip_derive_array(tns_ctx* ctx, int64_t N, const float* x, int64_t offset,
+                         int32_t activation, float* delta);
+
+/* BLAS-1 / elementwise support (TNNCuda.axpy/scale/fill/copy/clamp). */
+int tns_hip_axpy(tns_ctx* ctx, int64_t N, float a, const float* x, int64_t xOffset, int64_t incx,
+                 float* y, int64_t yOffset, int64_t incy);
+int tns_hip_scale(tns_ctx* ctx, int64_t N, float a, float* x, int64_t stride);
+int tns_hip_fill(tns_ctx* ctx, int64_t N, float* x, int64_t offset, float val, int64_t stride);
+int tns_hip_copy(tns_ctx* ctx, int64_t N, const float* src, int64_t srcOffset, int64_t inca,
+                 float* dst, int64_t dstOffset, int64_t incb);
+int tns_hip_clamp(tns_ctx* ctx, int64_t N, float alpha, const float* src, float* dst,
+                  int64_t stride, int64_t offset);
+
+/* ---- layer drivers (host logic of the reference, running on device) ---- */
+
+/* TTensor.Conv2D — ntensors.pas:8252-8349.  input: batch x C x H x W,
+ * weights: filters x (C*kH*kW) row-major, out: batch x filters x oH x oW.
+ * im2col is skipped for 1x1 / stride 1 / dilation 1 (ntensors.pas:8286-8312).
+ * workspace: >= batch*C*kH*kW*oH*oW floats, or NULL to use ctx scratch.
+ * NOTE: mirrors the reference's slot swap: xDilation is passed as dilationY
+ * (ntensors.pas:8303); harmless for square dilation. */
+int tns_hip_conv2d(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
+                   const float* input, const float* weights, int64_t filters,
+                   int64_t kH, int64_t kW, int64_t wPadding, int64_t hPadding,
+                   int64_t xStride, int64_t yStride, int64_t xDilation, int64_t yDilation,
+                   float* workspace, float* out);
+
+/* TConvolutionalLayer.forward / forwardGPU with fused (folded) BN —
+ * nConvolutionLayer.pas:457-569 / 1022-1153: Conv2D -> forwardBias ->
+ * activate.  fused=1 runs bias+activation in the SGEMM epilogue (same
+ * arithmetic, one fewer HBM pass); fused=0 runs the three reference stages. */
+int tns_hip_conv_forward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
+                         const float* input, const float* weights, const float* biases,
+                         int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
+                         int64_t dilation, int32_t activation, float* workspace,
+                         float* out, int32_t fused);
+
+/* Multi-GPU batched GEMM (config 4): batchCount independent GEMMs on the
+ * caller's device; sharding across ranks is done by the caller (one process
+ * per GPU) — see bench.py.  Provided for completeness with the ctx API. */
+
+/* ---- telemetry (TTensorMetrics-style per-op device timing) ------------ */
+int    tns_hip_set_telemetry(tns_ctx* ctx, int32_t enable);
+double tns_hip_op_ms(tns_ctx* ctx, int32_t op);   /* accumulated ms per op */
+enum { TNS_OP_GEMM = 0, TNS_OP_IM2COL = 1, TNS_OP_COL2IM = 2, TNS_OP_BIAS = 3,
+       TNS_OP_ACTIVATE = 4, TNS_OP_COUNT = 5 };
+
+/* ---- tuning / options -------------------------------------------------- */
+/* TNS_OPT_STRICT_BETA0 (default 1): beta==0 computes 0*C like the reference
+ * (NaN/Inf in C propagate).  0 = BLAS convention (C not read). */
+enum { TNS_OPT_STRICT_BETA0 = 0 };
+int tns_set_option(int32_t opt, int64_t value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TNS_H */

@@ -1,0 +1,116 @@
+/*
+ * tns_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of Tensorium's fp32 SGEMM + im2col-convolution hot path
+ * (reference: /root/reference/source, Free Pascal + inline AVX2 asm).  Used
+ * only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as
+ * the checker — never by the product path (libtensorium_hip.so).
+ *
+ * PARITY UNPINNED by reference artefacts: the reference ships no tests,
+ * golden vectors or fixtures, and its Pascal sources cannot be compiled here
+ * (no fpc/lazbuild/dcc).  This restatement is pinned instead by hand-derived
+ * known-answer vectors that exercise the reference's documented operation
+ * order (tests/golden/), by exact small-integer arithmetic, and by float64
+ * cross-checks.  See DESIGN.md §Oracle.
+ *
+ * Every function cites the reference lines it restates.
+ */
+#ifndef TNS_ORACLE_H
+#define TNS_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* worker count of the restated steroids TOPool (steroids.pas:281-296:
+ * max(ProcessorCount, 4) by default).  n<=0 restores the default. */
+void    ora_set_threads(int n);
+int     ora_get_threads(void);
+
+/* saxpy_avx2 (ntensors.pas:1308-1435): y[i] = fma(a, x[i], y[i]) for every i
+ * (the 4x8, 8 and scalar loops all use vfmadd231). */
+void    ora_saxpy(int64_t N, float a, const float* x, float* y);
+/* sdot_avx2 (ntensors.pas:1233-1306): 8 FMA lanes, masked FMA tail,
+ * s_l = lane_l + lane_{l+4}, result (s0+s1)+(s2+s3). */
+float   ora_sdot(int64_t N, const float* A, const float* B);
+
+/* cblas_sgemm (ntensors.pas:2231-2286) with sgemm_nn/nt/tn/tt
+ * (1957-2206), threaded over rows like MP.&For (steroids.pas:606-641). */
+void    ora_sgemm(int32_t order, int32_t transA, int32_t transB,
+                  int64_t M, int64_t N, int64_t K, float alpha,
+                  const float* A, int64_t lda, const float* B, int64_t ldb,
+                  float beta, float* C, int64_t ldc);
+/* Same computation restricted to rows [row0,row1) of C (CPU-baseline sample). */
+void    ora_sgemm_rows(int32_t transA, int32_t transB, int64_t row0, int64_t row1,
+                       int64_t M, int64_t N, int64_t K, float alpha,
+                       const float* A, int64_t lda, const float* B, int64_t ldb,
+                       float beta, float* C, int64_t ldc);
+/* cblas_sgemm_batch_strided (ntensors.pas:2288-2304). */
+void    ora_sgemm_batch_strided(int32_t order, int32_t transA, int32_t transB,
+                                int64_t M, int64_t N, int64_t K, float alpha,
+                                const float* A, int64_t lda, int64_t strideA,
+                                const float* B, int64_t ldb, int64_t strideB,
+                                float beta, float* C, int64_t ldc, int64_t strideC,
+                                int64_t batch);
+
+/* sim2Col (ntensors.pas:11415-11491) and sim2colStridedBatched (11493-11532). */
+void    ora_im2col(int64_t C, int64_t H, int64_t W, int64_t kH, int64_t kW,
+                   int64_t padH, int64_t padW, int64_t strideY, int64_t strideX,
+                   int64_t dilY, int64_t dilX, const float* im, int64_t imOffset,
+                   float* col, int64_t colOffset);
+void    ora_im2col_strided_batched(int64_t C, int64_t H, int64_t W, int64_t kH, int64_t kW,
+                   int64_t padH, int64_t padW, int64_t strideY, int64_t strideX,
+                   int64_t dilY, int64_t dilX, const float* im, int64_t imStride,
+                   int64_t imOffset, float* col, int64_t colStride, int64_t colOffset,
+                   int64_t batch);
+/* c2i / scol2im (ntensors.pas:11650-11763), single-threaded order, and
+ * scol2imStridedBatched (11833-11879). */
+void    ora_col2im(int64_t C, int64_t H, int64_t W, int64_t kH, int64_t kW,
+                   int64_t padH, int64_t padW, int64_t strideY, int64_t strideX,
+                   int64_t dilY, int64_t dilX, const float* col, int64_t colOffset,
+                   float* im, int64_t imOffset);
+void    ora_col2im_strided_batched(int64_t C, int64_t H, int64_t W, int64_t kH, int64_t kW,
+                   int64_t padH, int64_t padW, int64_t strideY, int64_t strideX,
+                   int64_t dilY, int64_t dilX, const float* col, int64_t colStride,
+                   int64_t colOffset, float* im, int64_t imStride, int64_t imOffset,
+                   int64_t batch);
+
+/* vsAddB (ntensors.pas:4066-4093) via TTensor.forwardBias (7709-7727). */
+void    ora_add_bias(int64_t N, float* a, int64_t blockSize, const float* b,
+                     int64_t incb, int64_t batch);
+/* addSums (ntensors.pas:7729-7781), non-AVX summation order. */
+void    ora_backward_bias(int64_t nDst, float* dst, int64_t groups, int64_t blockSize,
+                          const float* src);
+
+/* activate_array / gradient_array (nactivation.pas:508-717), scalar
+ * formulas (272-501); leaky uses the AVX2 leaky_array constant 0.1f. */
+int     ora_activate(float* x, int64_t N, int32_t act);
+int     ora_gradient(const float* x, int64_t N, int32_t act, float* delta);
+
+/* TTensor.Conv2D (ntensors.pas:8252-8349): im2col (unless 1x1/s1/d1) then
+ * per-image gemm(NN, filters, outHW, C*k^2, 1, W, .., 0, out_b, ..). */
+void    ora_conv2d(int64_t batch, int64_t C, int64_t H, int64_t W,
+                   const float* input, const float* weights, int64_t filters,
+                   int64_t kH, int64_t kW, int64_t wPadding, int64_t hPadding,
+                   int64_t xStride, int64_t yStride, int64_t xDilation, int64_t yDilation,
+                   float* workspace, float* out);
+/* TConvolutionalLayer.forward after fuseBatchNorm (nConvolutionLayer.pas:
+ * 457-569): Conv2D -> forwardBias -> activate. */
+void    ora_conv_forward(int64_t batch, int64_t C, int64_t H, int64_t W,
+                         const float* input, const float* weights, const float* biases,
+                         int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
+                         int64_t dilation, int32_t act, float* workspace, float* out);
+/* fuseBatchNorm (nConvolutionLayer.pas:102-126). */
+void    ora_fuse_batchnorm(int64_t filters, int64_t filterSize, float* weights,
+                           float* biases, const float* scales, const float* rollingMean,
+                           const float* rollingVariance);
+
+/* counter-based synthetic data (splitmix64 -> u in [lo,hi)), keyed by
+ * (seed, stream, index) so CPU and GPU regenerate identical tensors. */
+void    ora_fill_uniform(float* x, int64_t n, uint64_t seed, uint64_t stream,
+                         float lo, float hi);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,93 @@
+"""Build libtensorium_hip.so (gfx950) and the CPU oracle in-tree.
+
+The HIP library is compiled with plain ``hipcc --offload-arch=gfx950`` — no
+torch extension, no JIT cache — so the ``.so`` lives in the package directory
+and travels with the repo snapshot to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "_build"
+LIB = PKG / "libtensorium_hip.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "libtns_oracle.so"
+
+ARCH = "gfx950"
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXXFLAGS = [
+    "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+    # no implicit FMA contraction: the reference rounds mul and add separately
+    # wherever it does not issue an FMA itself (numerics)
+    "-ffp-contract=off",
+    "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result",
+]
+
+
+def _sources() -> list[Path]:
+    return sorted(CSRC.glob("*.hip")) + sorted(CSRC.glob("*.cpp"))
+
+
+def _newer(target: Path, deps: list[Path]) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd: list[str], verbose: bool) -> None:
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"command failed ({r.returncode}): {' '.join(cmd[:3])} ...")
+    if verbose and (r.stdout or r.stderr):
+        sys.stderr.write(r.stdout + r.stderr)
+
+
+def build_hip(verbose: bool = False, force: bool = False) -> Path:
+    BUILD.mkdir(exist_ok=True)
+    headers = sorted(CSRC.glob("*.hpp")) + [ROOT / "include" / "tns.h"]
+    objs: list[Path] = []
+    jobs = []
+    for src in _sources():
+        obj = BUILD / (src.name + ".o")
+        objs.append(obj)
+        if force or _newer(obj, [src, *headers]):
+            lang = ["-x", "hip"] if src.suffix == ".hip" else []
+            jobs.append([HIPCC, *CXXFLAGS, *lang, "-c", str(src), "-o", str(obj)])
+    if jobs:
+        with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
+            list(ex.map(lambda c: _run(c, verbose), jobs))
+    if force or jobs or _newer(LIB, objs):
+        tmp = LIB.with_suffix(".so.tmp")
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o",
+              str(tmp)], verbose)
+        os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(verbose: bool = False) -> Path:
+    if shutil.which("make") is None:
+        raise RuntimeError("make not found")
+    _run(["make", "-s", "-C", str(ORACLE_DIR)], verbose)
+    return ORACLE_LIB
+
+
+def build_all(verbose: bool = False, force: bool = False) -> None:
+    build_oracle(verbose)
+    build_hip(verbose, force)
+
+
+if __name__ == "__main__":
+    build_all(verbose=True, force="--force" in sys.argv)
+    print(LIB)

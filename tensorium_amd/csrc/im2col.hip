@@ -1,0 +1,174 @@
+// im2col.hip — im2col / col2im for gfx950.
+//
+// im2col restates sim2Col (ntensors.pas:11415-11491) and its batched form
+// (11493-11532): col[((c*kH+kr)*kW+kc)*oh*ow + orow*ow + ocol] =
+//   im[c][-padH + kr*dY + orow*sY][-padW + kc*dX + ocol*sX], 0 outside.
+// Pure copies => bit-exact.  Output-stationary: each thread writes 4
+// consecutive col elements with one 16-byte store when oh*ow % 4 == 0
+// (HBM-write bound; the gathered reads hit L2 — each input pixel is read
+// kH*kW times).
+//
+// col2im restates c2i/scol2im (ntensors.pas:11650-11763) as a race-free
+// GATHER: one thread per image pixel sums, in ascending kernel index order
+// (the single-threaded reference order), every col element that the
+// reference would scatter-add into it, starting from the pixel's current
+// value (the reference accumulates and never zeroes im).  Same float adds in
+// the same order => bit-exact.  The reference's col2im dilation formula,
+// input_row := (kernel_row - pad) * dil  (11693, 11700), is kept.
+#include "tns_internal.hpp"
+
+namespace tns {
+
+int64_t out_dim(int64_t in, int64_t pad, int64_t k, int64_t dil, int64_t stride) {
+  return (in + 2 * pad - (dil * (k - 1) + 1)) / stride + 1;
+}
+
+namespace {
+
+struct I2CArgs {
+  int C, H, W, kH, kW, padH, padW, sY, sX, dY, dX, oh, ow;
+  const float* im;
+  int64_t imStride;
+  float* col;
+  int64_t colStride;
+  int rows;         // C*kH*kW
+  int quads;        // ceil(oh*ow / VEC)
+};
+
+template <int VEC>
+__global__ __launch_bounds__(256) void im2col_kernel(I2CArgs a) {
+  // grid: x -> position quads of one col row, y -> (image, col row)
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= a.quads) return;
+  const int row = blockIdx.y % a.rows;
+  const int64_t img = blockIdx.y / a.rows;
+  const int kc = row % a.kW;
+  const int t = row / a.kW;
+  const int kr = t % a.kH;
+  const int c = t / a.kH;
+  const int ohw = a.oh * a.ow;
+  const float* __restrict__ im = a.im + img * a.imStride + (int64_t)c * a.H * a.W;
+  float* __restrict__ col = a.col + img * a.colStride + (int64_t)row * ohw;
+
+  const int p0 = q * VEC;
+  int orow = p0 / a.ow;
+  int ocol = p0 - orow * a.ow;
+  float v[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    const int ir = -a.padH + kr * a.dY + orow * a.sY;
+    const int ic = -a.padW + kc * a.dX + ocol * a.sX;
+    float x = 0.0f;
+    if ((unsigned)ir < (unsigned)a.H && (unsigned)ic < (unsigned)a.W && p0 + e < ohw)
+      x = im[ir * a.W + ic];
+    v[e] = x;
+    if (++ocol == a.ow) {
+      ocol = 0;
+      ++orow;
+    }
+  }
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(col + p0) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    if (p0 < ohw) col[p0] = v[0];
+  }
+}
+
+struct C2IArgs {
+  int C, H, W, kH, kW, padH, padW, sY, sX, dY, dX, oh, ow;
+  const float* col;
+  int64_t colStride;
+  float* im;
+  int64_t imStride;
+  int64_t pixels;  // C*H*W
+};
+
+__global__ __launch_bounds__(256) void col2im_kernel(C2IArgs a) {
+  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= a.pixels) return;
+  const int64_t img = blockIdx.y;
+  const int x = (int)(pix % a.W);
+  const int y = (int)((pix / a.W) % a.H);
+  const int c = (int)(pix / ((int64_t)a.W * a.H));
+  float* __restrict__ im = a.im + img * a.imStride;
+  const float* __restrict__ col = a.col + img * a.colStride;
+  const int64_t ohw = (int64_t)a.oh * a.ow;
+  float acc = im[pix];
+  for (int kr = 0; kr < a.kH; ++kr) {
+    // rows: y = (kr - padH)*dY + orow*sY
+    const int ry = y - (kr - a.padH) * a.dY;
+    if (ry < 0 || ry % a.sY != 0) continue;
+    const int orow = ry / a.sY;
+    if (orow >= a.oh) continue;
+    for (int kc = 0; kc < a.kW; ++kc) {
+      const int rx = x - (kc - a.padW) * a.dX;
+      if (rx < 0 || rx % a.sX != 0) continue;
+      const int ocol = rx / a.sX;
+      if (ocol >= a.ow) continue;
+      const int64_t i = ((int64_t)c * a.kH + kr) * a.kW + kc;
+      acc = acc + col[i * ohw + (int64_t)orow * a.ow + ocol];
+    }
+  }
+  im[pix] = acc;
+}
+
+}  // namespace
+
+hipError_t launch_im2col(const ConvGeom& g, const float* im, int64_t imStride, float* col,
+                         int64_t colStride, int64_t batch, hipStream_t s) {
+  if (g.oh <= 0 || g.ow <= 0 || batch <= 0 || g.C <= 0) return hipSuccess;
+  I2CArgs a;
+  a.C = (int)g.C; a.H = (int)g.H; a.W = (int)g.W; a.kH = (int)g.kH; a.kW = (int)g.kW;
+  a.padH = (int)g.padH; a.padW = (int)g.padW; a.sY = (int)g.sY; a.sX = (int)g.sX;
+  a.dY = (int)g.dY; a.dX = (int)g.dX; a.oh = (int)g.oh; a.ow = (int)g.ow;
+  a.im = im; a.imStride = imStride; a.col = col; a.colStride = colStride;
+  a.rows = (int)(g.C * g.kH * g.kW);
+  const int64_t ohw = g.oh * g.ow;
+  const bool vec = (ohw % 4 == 0) && ((reinterpret_cast<uintptr_t>(col) & 15) == 0) &&
+                   (colStride % 4 == 0 || batch == 1);
+  const int VEC = vec ? 4 : 1;
+  a.quads = (int)((ohw + VEC - 1) / VEC);
+  const int64_t ylim = 65535;
+  const int64_t rows_total = (int64_t)a.rows * batch;
+  // y = image*rows + row; split the batch so y fits the grid limit
+  const int64_t imgs_per_launch = rows_total <= ylim ? batch : ylim / a.rows;
+  if (imgs_per_launch <= 0) return hipErrorInvalidValue;
+  for (int64_t b0 = 0; b0 < batch; b0 += imgs_per_launch) {
+    const int64_t nb = batch - b0 < imgs_per_launch ? batch - b0 : imgs_per_launch;
+    I2CArgs sub = a;
+    sub.im = im + b0 * imStride;
+    sub.col = col + b0 * colStride;
+    dim3 grid((unsigned)((a.quads + 255) / 256), (unsigned)(nb * a.rows));
+    if (vec)
+      hipLaunchKernelGGL(im2col_kernel<4>, grid, dim3(256), 0, s, sub);
+    else
+      hipLaunchKernelGGL(im2col_kernel<1>, grid, dim3(256), 0, s, sub);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride, float* im,
+                         int64_t imStride, int64_t batch, hipStream_t s) {
+  if (g.oh <= 0 || g.ow <= 0 || batch <= 0 || g.C <= 0) return hipSuccess;
+  C2IArgs a;
+  a.C = (int)g.C; a.H = (int)g.H; a.W = (int)g.W; a.kH = (int)g.kH; a.kW = (int)g.kW;
+  a.padH = (int)g.padH; a.padW = (int)g.padW; a.sY = (int)g.sY; a.sX = (int)g.sX;
+  a.dY = (int)g.dY; a.dX = (int)g.dX; a.oh = (int)g.oh; a.ow = (int)g.ow;
+  a.col = col; a.colStride = colStride; a.im = im; a.imStride = imStride;
+  a.pixels = g.C * g.H * g.W;
+  for (int64_t b0 = 0; b0 < batch; b0 += 65535) {
+    const int64_t nb = batch - b0 < 65535 ? batch - b0 : 65535;
+    C2IArgs sub = a;
+    sub.col = col + b0 * colStride;
+    sub.im = im + b0 * imStride;
+    dim3 grid((unsigned)((a.pixels + 255) / 256), (unsigned)nb);
+    hipLaunchKernelGGL(col2im_kernel, grid, dim3(256), 0, s, sub);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // namespace tns

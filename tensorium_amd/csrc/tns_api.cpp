@@ -1,0 +1,704 @@
+// tns_api.cpp — the C ABI of libtensorium_hip.so (declared in include/tns.h).
+//
+// Host-side logic of the reference's hot path, restated for HIP:
+//   * boundary A: op-table drop-ins with host pointers (cblas_sgemm & co,
+//     ntensors.pas:345-385) staging through device scratch owned here;
+//   * boundary B: the TNNCuda<T>-shaped device API (nncuda.pas:35-157);
+//   * layer drivers: TTensor.Conv2D (ntensors.pas:8252-8349) and
+//     TConvolutionalLayer.forward/forwardGPU (nConvolutionLayer.pas:457-569,
+//     1022-1153).
+// Nothing here falls back to the CPU: every compute entry point launches a
+// gfx950 kernel or fails with a status.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "tns_internal.hpp"
+
+namespace tns {
+
+static thread_local std::string g_err;
+static tns_error_hook_t g_hook = nullptr;
+static int64_t g_strict_beta0 = 1;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  if (g_hook) g_hook(code, buf);
+  return code;
+}
+
+const char* hip_err_str(hipError_t e) { return hipGetErrorString(e); }
+
+}  // namespace tns
+
+using namespace tns;
+
+struct tns_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  // device scratch (im2col workspace, host-API staging)
+  float* scratch[4] = {nullptr, nullptr, nullptr, nullptr};
+  size_t scratch_elems[4] = {0, 0, 0, 0};
+  // telemetry (TTensorMetrics-style, nopmetrics.pas:25-44)
+  bool telemetry = false;
+  double op_ms[TNS_OP_COUNT] = {0};
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::mutex mu;  // serialises host-API use of one context
+};
+
+namespace {
+
+int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
+  if (elems < 1) elems = 1;
+  if ((size_t)elems > c->scratch_elems[slot]) {
+    if (c->scratch[slot]) {
+      hipStreamSynchronize(c->stream);
+      hipFree(c->scratch[slot]);
+      c->scratch[slot] = nullptr;
+      c->scratch_elems[slot] = 0;
+    }
+    hipError_t e = hipMalloc(&c->scratch[slot], (size_t)elems * sizeof(float));
+    if (e != hipSuccess)
+      return set_error(TNS_ERR_NOMEM, "hipMalloc(%lld floats) failed: %s", (long long)elems,
+                       hipGetErrorString(e));
+    c->scratch_elems[slot] = (size_t)elems;
+  }
+  *out = c->scratch[slot];
+  return TNS_OK;
+}
+
+struct OpTimer {
+  tns_ctx* c;
+  int op;
+  explicit OpTimer(tns_ctx* c_, int op_) : c(c_), op(op_) {
+    if (c->telemetry) hipEventRecord(c->ev0, c->stream);
+  }
+  ~OpTimer() {
+    if (c->telemetry) {
+      hipEventRecord(c->ev1, c->stream);
+      hipEventSynchronize(c->ev1);
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, c->ev0, c->ev1);
+      c->op_ms[op] += ms;
+    }
+  }
+};
+
+int check_ctx(tns_ctx* c) {
+  if (!c) return set_error(TNS_ERR_ARG, "null tns_ctx");
+  return TNS_OK;
+}
+
+int hip_status(hipError_t e, const char* what) {
+  if (e != hipSuccess) return set_error(TNS_ERR_HIP, "%s: %s", what, hipGetErrorString(e));
+  return TNS_OK;
+}
+
+int beta_mode_for(float beta) {
+  if (beta == 1.0f) return BETA_ONE;
+  if (beta == 0.0f && !g_strict_beta0) return BETA_ZERO;
+  return BETA_SCALE;
+}
+
+int do_gemm(tns_ctx* c, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha,
+            const float* A, int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
+            float beta, float* C, int64_t ldc, int64_t sC, int64_t batch, int epi,
+            const float* bias, int act) {
+  if (M < 0 || N < 0 || K < 0 || batch < 0)
+    return set_error(TNS_ERR_ARG, "gemm: negative dimension");
+  if (M == 0 || N == 0 || batch == 0) return TNS_OK;
+  // leading dimensions, row-major (cblas_sgemm conventions)
+  const int64_t minlda = ta ? M : K, minldb = tb ? K : N;
+  if ((K > 0 && (lda < (minlda > 1 ? minlda : 1) || ldb < (minldb > 1 ? minldb : 1))) ||
+      ldc < N)
+    return set_error(TNS_ERR_ARG, "gemm: leading dimension too small (lda=%lld ldb=%lld ldc=%lld)",
+                     (long long)lda, (long long)ldb, (long long)ldc);
+  if (!C || (K > 0 && (!A || !B))) return set_error(TNS_ERR_ARG, "gemm: null operand");
+  if (epi == EPI_BIAS_ACT && (!bias || !act_supported(act)))
+    return set_error(TNS_ERR_ARG, "gemm: bad fused epilogue");
+  GemmArgs a;
+  a.M = M; a.N = N; a.K = K;
+  a.alpha = alpha; a.beta = beta; a.beta_mode = beta_mode_for(beta);
+  a.A = A; a.lda = lda; a.strideA = sA;
+  a.B = B; a.ldb = ldb; a.strideB = sB;
+  a.C = C; a.ldc = ldc; a.strideC = sC;
+  a.batch = batch; a.epi = epi; a.bias = bias; a.act = act;
+  OpTimer t(c, TNS_OP_GEMM);
+  return hip_status(launch_sgemm(a, ta, tb, c->stream), "sgemm launch");
+}
+
+ConvGeom geom(int64_t C, int64_t H, int64_t W, int64_t kH, int64_t kW, int64_t pH, int64_t pW,
+              int64_t sY, int64_t sX, int64_t dY, int64_t dX) {
+  ConvGeom g;
+  g.C = C; g.H = H; g.W = W; g.kH = kH; g.kW = kW; g.padH = pH; g.padW = pW;
+  g.sY = sY; g.sX = sX; g.dY = dY; g.dX = dX;
+  g.oh = out_dim(H, pH, kH, dY, sY);
+  g.ow = out_dim(W, pW, kW, dX, sX);
+  return g;
+}
+
+int check_geom(const ConvGeom& g) {
+  if (g.C < 0 || g.H < 0 || g.W < 0 || g.kH <= 0 || g.kW <= 0 || g.sY <= 0 || g.sX <= 0 ||
+      g.dY <= 0 || g.dX <= 0 || g.padH < 0 || g.padW < 0)
+    return set_error(TNS_ERR_ARG, "im2col: invalid geometry");
+  // kernel indexing is 32-bit inside one image
+  if (g.C * g.kH * g.kW * (g.oh > 0 ? g.oh : 1) * (g.ow > 0 ? g.ow : 1) > 0x7fffffffLL ||
+      g.C * g.H * g.W > 0x7fffffffLL)
+    return set_error(TNS_ERR_ARG, "im2col: image too large for 32-bit indexing");
+  return TNS_OK;
+}
+
+// ---- default context for the host-pointer API (boundary A) ---------------
+std::once_flag g_default_once;
+tns_ctx* g_default = nullptr;
+int g_default_status = TNS_OK;
+
+tns_ctx* default_ctx() {
+  std::call_once(g_default_once, [] {
+    int dev = 0;
+    hipGetDevice(&dev);
+    g_default_status = tns_hip_create(dev, &g_default);
+  });
+  return g_default_status == TNS_OK ? g_default : nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tns_abi_version(void) { return TNS_ABI_VERSION; }
+const char* tns_last_error(void) { return g_err.c_str(); }
+void tns_clear_error(void) { g_err.clear(); }
+void tns_set_error_hook(tns_error_hook_t hook) { g_hook = hook; }
+
+int tns_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int tns_set_option(int32_t opt, int64_t value) {
+  switch (opt) {
+    case TNS_OPT_STRICT_BETA0:
+      g_strict_beta0 = value ? 1 : 0;
+      return TNS_OK;
+    default:
+      return set_error(TNS_ERR_ARG, "unknown option %d", opt);
+  }
+}
+
+// ---- context ---------------------------------------------------------------
+int tns_hip_create(int32_t deviceIndex, tns_ctx** out) {
+  if (!out) return set_error(TNS_ERR_ARG, "tns_hip_create: null out");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return set_error(TNS_ERR_HIP, "no HIP device available (%s)", hipGetErrorString(e));
+  if (deviceIndex < 0 || deviceIndex >= n)
+    return set_error(TNS_ERR_ARG, "device index %d out of range [0,%d)", deviceIndex, n);
+  TNS_HIP_TRY(hipSetDevice(deviceIndex));
+  tns_ctx* c = new tns_ctx();
+  c->device = deviceIndex;
+  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return set_error(TNS_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  c->own_stream = true;
+  hipEventCreate(&c->ev0);
+  hipEventCreate(&c->ev1);
+  *out = c;
+  return TNS_OK;
+}
+
+int tns_hip_destroy(tns_ctx* c) {
+  if (!c) return TNS_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (int i = 0; i < 4; ++i)
+    if (c->scratch[i]) hipFree(c->scratch[i]);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return TNS_OK;
+}
+
+int tns_hip_set_stream(tns_ctx* c, void* s) {
+  if (int r = check_ctx(c)) return r;
+  if (c->own_stream && c->stream) {
+    hipStreamSynchronize(c->stream);
+    hipStreamDestroy(c->stream);
+  }
+  c->stream = (hipStream_t)s;
+  c->own_stream = false;
+  return TNS_OK;
+}
+
+void* tns_hip_get_stream(tns_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int tns_hip_finish(tns_ctx* c) {
+  if (int r = check_ctx(c)) return r;
+  return hip_status(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+}
+
+int tns_hip_malloc(tns_ctx* c, int64_t n, float** out) {
+  if (int r = check_ctx(c)) return r;
+  if (!out || n < 0) return set_error(TNS_ERR_ARG, "tns_hip_malloc: bad args");
+  hipError_t e = hipMalloc((void**)out, (size_t)(n > 0 ? n : 1) * sizeof(float));
+  if (e != hipSuccess) return set_error(TNS_ERR_NOMEM, "hipMalloc: %s", hipGetErrorString(e));
+  return TNS_OK;
+}
+
+int tns_hip_free(tns_ctx* c, float* p) {
+  if (int r = check_ctx(c)) return r;
+  return hip_status(hipFree(p), "hipFree");
+}
+
+int tns_hip_write_buffer(tns_ctx* c, float* dev, int64_t bytes, const void* host) {
+  if (int r = check_ctx(c)) return r;
+  if (bytes <= 0) return TNS_OK;
+  TNS_HIP_TRY(hipMemcpyAsync(dev, host, (size_t)bytes, hipMemcpyHostToDevice, c->stream));
+  return hip_status(hipStreamSynchronize(c->stream), "writeBuffer sync");
+}
+
+int tns_hip_read_buffer(tns_ctx* c, const float* dev, int64_t bytes, void* host) {
+  if (int r = check_ctx(c)) return r;
+  if (bytes <= 0) return TNS_OK;
+  TNS_HIP_TRY(hipMemcpyAsync(host, dev, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
+  return hip_status(hipStreamSynchronize(c->stream), "readBuffer sync");
+}
+
+// ---- boundary B: device API ---------------------------------------------------
+int tns_hip_gemm(tns_ctx* c, uint8_t transA, uint8_t transB, int64_t M, int64_t N, int64_t K,
+                 float ALPHA, const float* A, int64_t aOffset, int64_t lda, const float* B,
+                 int64_t bOffset, int64_t ldb, float BETA, float* C, int64_t cOffset,
+                 int64_t ldc) {
+  if (int r = check_ctx(c)) return r;
+  return do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, A ? A + aOffset : nullptr, lda, 0,
+                 B ? B + bOffset : nullptr, ldb, 0, BETA, C ? C + cOffset : nullptr, ldc, 0, 1,
+                 EPI_NONE, nullptr, 0);
+}
+
+int tns_hip_gemm_strided_batched(tns_ctx* c, uint8_t transA, uint8_t transB, int64_t M,
+                                 int64_t N, int64_t K, float ALPHA, const float* A,
+                                 int64_t aOffset, int64_t lda, int64_t strideA, const float* B,
+                                 int64_t bOffset, int64_t ldb, int64_t strideB, float BETA,
+                                 float* C, int64_t cOffset, int64_t ldc, int64_t strideC,
+                                 int64_t batchCount) {
+  if (int r = check_ctx(c)) return r;
+  return do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, A ? A + aOffset : nullptr, lda,
+                 strideA, B ? B + bOffset : nullptr, ldb, strideB, BETA,
+                 C ? C + cOffset : nullptr, ldc, strideC, batchCount, EPI_NONE, nullptr, 0);
+}
+
+int tns_hip_im2col_strided_batched(tns_ctx* c, int64_t aChannels, int64_t aHeight,
+                                   int64_t aWidth, int64_t kernelHeight, int64_t kernelWidth,
+                                   int64_t padHeight, int64_t padWidth, int64_t strideY,
+                                   int64_t strideX, int64_t dilationY, int64_t dilationX,
+                                   const float* im, int64_t imStride, int64_t imOffset,
+                                   float* col, int64_t colStride, int64_t colOffset,
+                                   int64_t batchCount) {
+  if (int r = check_ctx(c)) return r;
+  ConvGeom g = geom(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+                    strideY, strideX, dilationY, dilationX);
+  if (int r = check_geom(g)) return r;
+  if (!im || !col) return set_error(TNS_ERR_ARG, "im2col: null pointer");
+  OpTimer t(c, TNS_OP_IM2COL);
+  return hip_status(launch_im2col(g, im + imOffset, imStride, col + colOffset, colStride,
+                                  batchCount, c->stream),
+                    "im2col launch");
+}
+
+int tns_hip_im2col(tns_ctx* c, int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                   int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight, int64_t padWidth,
+                   int64_t strideY, int64_t strideX, int64_t dilationY, int64_t dilationX,
+                   const float* im, int64_t imOffset, float* col, int64_t colOffset) {
+  return tns_hip_im2col_strided_batched(c, aChannels, aHeight, aWidth, kernelHeight, kernelWidth,
+                                        padHeight, padWidth, strideY, strideX, dilationY,
+                                        dilationX, im, 0, imOffset, col, 0, colOffset, 1);
+}
+
+int tns_hip_col2im_strided_batched(tns_ctx* c, int64_t aChannels, int64_t aHeight,
+                                   int64_t aWidth, int64_t kernelHeight, int64_t kernelWidth,
+                                   int64_t padHeight, int64_t padWidth, int64_t strideY,
+                                   int64_t strideX, int64_t dilationY, int64_t dilationX,
+                                   const float* col, int64_t colStride, int64_t colOffset,
+                                   float* im, int64_t imStride, int64_t imOffset,
+                                   int64_t batchCount) {
+  if (int r = check_ctx(c)) return r;
+  ConvGeom g = geom(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+                    strideY, strideX, dilationY, dilationX);
+  if (int r = check_geom(g)) return r;
+  if (!im || !col) return set_error(TNS_ERR_ARG, "col2im: null pointer");
+  if (batchCount > 1 && imStride < aChannels * aHeight * aWidth)
+    return set_error(TNS_ERR_ARG, "col2im: overlapping image strides");
+  OpTimer t(c, TNS_OP_COL2IM);
+  return hip_status(launch_col2im(g, col + colOffset, colStride, im + imOffset, imStride,
+                                  batchCount, c->stream),
+                    "col2im launch");
+}
+
+int tns_hip_col2im(tns_ctx* c, int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                   int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight, int64_t padWidth,
+                   int64_t strideY, int64_t strideX, int64_t dilationY, int64_t dilationX,
+                   const float* col, int64_t colOffset, float* im, int64_t imOffset) {
+  return tns_hip_col2im_strided_batched(c, aChannels, aHeight, aWidth, kernelHeight, kernelWidth,
+                                        padHeight, padWidth, strideY, strideX, dilationY,
+                                        dilationX, col, 0, colOffset, im, 0, imOffset, 1);
+}
+
+int tns_hip_forward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t offset, int64_t srcSize,
+                         const float* src, int64_t incb, int64_t batch) {
+  if (int r = check_ctx(c)) return r;
+  if (dstSize == 0) return TNS_OK;
+  if (!dst || !src || srcSize <= 0 || batch <= 0 || dstSize % (srcSize * batch) != 0)
+    return set_error(TNS_ERR_ARG, "forwardBias: sizes do not align");
+  const int64_t bs = dstSize / (srcSize * batch);
+  OpTimer t(c, TNS_OP_BIAS);
+  return hip_status(launch_forward_bias(dst + offset, srcSize, bs, src, incb, batch, c->stream),
+                    "forwardBias launch");
+}
+
+int tns_hip_backward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t srcSize,
+                          const float* src, int64_t srcOffset, int64_t incb, int64_t batch) {
+  if (int r = check_ctx(c)) return r;
+  if (!dst || !src || dstSize <= 0 || batch <= 0 || srcSize % (dstSize * batch) != 0)
+    return set_error(TNS_ERR_ARG, "backwardBias: sizes do not align");
+  const int64_t bs = srcSize / (dstSize * batch);
+  OpTimer t(c, TNS_OP_BIAS);
+  return hip_status(launch_backward_bias(dst, dstSize, src + srcOffset, bs, batch, incb, c->stream),
+                    "backwardBias launch");
+}
+
+int tns_hip_activate_array(tns_ctx* c, int64_t N, float* x, int64_t offset, int32_t activation) {
+  if (int r = check_ctx(c)) return r;
+  if (!act_supported(activation))
+    return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
+  if (N <= 0) return TNS_OK;
+  if (!x) return set_error(TNS_ERR_ARG, "activate: null pointer");
+  OpTimer t(c, TNS_OP_ACTIVATE);
+  return hip_status(launch_activate(x + offset, N, activation, c->stream), "activate launch");
+}
+
+int tns_hip_derive_array(tns_ctx* c, int64_t N, const float* x, int64_t offset,
+                         int32_t activation, float* delta) {
+  if (int r = check_ctx(c)) return r;
+  if (!act_supported(activation))
+    return set_error(TNS_ERR_UNSUPPORTED, "derivative %d not implemented", activation);
+  if (N <= 0) return TNS_OK;
+  if (!x || !delta) return set_error(TNS_ERR_ARG, "derive: null pointer");
+  OpTimer t(c, TNS_OP_ACTIVATE);
+  return hip_status(launch_derive(x + offset, N, activation, delta, c->stream), "derive launch");
+}
+
+int tns_hip_axpy(tns_ctx* c, int64_t N, float a, const float* x, int64_t xOffset, int64_t incx,
+                 float* y, int64_t yOffset, int64_t incy) {
+  if (int r = check_ctx(c)) return r;
+  return hip_status(launch_axpy(N, a, x + xOffset, incx, y + yOffset, incy, c->stream), "axpy");
+}
+
+int tns_hip_scale(tns_ctx* c, int64_t N, float a, float* x, int64_t stride) {
+  if (int r = check_ctx(c)) return r;
+  return hip_status(launch_scale(N, a, x, stride, c->stream), "scale");
+}
+
+int tns_hip_fill(tns_ctx* c, int64_t N, float* x, int64_t offset, float val, int64_t stride) {
+  if (int r = check_ctx(c)) return r;
+  return hip_status(launch_fill(N, x + offset, val, stride, c->stream), "fill");
+}
+
+int tns_hip_copy(tns_ctx* c, int64_t N, const float* src, int64_t srcOffset, int64_t inca,
+                 float* dst, int64_t dstOffset, int64_t incb) {
+  if (int r = check_ctx(c)) return r;
+  return hip_status(launch_copy(N, src + srcOffset, inca, dst + dstOffset, incb, c->stream),
+                    "copy");
+}
+
+int tns_hip_clamp(tns_ctx* c, int64_t N, float alpha, const float* src, float* dst,
+                  int64_t stride, int64_t offset) {
+  if (int r = check_ctx(c)) return r;
+  return hip_status(launch_clamp(N, alpha, src + offset, dst + offset, stride, c->stream),
+                    "clamp");
+}
+
+// ---- layer drivers ------------------------------------------------------------
+int tns_hip_conv2d(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                   const float* input, const float* weights, int64_t filters, int64_t kH,
+                   int64_t kW, int64_t wPadding, int64_t hPadding, int64_t xStride,
+                   int64_t yStride, int64_t xDilation, int64_t yDilation, float* workspace,
+                   float* out) {
+  if (int r = check_ctx(c)) return r;
+  // ntensors.pas:8266-8269: negative padding => "same"-style default
+  if (wPadding < 0) wPadding = xDilation + kW / 2 - 1;
+  if (hPadding < 0) hPadding = yDilation + kH / 2 - 1;
+  // Conv2D hands (xDilation, yDilation) to im2col's (dilationY, dilationX)
+  // slots (ntensors.pas:8303); keep the swap so non-square dilation matches.
+  ConvGeom g = geom(C, H, W, kH, kW, hPadding, wPadding, yStride, xStride, xDilation, yDilation);
+  if (int r = check_geom(g)) return r;
+  // output size as the layer computes it (nConvolutionLayer.pas:92-100)
+  const int64_t oh = out_dim(H, hPadding, kH, yDilation, yStride);
+  const int64_t ow = out_dim(W, wPadding, kW, xDilation, xStride);
+  const int64_t outImg = oh * ow, kSize = kH * kW, k = C * kSize;
+  if (oh <= 0 || ow <= 0 || batch <= 0) return TNS_OK;
+  const float* Bp;
+  int64_t strideB;
+  if (kSize != 1 || xDilation * yDilation != 1 || xStride * yStride != 1) {
+    strideB = k * outImg;
+    float* ws = workspace;
+    if (!ws)
+      if (int r = ensure_scratch(c, 0, batch * strideB, &ws)) return r;
+    {
+      OpTimer t(c, TNS_OP_IM2COL);
+      if (int r = hip_status(launch_im2col(g, input, C * H * W, ws, strideB, batch, c->stream),
+                             "im2col launch"))
+        return r;
+    }
+    Bp = ws;
+  } else {
+    strideB = C * H * W;
+    Bp = input;
+  }
+  // one strided-batched launch with the weights shared (strideA = 0) — the
+  // GPU path of nConvolutionLayer.pas:1078; beta = 0 as in Conv2D (8328)
+  return do_gemm(c, false, false, filters, outImg, k, 1.0f, weights, k, 0, Bp, outImg, strideB,
+                 0.0f, out, outImg, outImg * filters, batch, EPI_NONE, nullptr, 0);
+}
+
+int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                         const float* input, const float* weights, const float* biases,
+                         int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
+                         int64_t dilation, int32_t activation, float* workspace, float* out,
+                         int32_t fused) {
+  if (int r = check_ctx(c)) return r;
+  if (!act_supported(activation))
+    return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
+  const int64_t oh = out_dim(H, padding, kSize, dilation, stride);
+  const int64_t ow = out_dim(W, padding, kSize, dilation, stride);
+  if (!fused) {
+    if (int r = tns_hip_conv2d(c, batch, C, H, W, input, weights, filters, kSize, kSize, padding,
+                               padding, stride, stride, dilation, dilation, workspace, out))
+      return r;
+    OpTimer t(c, TNS_OP_BIAS);
+    return hip_status(launch_bias_activate(out, filters, oh * ow, biases, batch, activation,
+                                           c->stream),
+                      "bias+activate launch");
+  }
+  ConvGeom g = geom(C, H, W, kSize, kSize, padding, padding, stride, stride, dilation, dilation);
+  if (int r = check_geom(g)) return r;
+  const int64_t outImg = oh * ow, ks = kSize * kSize, k = C * ks;
+  if (oh <= 0 || ow <= 0 || batch <= 0) return TNS_OK;
+  const float* Bp;
+  int64_t strideB;
+  if (ks != 1 || dilation != 1 || stride != 1) {
+    strideB = k * outImg;
+    float* ws = workspace;
+    if (!ws)
+      if (int r = ensure_scratch(c, 0, batch * strideB, &ws)) return r;
+    {
+      OpTimer t(c, TNS_OP_IM2COL);
+      if (int r = hip_status(launch_im2col(g, input, C * H * W, ws, strideB, batch, c->stream),
+                             "im2col launch"))
+        return r;
+    }
+    Bp = ws;
+  } else {
+    strideB = C * H * W;
+    Bp = input;
+  }
+  // conv GEMM with forwardBias + activate fused into the epilogue
+  return do_gemm(c, false, false, filters, outImg, k, 1.0f, weights, k, 0, Bp, outImg, strideB,
+                 0.0f, out, outImg, outImg * filters, batch, EPI_BIAS_ACT, biases, activation);
+}
+
+int tns_hip_set_telemetry(tns_ctx* c, int32_t enable) {
+  if (int r = check_ctx(c)) return r;
+  c->telemetry = enable != 0;
+  if (c->telemetry)
+    for (double& v : c->op_ms) v = 0.0;
+  return TNS_OK;
+}
+
+double tns_hip_op_ms(tns_ctx* c, int32_t op) {
+  if (!c || op < 0 || op >= TNS_OP_COUNT) return 0.0;
+  return c->op_ms[op];
+}
+
+// ---- boundary A: host-pointer op-table drop-ins ------------------------------
+// Each stages operands through the default context's scratch and returns when
+// C (or col/im) holds the result.  No status channel exists in the Pascal
+// pointer types, so failures go to tns_last_error() / the error hook.
+
+void tns_cblas_sgemm_batch_strided(int32_t Layout, int32_t TransA, int32_t TransB, int64_t M,
+                                   int64_t N, int64_t K, float alpha, const float* A, int64_t lda,
+                                   int64_t strideA, const float* B, int64_t ldb, int64_t strideB,
+                                   float beta, float* C, int64_t ldc, int64_t strideC,
+                                   int64_t batch_size) {
+  (void)Layout;  // ignored, as cblas_sgemm ignores Order (ntensors.pas:2231)
+  tns_ctx* c = default_ctx();
+  if (!c) return;
+  if ((TransA != TNS_CblasNoTrans && TransA != TNS_CblasTrans) ||
+      (TransB != TNS_CblasNoTrans && TransB != TNS_CblasTrans)) {
+    set_error(TNS_ERR_ARG, "cblas_sgemm: bad transpose enum");
+    return;
+  }
+  if (M <= 0 || N <= 0 || batch_size <= 0) return;
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipSetDevice(c->device);
+  const bool ta = TransA == TNS_CblasTrans, tb = TransB == TNS_CblasTrans;
+  const int64_t a_rows = ta ? K : M, b_rows = tb ? N : K;
+  // extent of each operand (last batch's last element + 1)
+  auto extent = [](int64_t rows, int64_t ld, int64_t cols, int64_t stride, int64_t batch) {
+    if (rows <= 0 || cols <= 0) return (int64_t)0;
+    return (batch - 1) * stride + (rows - 1) * ld + cols;
+  };
+  const int64_t nA = extent(a_rows, lda, ta ? M : K, strideA, batch_size);
+  const int64_t nB = extent(b_rows, ldb, tb ? K : N, strideB, batch_size);
+  const int64_t nC = extent(M, ldc, N, strideC, batch_size);
+  float *dA = nullptr, *dB = nullptr, *dC = nullptr;
+  if (ensure_scratch(c, 1, nA, &dA) || ensure_scratch(c, 2, nB, &dB) ||
+      ensure_scratch(c, 3, nC, &dC))
+    return;
+  hipStream_t s = c->stream;
+  if (nA && hip_status(hipMemcpyAsync(dA, A, nA * 4, hipMemcpyHostToDevice, s), "H2D A")) return;
+  if (nB && hip_status(hipMemcpyAsync(dB, B, nB * 4, hipMemcpyHostToDevice, s), "H2D B")) return;
+  const bool needC = beta_mode_for(beta) != BETA_ZERO;
+  if (needC && hip_status(hipMemcpyAsync(dC, C, nC * 4, hipMemcpyHostToDevice, s), "H2D C"))
+    return;
+  if (!needC && strideC != M * ldc && batch_size > 1) {
+    // gaps between batches must survive the copy back
+    if (hip_status(hipMemcpyAsync(dC, C, nC * 4, hipMemcpyHostToDevice, s), "H2D C")) return;
+  } else if (!needC && ldc != N) {
+    if (hip_status(hipMemcpyAsync(dC, C, nC * 4, hipMemcpyHostToDevice, s), "H2D C")) return;
+  }
+  if (do_gemm(c, ta, tb, M, N, K, alpha, dA, lda, strideA, dB, ldb, strideB, beta, dC, ldc,
+              strideC, batch_size, EPI_NONE, nullptr, 0))
+    return;
+  if (hip_status(hipMemcpyAsync(C, dC, nC * 4, hipMemcpyDeviceToHost, s), "D2H C")) return;
+  hip_status(hipStreamSynchronize(s), "sync");
+}
+
+void tns_cblas_sgemm(int32_t Order, int32_t TransA, int32_t TransB, int64_t M, int64_t N,
+                     int64_t K, float ALPHA, const float* A, int64_t lda, const float* B,
+                     int64_t ldb, float BETA, float* C, int64_t ldc) {
+  tns_cblas_sgemm_batch_strided(Order, TransA, TransB, M, N, K, ALPHA, A, lda, 0, B, ldb, 0,
+                                BETA, C, ldc, 0, 1);
+}
+
+void tns_im2col_strided_batched(int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                                int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight,
+                                int64_t padWidth, int64_t strideY, int64_t strideX,
+                                int64_t dilationY, int64_t dilationX, const float* im,
+                                int64_t imStride, int64_t imOffset, float* col,
+                                int64_t colStride, int64_t colOffset, int64_t batchCount) {
+  tns_ctx* c = default_ctx();
+  if (!c || batchCount <= 0) return;
+  ConvGeom g = geom(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+                    strideY, strideX, dilationY, dilationX);
+  if (check_geom(g) || g.oh <= 0 || g.ow <= 0) return;
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipSetDevice(c->device);
+  const int64_t imgElems = aChannels * aHeight * aWidth;
+  const int64_t colElems = aChannels * kernelHeight * kernelWidth * g.oh * g.ow;
+  // pack images/cols densely on the device; strides apply on the host side
+  float *dIm = nullptr, *dCol = nullptr;
+  if (ensure_scratch(c, 1, imgElems * batchCount, &dIm) ||
+      ensure_scratch(c, 2, colElems * batchCount, &dCol))
+    return;
+  hipStream_t s = c->stream;
+  for (int64_t b = 0; b < batchCount; ++b)
+    if (hip_status(hipMemcpyAsync(dIm + b * imgElems, im + imOffset + b * imStride,
+                                  imgElems * 4, hipMemcpyHostToDevice, s),
+                   "H2D im"))
+      return;
+  {
+    OpTimer t(c, TNS_OP_IM2COL);
+    if (hip_status(launch_im2col(g, dIm, imgElems, dCol, colElems, batchCount, s), "im2col"))
+      return;
+  }
+  for (int64_t b = 0; b < batchCount; ++b)
+    if (hip_status(hipMemcpyAsync(col + colOffset + b * colStride, dCol + b * colElems,
+                                  colElems * 4, hipMemcpyDeviceToHost, s),
+                   "D2H col"))
+      return;
+  hip_status(hipStreamSynchronize(s), "sync");
+}
+
+void tns_im2col(int64_t aChannels, int64_t aHeight, int64_t aWidth, int64_t kernelHeight,
+                int64_t kernelWidth, int64_t padHeight, int64_t padWidth, int64_t strideY,
+                int64_t strideX, int64_t dilationY, int64_t dilationX, const float* inData,
+                int64_t inOffset, float* outData, int64_t outOffset, uint8_t multiThread) {
+  (void)multiThread;  // the device kernel is always parallel and race-free
+  tns_im2col_strided_batched(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight,
+                             padWidth, strideY, strideX, dilationY, dilationX, inData, 0,
+                             inOffset, outData, 0, outOffset, 1);
+}
+
+void tns_col2im_strided_batched(int64_t aChannels, int64_t aHeight, int64_t aWidth,
+                                int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight,
+                                int64_t padWidth, int64_t strideY, int64_t strideX,
+                                int64_t dilationY, int64_t dilationX, const float* inData,
+                                int64_t inStride, int64_t inOffset, float* outData,
+                                int64_t outStride, int64_t outOffset, int64_t batchCount) {
+  tns_ctx* c = default_ctx();
+  if (!c || batchCount <= 0) return;
+  ConvGeom g = geom(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+                    strideY, strideX, dilationY, dilationX);
+  if (check_geom(g) || g.oh <= 0 || g.ow <= 0) return;
+  std::lock_guard<std::mutex> lk(c->mu);
+  hipSetDevice(c->device);
+  const int64_t imgElems = aChannels * aHeight * aWidth;
+  const int64_t colElems = aChannels * kernelHeight * kernelWidth * g.oh * g.ow;
+  float *dIm = nullptr, *dCol = nullptr;
+  if (ensure_scratch(c, 1, imgElems * batchCount, &dIm) ||
+      ensure_scratch(c, 2, colElems * batchCount, &dCol))
+    return;
+  hipStream_t s = c->stream;
+  for (int64_t b = 0; b < batchCount; ++b) {
+    if (hip_status(hipMemcpyAsync(dCol + b * colElems, inData + inOffset + b * inStride,
+                                  colElems * 4, hipMemcpyHostToDevice, s),
+                   "H2D col"))
+      return;
+    // col2im accumulates into the existing image (ntensors.pas:11703)
+    if (hip_status(hipMemcpyAsync(dIm + b * imgElems, outData + outOffset + b * outStride,
+                                  imgElems * 4, hipMemcpyHostToDevice, s),
+                   "H2D im"))
+      return;
+  }
+  {
+    OpTimer t(c, TNS_OP_COL2IM);
+    if (hip_status(launch_col2im(g, dCol, colElems, dIm, imgElems, batchCount, s), "col2im"))
+      return;
+  }
+  for (int64_t b = 0; b < batchCount; ++b)
+    if (hip_status(hipMemcpyAsync(outData + outOffset + b * outStride, dIm + b * imgElems,
+                                  imgElems * 4, hipMemcpyDeviceToHost, s),
+                   "D2H im"))
+      return;
+  hip_status(hipStreamSynchronize(s), "sync");
+}
+
+void tns_col2im(int64_t aChannels, int64_t aHeight, int64_t aWidth, int64_t kernelHeight,
+                int64_t kernelWidth, int64_t padHeight, int64_t padWidth, int64_t strideY,
+                int64_t strideX, int64_t dilationY, int64_t dilationX, const float* inData,
+                int64_t inOffset, float* outData, int64_t outOffset, int64_t batch,
+                uint8_t multiThread) {
+  (void)batch;        // scol2im's `batch` argument is unused by the reference too
+  (void)multiThread;  // race-free gather; matches the single-threaded order
+  tns_col2im_strided_batched(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight,
+                             padWidth, strideY, strideX, dilationY, dilationX, inData, 0,
+                             inOffset, outData, 0, outOffset, 1);
+}
+
+}  // extern "C"

@@ -1,0 +1,84 @@
+// tns_internal.hpp — shared declarations of libtensorium_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tns.h"
+
+namespace tns {
+
+// ---- error channel ---------------------------------------------------------
+int set_error(int code, const char* fmt, ...);
+const char* hip_err_str(hipError_t e);
+
+#define TNS_HIP_TRY(expr)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return ::tns::set_error(TNS_ERR_HIP, "%s failed: %s (%s:%d)", #expr,            \
+                              ::tns::hip_err_str(_e), __FILE__, __LINE__);             \
+  } while (0)
+
+// ---- SGEMM -----------------------------------------------------------------
+// Epilogue applied after the K loop (fused conv path):
+//   EPI_NONE          C = acc
+//   EPI_BIAS_ACT      C = act(acc + bias[row])   (forwardBias + activate)
+enum EpiKind { EPI_NONE = 0, EPI_BIAS_ACT = 1 };
+
+// beta handling, decided on the host:
+//   BETA_ZERO   acc starts at 0 (C not read)       — BLAS convention
+//   BETA_ONE    acc starts at C                     — matMul accumulate
+//   BETA_SCALE  acc starts at beta*C (single mul)   — reference mulvs, incl.
+//               strict beta=0 (0*C keeps NaN/Inf like ntensors.pas:2259)
+enum BetaMode { BETA_ZERO = 0, BETA_ONE = 1, BETA_SCALE = 2 };
+
+struct GemmArgs {
+  int64_t M, N, K;
+  float alpha, beta;
+  int beta_mode;
+  const float* A;
+  int64_t lda, strideA;
+  const float* B;
+  int64_t ldb, strideB;
+  float* C;
+  int64_t ldc, strideC;
+  int64_t batch;
+  // epilogue
+  int epi;
+  const float* bias;  // per row of C (filters)
+  int act;            // TActivationType ordinal
+};
+
+hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s);
+
+// ---- im2col / col2im -------------------------------------------------------
+struct ConvGeom {
+  int64_t C, H, W, kH, kW, padH, padW, sY, sX, dY, dX;
+  int64_t oh, ow;
+};
+int64_t out_dim(int64_t in, int64_t pad, int64_t k, int64_t dil, int64_t stride);
+hipError_t launch_im2col(const ConvGeom& g, const float* im, int64_t imStride, float* col,
+                         int64_t colStride, int64_t batch, hipStream_t s);
+hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride, float* im,
+                         int64_t imStride, int64_t batch, hipStream_t s);
+
+// ---- elementwise -------------------------------------------------------------
+bool act_supported(int act);
+hipError_t launch_forward_bias(float* dst, int64_t nFilters, int64_t blockSize,
+                               const float* bias, int64_t incb, int64_t batch, hipStream_t s);
+hipError_t launch_backward_bias(float* dst, int64_t nDst, const float* src, int64_t blockSize,
+                                int64_t batch, int64_t incb, hipStream_t s);
+hipError_t launch_activate(float* x, int64_t n, int act, hipStream_t s);
+hipError_t launch_bias_activate(float* dst, int64_t nFilters, int64_t blockSize,
+                                const float* bias, int64_t batch, int act, hipStream_t s);
+hipError_t launch_derive(const float* x, int64_t n, int act, float* delta, hipStream_t s);
+hipError_t launch_axpy(int64_t n, float a, const float* x, int64_t incx, float* y, int64_t incy,
+                       hipStream_t s);
+hipError_t launch_scale(int64_t n, float a, float* x, int64_t stride, hipStream_t s);
+hipError_t launch_fill(int64_t n, float* x, float v, int64_t stride, hipStream_t s);
+hipError_t launch_copy(int64_t n, const float* src, int64_t inca, float* dst, int64_t incb,
+                       hipStream_t s);
+hipError_t launch_clamp(int64_t n, float alpha, const float* src, float* dst, int64_t stride,
+                        hipStream_t s);
+
+}  // namespace tns

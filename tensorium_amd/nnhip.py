@@ -1,0 +1,170 @@
+"""TNNHip — the device-resident HIP backend, shaped like the reference's
+TNNCuda<T> (source/nncuda.pas:35-157) / TNNOpenCL<T> (nnopencl.pas:222-319).
+
+Method names, argument order and meaning follow TNNCuda: device buffers plus
+ELEMENT offsets, calls asynchronous on the backend's stream, ``finish()``
+synchronises.  Device buffers are torch CUDA tensors (fp32, contiguous) or raw
+integer device pointers; torch is only plumbing for memory and streams — all
+compute runs in libtensorium_hip.so.  Errors raise ``TnsError`` the way the
+reference's SAFE_CALL raises (nncuda.pas:216-275).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+from ._abi import TnsError, check, load
+
+try:  # torch is optional plumbing
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if torch is not None and isinstance(x, torch.Tensor):
+        if not x.is_cuda:
+            raise TnsError("TNNHip expects device (cuda) tensors")
+        if x.dtype != torch.float32:
+            raise TnsError(f"TNNHip expects float32 tensors, got {x.dtype}")
+        if not x.is_contiguous():
+            raise TnsError("TNNHip expects contiguous tensors")
+        return x.data_ptr()
+    raise TnsError(f"unsupported buffer type {type(x)!r}")
+
+
+class TNNHip:
+    """HIP twin of TNNCuda<single> (one context = one device + one stream)."""
+
+    def __init__(self, deviceIndex: int = 0, stream=None, use_torch_stream: bool = True):
+        self.lib = load()
+        h = C.c_void_p()
+        check(self.lib.tns_hip_create(int(deviceIndex), C.byref(h)))
+        self.ctx = h
+        self.device = int(deviceIndex)
+        if stream is not None:
+            check(self.lib.tns_hip_set_stream(self.ctx, C.c_void_p(int(stream))))
+        elif use_torch_stream and torch is not None and torch.cuda.is_available():
+            s = torch.cuda.current_stream(self.device).cuda_stream
+            check(self.lib.tns_hip_set_stream(self.ctx, C.c_void_p(s)))
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.tns_hip_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self) -> int:
+        return int(self.lib.tns_hip_get_stream(self.ctx) or 0)
+
+    def finish(self):  # TNNCuda.finish, nncuda.pas:1575
+        check(self.lib.tns_hip_finish(self.ctx))
+
+    def setTelemetry(self, on: bool):
+        check(self.lib.tns_hip_set_telemetry(self.ctx, 1 if on else 0))
+
+    def opMs(self, op: int) -> float:
+        return float(self.lib.tns_hip_op_ms(self.ctx, op))
+
+    # -- GEMM ----------------------------------------------------------------
+    def gemm(self, transA, transB, M, N, K, ALPHA, A, aOffset, lda, B, bOffset, ldb, BETA, C_,
+             cOffset, ldc):
+        check(self.lib.tns_hip_gemm(self.ctx, int(bool(transA)), int(bool(transB)), M, N, K,
+                                    float(ALPHA), _ptr(A), aOffset, lda, _ptr(B), bOffset, ldb,
+                                    float(BETA), _ptr(C_), cOffset, ldc))
+
+    def gemmStridedBatched(self, transA, transB, M, N, K, ALPHA, A, aOffset, lda, strideA, B,
+                           bOffset, ldb, strideB, BETA, C_, cOffset, ldc, strideC, batchCount):
+        check(self.lib.tns_hip_gemm_strided_batched(
+            self.ctx, int(bool(transA)), int(bool(transB)), M, N, K, float(ALPHA), _ptr(A),
+            aOffset, lda, strideA, _ptr(B), bOffset, ldb, strideB, float(BETA), _ptr(C_), cOffset,
+            ldc, strideC, batchCount))
+
+    # -- im2col / col2im --------------------------------------------------------
+    def im2col(self, aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+               strideY, strideX, dilationY, dilationX, im, imOffset, col, colOffset):
+        check(self.lib.tns_hip_im2col(self.ctx, aChannels, aHeight, aWidth, kernelHeight,
+                                      kernelWidth, padHeight, padWidth, strideY, strideX,
+                                      dilationY, dilationX, _ptr(im), imOffset, _ptr(col),
+                                      colOffset))
+
+    def im2colStridedBatched(self, aChannels, aHeight, aWidth, kernelHeight, kernelWidth,
+                             padHeight, padWidth, strideY, strideX, dilationY, dilationX, im,
+                             imStride, imOffset, col, colStride, colOffset, batchCount):
+        check(self.lib.tns_hip_im2col_strided_batched(
+            self.ctx, aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+            strideY, strideX, dilationY, dilationX, _ptr(im), imStride, imOffset, _ptr(col),
+            colStride, colOffset, batchCount))
+
+    def col2im(self, aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+               strideY, strideX, dilationY, dilationX, col, colOffset, im, imOffset):
+        check(self.lib.tns_hip_col2im(self.ctx, aChannels, aHeight, aWidth, kernelHeight,
+                                      kernelWidth, padHeight, padWidth, strideY, strideX,
+                                      dilationY, dilationX, _ptr(col), colOffset, _ptr(im),
+                                      imOffset))
+
+    def col2imStridedBatched(self, aChannels, aHeight, aWidth, kernelHeight, kernelWidth,
+                             padHeight, padWidth, strideY, strideX, dilationY, dilationX, col,
+                             colStride, colOffset, im, imStride, imOffset, batchCount):
+        check(self.lib.tns_hip_col2im_strided_batched(
+            self.ctx, aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
+            strideY, strideX, dilationY, dilationX, _ptr(col), colStride, colOffset, _ptr(im),
+            imStride, imOffset, batchCount))
+
+    # -- elementwise -------------------------------------------------------------
+    def forwardBias(self, dstSize, dst, offset, srcSize, src, incb, batch):
+        check(self.lib.tns_hip_forward_bias(self.ctx, dstSize, _ptr(dst), offset, srcSize,
+                                            _ptr(src), incb, batch))
+
+    def backwardBias(self, dstSize, dst, srcSize, src, srcOffset, incb, batch):
+        check(self.lib.tns_hip_backward_bias(self.ctx, dstSize, _ptr(dst), srcSize, _ptr(src),
+                                             srcOffset, incb, batch))
+
+    def ActivateArray(self, N, x, offset, activation):
+        check(self.lib.tns_hip_activate_array(self.ctx, N, _ptr(x), offset, int(activation)))
+
+    def DeriveArray(self, N, x, offset, activation, delta):
+        check(self.lib.tns_hip_derive_array(self.ctx, N, _ptr(x), offset, int(activation),
+                                            _ptr(delta)))
+
+    def axpy(self, N, a, x, xOffset, incx, y, yOffset, incy):
+        check(self.lib.tns_hip_axpy(self.ctx, N, float(a), _ptr(x), xOffset, incx, _ptr(y),
+                                    yOffset, incy))
+
+    def scale(self, N, a, x, stride):
+        check(self.lib.tns_hip_scale(self.ctx, N, float(a), _ptr(x), stride))
+
+    def fill(self, N, x, offset, val, stride):
+        check(self.lib.tns_hip_fill(self.ctx, N, _ptr(x), offset, float(val), stride))
+
+    def copy(self, N, src, srcOffset, inca, dst, dstOffset, incb):
+        check(self.lib.tns_hip_copy(self.ctx, N, _ptr(src), srcOffset, inca, _ptr(dst), dstOffset,
+                                    incb))
+
+    def clamp(self, N, alpha, src, dst, stride=1, offset=0):
+        check(self.lib.tns_hip_clamp(self.ctx, N, float(alpha), _ptr(src), _ptr(dst), stride,
+                                     offset))
+
+    # -- layer drivers ------------------------------------------------------------
+    def conv2d(self, batch, C_, H, W, input, weights, filters, kH, kW, wPadding, hPadding,
+               xStride, yStride, xDilation, yDilation, workspace, out):
+        check(self.lib.tns_hip_conv2d(self.ctx, batch, C_, H, W, _ptr(input), _ptr(weights),
+                                      filters, kH, kW, wPadding, hPadding, xStride, yStride,
+                                      xDilation, yDilation, _ptr(workspace), _ptr(out)))
+
+    def convForward(self, batch, C_, H, W, input, weights, biases, filters, kSize, stride,
+                    padding, dilation, activation, workspace, out, fused=True):
+        check(self.lib.tns_hip_conv_forward(self.ctx, batch, C_, H, W, _ptr(input),
+                                            _ptr(weights), _ptr(biases), filters, kSize, stride,
+                                            padding, dilation, int(activation), _ptr(workspace),
+                                            _ptr(out), 1 if fused else 0))

@@ -1,0 +1,64 @@
+"""Conv2D / conv-layer forward on the GPU vs the oracle (TTensor.Conv2D,
+ntensors.pas:8252-8349; TConvolutionalLayer.forward, nConvolutionLayer.pas:
+457-569).  Conv GEMMs are NN, so with bias add and leaky/linear/relu the whole
+layer is bit-exact; YOLOv3 layers are checked per layer (teacher forcing:
+each layer gets the oracle's input), batch 8 at full 416 resolution for a
+layer subset, all 75 layers at batch 1."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def conv_case(hip, torch, ora, batch, C, H, F, k, s, p, act, fused, seed=0):
+    x = ora.uniform(batch * C * H * H, 3, seed, 0.0, 1.0).reshape(batch, C, H, H)
+    sc = float(np.sqrt(2.0 / (k * k * C)))
+    w = ora.uniform(F * C * k * k, 30 + seed, seed, -sc, sc)
+    b = ora.uniform(F, 60 + seed, seed, -0.1, 0.1)
+    ref = ora.conv_forward(x, w, b, F, k, s, p, act)
+    dx, dw, db = (torch.from_numpy(t).cuda() for t in (x, w, b))
+    out = torch.full(ref.shape, float("nan"), device="cuda")
+    hip.convForward(batch, C, H, H, dx, dw, db, F, k, s, p, 1, act, None, out, fused=fused)
+    hip.finish()
+    return out.cpu().numpy(), ref
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("batch,C,H,F,k,s,p,act", [
+    (2, 3, 17, 8, 3, 1, 1, 9), (3, 5, 12, 7, 3, 2, 1, 9), (2, 16, 9, 5, 1, 1, 0, 4),
+    (1, 4, 20, 33, 3, 2, 1, 1), (2, 3, 13, 6, 5, 1, 2, 0)])
+def test_conv_forward_small(hip, torch_cuda, ora, fused, batch, C, H, F, k, s, p, act):
+    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, fused)
+    if act == 0:
+        assert np.allclose(got, ref, rtol=1e-5, atol=1e-6)
+    else:
+        assert np.array_equal(got, ref)
+
+
+def test_conv2d_driver_matches_oracle(hip, torch_cuda, ora):
+    batch, C, H, F, k, s, p = 2, 6, 15, 9, 3, 2, 1
+    x = ora.uniform(batch * C * H * H, 3, 77).reshape(batch, C, H, H)
+    w = ora.uniform(F * C * k * k, 4, 77, -0.2, 0.2)
+    ref = ora.conv2d(x, w, F, k, p, s)
+    dx, dw = torch_cuda.from_numpy(x).cuda(), torch_cuda.from_numpy(w).cuda()
+    out = torch_cuda.zeros(ref.shape, device="cuda")
+    hip.conv2d(batch, C, H, H, dx, dw, F, k, k, p, p, s, s, 1, 1, None, out)
+    hip.finish()
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
+def test_yolov3_all_layers_batch1_bit_exact(hip, torch_cuda, ora):
+    from tensorium_amd.yolo import yolov3_conv_table
+    for spec in yolov3_conv_table():
+        got, ref = conv_case(hip, torch_cuda, ora, 1, spec.c, spec.h, spec.filters, spec.size,
+                             spec.stride, spec.pad, spec.activation, True, seed=spec.index)
+        assert np.array_equal(got, ref), spec
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2, 11, 62, 74])
+def test_yolov3_layers_batch8_full_size(hip, torch_cuda, ora, idx):
+    from tensorium_amd.yolo import yolov3_conv_table
+    spec = yolov3_conv_table()[idx]
+    got, ref = conv_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,
+                         spec.stride, spec.pad, spec.activation, True, seed=spec.index)
+    assert np.array_equal(got, ref), spec

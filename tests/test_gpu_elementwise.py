@@ -1,0 +1,88 @@
+"""Bias / activation / BLAS-1 kernels vs the oracle.
+Bar: bias add, relu, leaky (x*0.1f), linear, hardtan: bit-exact;
+logistic / tanh (libm differences): |d| <= 1e-4*max(|ref|,1e-6) + 4 ulp."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+EXACT = [1, 4, 8, 9, 13]
+TRANSC = [0, 6]
+
+
+def close_transc(got, ref):
+    ulp = np.spacing(np.abs(ref).astype(np.float32))
+    return np.all(np.abs(got - ref) <= 1e-4 * np.maximum(np.abs(ref), 1e-6) + 4 * ulp)
+
+
+@pytest.mark.parametrize("act", EXACT + TRANSC)
+@pytest.mark.parametrize("n", [1, 7, 1024, 100003])
+def test_activate(hip, torch_cuda, ora, act, n):
+    x = ora.uniform(n, 8, act, -6.0, 6.0)
+    ref = ora.activate(x.copy(), act)
+    dx = torch_cuda.from_numpy(x).cuda()
+    hip.ActivateArray(n, dx, 0, act)
+    hip.finish()
+    got = dx.cpu().numpy()
+    if act in EXACT:
+        assert np.array_equal(got, ref)
+    else:
+        assert close_transc(got, ref)
+
+
+@pytest.mark.parametrize("act", EXACT + TRANSC)
+def test_derive(hip, torch_cuda, ora, act):
+    n = 5001
+    y = ora.activate(ora.uniform(n, 9, act, -3.0, 3.0), act)
+    delta = ora.uniform(n, 10, act)
+    ref = ora.gradient(y, act, delta.copy())
+    dy, dd = torch_cuda.from_numpy(y).cuda(), torch_cuda.from_numpy(delta.copy()).cuda()
+    hip.DeriveArray(n, dy, 0, act, dd)
+    hip.finish()
+    assert np.array_equal(dd.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("F,bs,batch", [(3, 5, 2), (64, 2704, 2), (255, 169, 1), (10, 1, 32),
+                                        (32, 173056, 1)])
+def test_forward_bias(hip, torch_cuda, ora, F, bs, batch):
+    x = ora.uniform(batch * F * bs, 11, F)
+    b = ora.uniform(F, 12, F, -0.1, 0.1)
+    ref = ora.add_bias(x.copy(), b, F, bs, batch)
+    dx, db = torch_cuda.from_numpy(x).cuda(), torch_cuda.from_numpy(b).cuda()
+    hip.forwardBias(x.size, dx, 0, F, db, 1, batch)
+    hip.finish()
+    assert np.array_equal(dx.cpu().numpy(), ref)
+
+
+def test_backward_bias_close(hip, torch_cuda, ora):
+    F, bs, batch = 16, 333, 4
+    src = ora.uniform(batch * F * bs, 13, 0)
+    dst = ora.uniform(F, 14, 0)
+    ref = dst.astype(np.float64) + src.reshape(batch, F, bs).astype(np.float64).sum(axis=(0, 2))
+    dsrc, ddst = torch_cuda.from_numpy(src).cuda(), torch_cuda.from_numpy(dst.copy()).cuda()
+    hip.backwardBias(F, ddst, src.size, dsrc, 0, 1, batch)
+    hip.finish()
+    scale = np.abs(src.reshape(batch, F, bs)).sum(axis=(0, 2)) + np.abs(dst)
+    assert np.all(np.abs(ddst.cpu().numpy() - ref) <= 1e-5 * scale)
+
+
+def test_blas1(hip, torch_cuda, ora):
+    n = 10007
+    x = ora.uniform(n, 15, 0)
+    y = ora.uniform(n, 16, 0)
+    dx, dy = torch_cuda.from_numpy(x).cuda(), torch_cuda.from_numpy(y.copy()).cuda()
+    hip.axpy(n, 0.37, dx, 0, 1, dy, 0, 1)
+    hip.finish()
+    ref = y.copy()
+    ora.lib().ora_saxpy(n, 0.37, x.ctypes.data, ref.ctypes.data)
+    assert np.array_equal(dy.cpu().numpy(), ref)
+    hip.scale(n, 2.5, dy, 1)
+    hip.finish()
+    assert np.array_equal(dy.cpu().numpy(), (ref * np.float32(2.5)).astype(np.float32))
+    hip.fill(n, dy, 0, 3.0, 1)
+    hip.clamp(n, 1.0, dx, dx, 1, 0)
+    hip.copy(n // 2, dx, 0, 2, dy, 0, 1)
+    hip.finish()
+    got = dy.cpu().numpy()
+    assert np.array_equal(got[: n // 2], np.clip(x, -1, 1)[0:2 * (n // 2):2])
+    assert np.all(got[n // 2:] == 3.0)

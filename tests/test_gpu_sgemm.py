@@ -1,0 +1,184 @@
+"""SGEMM parity on the GPU (boundary B device API and boundary A host API)
+against the oracle (restated cblas_sgemm, ntensors.pas:2231-2304).
+
+Bar:
+  * NN and TN: bit-identical to the reference's ascending-k FMA chain
+    (gfx950 f32 MFMA is an exact k-ordered fmaf chain).
+  * NT and TT: componentwise |C - C_ref| <= 1e-4 * (|alpha||A||B| + |beta||C0|)_ij
+    (the reference sums NT in 8 sdot lanes and TT with unfused mul+add).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def bound(ta, tb, A, B, alpha, beta, C0):
+    a = A.T if ta else A
+    b = B.T if tb else B
+    return abs(alpha) * (np.abs(a.astype(np.float64)) @ np.abs(b.astype(np.float64))) + \
+        abs(beta) * np.abs(C0.astype(np.float64))
+
+
+def run_dev(hip, torch, ta, tb, A, B, C0, alpha, beta):
+    M, N = C0.shape
+    K = A.shape[0] if ta else A.shape[1]
+    dA, dB, dC = (torch.from_numpy(x).cuda() for x in (A, B, C0.copy()))
+    hip.gemm(ta, tb, M, N, K, alpha, dA, 0, A.shape[1], dB, 0, B.shape[1], beta, dC, 0, N)
+    hip.finish()
+    return dC.cpu().numpy()
+
+
+def run_ref(ora, ta, tb, A, B, C0, alpha, beta):
+    M, N = C0.shape
+    K = A.shape[0] if ta else A.shape[1]
+    C = C0.copy()
+    ora.sgemm(bool(ta), bool(tb), M, N, K, alpha, A, A.shape[1], B, B.shape[1], beta, C, N)
+    return C
+
+
+def operands(rng, ta, tb, M, N, K):
+    A = rng.uniform(-1, 1, (K, M) if ta else (M, K)).astype(np.float32)
+    B = rng.uniform(-1, 1, (N, K) if tb else (K, N)).astype(np.float32)
+    C0 = rng.uniform(-1, 1, (M, N)).astype(np.float32)
+    return A, B, C0
+
+
+SHAPES = [(1, 1, 1), (5, 7, 13), (37, 53, 61), (128, 128, 32), (129, 130, 33), (256, 256, 256),
+          (32, 1000, 27), (255, 2704 // 4, 256), (1, 513, 300), (300, 1, 64), (64, 64, 1),
+          (200, 72, 0)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("ta,tb", [(0, 0), (1, 0)])
+def test_nn_tn_bit_exact(hip, torch_cuda, ora, M, N, K, ta, tb):
+    rng = np.random.default_rng(M * 7919 + N * 31 + K)
+    A, B, C0 = operands(rng, ta, tb, M, N, K)
+    for alpha, beta in [(1.0, 0.0), (0.5, 2.0), (1.0, 1.0), (-1.5, 0.25)]:
+        got = run_dev(hip, torch_cuda, ta, tb, A, B, C0, alpha, beta)
+        ref = run_ref(ora, ta, tb, A, B, C0, alpha, beta)
+        assert np.array_equal(got, ref), (M, N, K, alpha, beta,
+                                          float(np.abs(got - ref).max()))
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("ta,tb", [(0, 1), (1, 1), (0, 0), (1, 0)])
+def test_all_transposes_within_bound(hip, torch_cuda, ora, M, N, K, ta, tb):
+    rng = np.random.default_rng(M * 131 + N * 17 + K + 5)
+    A, B, C0 = operands(rng, ta, tb, M, N, K)
+    for alpha, beta in [(1.0, 0.0), (0.5, 2.0)]:
+        got = run_dev(hip, torch_cuda, ta, tb, A, B, C0, alpha, beta)
+        ref = run_ref(ora, ta, tb, A, B, C0, alpha, beta)
+        bnd = bound(ta, tb, A, B, alpha, beta, C0)
+        err = np.abs(got.astype(np.float64) - ref)
+        assert np.all(err <= TOL * bnd + 1e-30), float((err / (bnd + 1e-30)).max())
+
+
+def test_unaligned_leading_dims_and_offsets(hip, torch_cuda, ora):
+    # lda/ldb/ldc larger than the logical width, element offsets into buffers
+    rng = np.random.default_rng(1)
+    M, N, K, lda, ldb, ldc, off = 45, 70, 33, 37, 75, 73, 3
+    A = rng.uniform(-1, 1, off + M * lda).astype(np.float32)
+    B = rng.uniform(-1, 1, off + K * ldb).astype(np.float32)
+    C = rng.uniform(-1, 1, off + M * ldc).astype(np.float32)
+    dA, dB, dC = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B, C))
+    hip.gemm(False, False, M, N, K, 1.0, dA, off, lda, dB, off, ldb, 0.5, dC, off, ldc)
+    hip.finish()
+    ref = C.copy()
+    ora.sgemm(False, False, M, N, K, 1.0, A[off:], lda, B[off:], ldb, 0.5, ref[off:], ldc)
+    assert np.array_equal(dC.cpu().numpy(), ref)
+
+
+def test_strided_batched_shared_a(hip, torch_cuda, ora):
+    # conv-style: strideA = 0 (weights shared), nConvolutionLayer.pas:1078
+    rng = np.random.default_rng(2)
+    batch, M, N, K = 5, 64, 300, 75
+    A = rng.uniform(-1, 1, (M, K)).astype(np.float32)
+    B = rng.uniform(-1, 1, (batch, K, N)).astype(np.float32)
+    C = np.zeros((batch, M, N), np.float32)
+    dA, dB, dC = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B, C))
+    hip.gemmStridedBatched(False, False, M, N, K, 1.0, dA, 0, K, 0, dB, 0, N, K * N, 0.0, dC, 0,
+                           N, M * N, batch)
+    hip.finish()
+    ref = C.copy()
+    ora.sgemm_batch_strided(False, False, M, N, K, 1.0, A, K, 0, B, N, K * N, 0.0, ref, N, M * N,
+                            batch)
+    assert np.array_equal(dC.cpu().numpy(), ref)
+
+
+def test_beta0_strict_propagates_nan(hip, torch_cuda, hiplib):
+    A = np.ones((4, 4), np.float32)
+    C = np.zeros((4, 4), np.float32)
+    C[1, 2] = np.nan
+    C[3, 0] = np.inf
+    dA, dB, dC = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, A, C))
+    hip.gemm(False, False, 4, 4, 4, 1.0, dA, 0, 4, dB, 0, 4, 0.0, dC, 0, 4)
+    hip.finish()
+    out = dC.cpu().numpy()
+    assert np.isnan(out[1, 2]) and np.isnan(out[3, 0]) and out[0, 0] == 4.0
+    # BLAS convention when strict mode is off: C not read
+    hiplib.tns_set_option(0, 0)
+    try:
+        dC = torch_cuda.from_numpy(C.copy()).cuda()
+        hip.gemm(False, False, 4, 4, 4, 1.0, dA, 0, 4, dB, 0, 4, 0.0, dC, 0, 4)
+        hip.finish()
+        assert np.all(dC.cpu().numpy() == 4.0)
+    finally:
+        hiplib.tns_set_option(0, 1)
+
+
+def test_host_api_matmul_accumulates(hiplib, torch_cuda, ora):
+    # boundary A: TSingleTensor.matMul via the op-table drop-in (beta = One)
+    from tensorium_amd.ntensors import matMul
+    rng = np.random.default_rng(3)
+    a = rng.uniform(-1, 1, (256, 256)).astype(np.float32)
+    b = rng.uniform(-1, 1, (256, 256)).astype(np.float32)
+    c = rng.uniform(-1, 1, (256, 256)).astype(np.float32)
+    ref = c.copy()
+    ora.sgemm(False, False, 256, 256, 256, 1.0, a, 256, b, 256, 1.0, ref, 256)
+    got = matMul(a, b, c.copy())
+    assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("ta,tb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_host_api_all_transposes(hiplib, torch_cuda, ora, ta, tb):
+    from tensorium_amd.ntensors import bind_hip_op_table
+    ops = bind_hip_op_table()
+    rng = np.random.default_rng(4 + ta * 2 + tb)
+    M, N, K = 70, 90, 110
+    A, B, C0 = operands(rng, ta, tb, M, N, K)
+    C = C0.copy()
+    ops.gemm(101, 112 if ta else 111, 112 if tb else 111, M, N, K, 0.5, A.ctypes.data,
+             A.shape[1], B.ctypes.data, B.shape[1], 2.0, C.ctypes.data, N)
+    assert hiplib.tns_last_error() == b""
+    ref = run_ref(ora, ta, tb, A, B, C0, 0.5, 2.0)
+    if (ta, tb) in [(0, 0), (1, 0)]:
+        assert np.array_equal(C, ref)
+    else:
+        bnd = bound(ta, tb, A, B, 0.5, 2.0, C0)
+        assert np.all(np.abs(C.astype(np.float64) - ref) <= TOL * bnd)
+
+
+def test_4096_cubed_sampled_rows_bit_exact(hip, torch_cuda, ora):
+    """Full BASELINE size: GPU 4096^3 against the oracle on 24 sampled rows
+    (the oracle restricted to those rows computes the identical chains)."""
+    n = 4096
+    A = ora.uniform(n * n, 2, 0).reshape(n, n)
+    B = ora.uniform(n * n, 2, 1).reshape(n, n)
+    dA, dB = torch_cuda.from_numpy(A).cuda(), torch_cuda.from_numpy(B).cuda()
+    dC = torch_cuda.zeros((n, n), device="cuda")
+    hip.gemm(False, False, n, n, n, 1.0, dA, 0, n, dB, 0, n, 0.0, dC, 0, n)
+    hip.finish()
+    got = dC.cpu().numpy()
+    rows = [0, 1, 127, 128, 129, 1000, 2047, 2048, 3071, 4095] + list(range(600, 614))
+    ref = np.zeros((n, n), np.float32)
+    for r in rows:
+        ora.sgemm_rows(False, False, r, r + 1, n, n, n, 1.0, A, n, B, n, 0.0, ref, n)
+        assert np.array_equal(got[r], ref[r]), r
+    # size-independent property: checksum linearity  1^T (A B) = (1^T A) B
+    lhs = got.astype(np.float64).sum(axis=0)
+    rhs = A.astype(np.float64).sum(axis=0) @ B.astype(np.float64)
+    scale = np.abs(A).astype(np.float64).sum(axis=0) @ np.abs(B).astype(np.float64)
+    assert np.all(np.abs(lhs - rhs) <= 1e-4 * scale)
