@@ -257,6 +257,18 @@ enum { TNS_OP_GEMM = 0, TNS_OP_IM2COL = 1, TNS_OP_COL2IM = 2, TNS_OP_BIAS = 3,
        TNS_OP_ACTIVATE = 4, TNS_OP_COUNT = 5 };
 
 /* ---- tuning / options -------------------------------------------------- */
+/* SGEMM tile-shape variants (the production path picks one per problem;
+ * these force one, for sweeps).  variant < 0 = heuristic.  Some shapes are
+ * NN-with-aligned-operands only and return TNS_ERR_UNSUPPORTED otherwise. */
+int         tns_gemm_variant_count(void);
+const char* tns_gemm_variant_name(int32_t variant);
+int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t transB,
+                         int64_t M, int64_t N, int64_t K, float ALPHA,
+                         const float* A, int64_t aOffset, int64_t lda, int64_t strideA,
+                         const float* B, int64_t bOffset, int64_t ldb, int64_t strideB,
+                         float BETA, float* C, int64_t cOffset, int64_t ldc, int64_t strideC,
+                         int64_t batchCount);
+
 /* TNS_OPT_STRICT_BETA0 (default 1): beta==0 computes 0*C like the reference
  * (NaN/Inf in C propagate).  0 = BLAS convention (C not read). */
 enum { TNS_OPT_STRICT_BETA0 = 0 };

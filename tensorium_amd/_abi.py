@@ -82,6 +82,10 @@ PROTOTYPES: dict[str, tuple] = {
     "tns_hip_conv_forward": (C.c_int, [vp, i64, i64, i64, i64, fptr, fptr, fptr, i64, i64, i64,
                                        i64, i64, i32, fptr, fptr, i32]),
     "tns_hip_set_telemetry": (C.c_int, [vp, i32]),
+    "tns_gemm_variant_count": (C.c_int, []),
+    "tns_gemm_variant_name": (C.c_char_p, [i32]),
+    "tns_hip_gemm_variant": (C.c_int, [vp, i32, u8, u8, i64, i64, i64, f32, fptr, i64, i64, i64,
+                                       fptr, i64, i64, i64, f32, fptr, i64, i64, i64, i64]),
     "tns_hip_op_ms": (C.c_double, [vp, i32]),
 }
 

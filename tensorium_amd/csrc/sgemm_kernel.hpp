@@ -1,0 +1,375 @@
+// sgemm_kernel.hpp — fp32 SGEMM on gfx950 fp32 MFMA (v_mfma_f32_32x32x2_f32).
+//
+// Replaces the reference's GEMM backends for TTensor<Single>.gemm /
+// gemmStridedBatched (cblas_sgemm, ntensors.pas:2231-2304; TNNCuda.gemm,
+// nncuda.pas:624-725; cl_las TXgemm, cl_las.pas:483-640).
+//
+// Numerics (why NN/TN are bit-identical to the reference CPU path):
+//   The reference computes every C element as an ascending-k FMA chain
+//   starting from beta*C:  c = fma(alpha*A[i,k], B[k,j], c)   (saxpy_avx2
+//   vfmadd231, s_nn/s_tn ntensors.pas:2007-2133).  gfx950's f32 MFMA is
+//   bit-for-bit a k-ordered fmaf chain (D = fma(a_k1,b_k1, fma(a_k0,b_k0,C))).
+//   Every kernel here feeds each accumulator k in ascending order (k-tiles
+//   ascending, MFMA steps ascending, lane-half 0 = the lower k of a step),
+//   pre-multiplies A by alpha once (the reference's A_PART) and starts the
+//   accumulator at beta*C (the reference's mulvs pre-scale).  No split-K.
+//   NT/TT use a different order in the reference (8-lane sdot / unfused
+//   mul+add) and agree within the componentwise bound documented in DESIGN.md.
+//
+// Structure (one template, several tile shapes picked per problem):
+//   block tile BM x BN, k-tile BK, WM x WN waves, each wave owning
+//   (BM/WM) x (BN/WN) as a grid of 32x32 MFMA accumulators.  Operands are
+//   staged global -> registers (float4 where the layout allows) -> LDS in
+//   k-major [k][m] / [k][n] images, double-buffered with one barrier per
+//   k-tile; the next tile's global loads are issued before the current
+//   tile's MFMAs and written to LDS after them.  The block index is remapped
+//   so each of the 8 XCDs sweeps a contiguous, grouped region of C.
+#pragma once
+#include "tns_act.hpp"
+#include "tns_internal.hpp"
+
+namespace tns {
+namespace sgemm_detail {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int GROUP_M = 8;
+
+// LDS row length of a k-major operand image.  K-contiguous operands are
+// transposed on the way in (scalar ds_writes); a row length ≡ 1 (mod 32)
+// makes those writes conflict-free.  MN-contiguous operands are written with
+// ds_write_b128 and keep the plain length.
+template <bool KCONTIG, int BMN>
+struct LdsLd {
+  static constexpr int value = KCONTIG ? BMN + 1 : BMN;
+};
+
+// Loads one BK x BMN operand tile (k, mn) into E registers per thread.
+//   KCONTIG:  element (k, mn) at base[(mn0+mn)*ld + k0+k]   (A NoTrans / B Trans)
+//   else   :  element (k, mn) at base[(k0+k)*ld + mn0+mn]   (A Trans / B NoTrans)
+// Out-of-range elements read as 0.  Branch-free: an out-of-range load is
+// redirected to element 0 of the operand and its value replaced by 0.  VEC=4
+// is only instantiated when the contiguous extent is a multiple of 4 (the
+// host checks), so a float4 is either wholly inside or wholly outside.
+template <bool KCONTIG, int VEC, int BK, int BMN, int NT>
+struct TileIO {
+  static constexpr int E = BK * BMN / NT;
+  static_assert(E % VEC == 0, "tile not divisible");
+  static constexpr int LD = LdsLd<KCONTIG, BMN>::value;
+
+  __device__ static __forceinline__ void load(float (&r)[E], const float* __restrict__ base,
+                                              int64_t ld, int64_t mn0, int64_t k0, int64_t MN,
+                                              int64_t K, int tid) {
+#pragma unroll
+    for (int it = 0; it < E / VEC; ++it) {
+      const int idx = tid + NT * it;
+      int64_t gk, gmn;
+      if constexpr (KCONTIG) {
+        gk = k0 + VEC * (idx % (BK / VEC));
+        gmn = mn0 + idx / (BK / VEC);
+      } else {
+        gk = k0 + idx / (BMN / VEC);
+        gmn = mn0 + VEC * (idx % (BMN / VEC));
+      }
+      const bool ok = (gmn < MN) && (gk < K);
+      const int64_t off = ok ? (KCONTIG ? gmn * ld + gk : gk * ld + gmn) : 0;
+      if constexpr (VEC == 4) {
+        float4 v = *reinterpret_cast<const float4*>(base + off);
+        r[4 * it + 0] = ok ? v.x : 0.0f;
+        r[4 * it + 1] = ok ? v.y : 0.0f;
+        r[4 * it + 2] = ok ? v.z : 0.0f;
+        r[4 * it + 3] = ok ? v.w : 0.0f;
+      } else {
+        const float v = base[off];
+        r[it] = ok ? v : 0.0f;
+      }
+    }
+  }
+
+  __device__ static __forceinline__ void store(const float (&r)[E], float* __restrict__ xs,
+                                               int tid) {
+    if constexpr (VEC == 4) {
+#pragma unroll
+      for (int it = 0; it < E / 4; ++it) {
+        const int idx = tid + NT * it;
+        if constexpr (KCONTIG) {
+          const int kq = idx % (BK / 4), mn = idx / (BK / 4);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) xs[(4 * kq + c) * LD + mn] = r[4 * it + c];
+        } else {
+          const int mq = idx % (BMN / 4), k = idx / (BMN / 4);
+          *reinterpret_cast<float4*>(xs + k * LD + 4 * mq) =
+              make_float4(r[4 * it], r[4 * it + 1], r[4 * it + 2], r[4 * it + 3]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < E; ++it) {
+        const int idx = tid + NT * it;
+        if constexpr (KCONTIG) {
+          xs[(idx % BK) * LD + idx / BK] = r[it];
+        } else {
+          xs[(idx / BMN) * LD + idx % BMN] = r[it];
+        }
+      }
+    }
+  }
+};
+
+// XCD-aware, grouped mapping of a linear block id onto (tile_m, tile_n).
+__device__ __forceinline__ void map_tile(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int nb = tiles_m * tiles_n;
+  // blocks b and b+8 are dispatched to the same XCD: give each XCD a
+  // contiguous range of the logical order (bijective for any nb).
+  const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  // grouped raster: GROUP_M tile rows swept column by column.
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wg / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wg - group * per_group;
+  tm = first_m + in_group % gsize;
+  tn = in_group / gsize;
+}
+
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int MINW_>
+struct Shape {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_, MINW = MINW_;
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int WTM = BM / WM, WTN = BN / WN;
+  static constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "bad wave tile");
+};
+
+// MFMA steps [S0, S1) of one k-tile: step s consumes k = 2s (lanes 0-31) and
+// 2s+1 (lanes 32-63) — ascending k per accumulator.
+template <int TM, int TN, int LDA_S, int LDB_S, int S0, int S1>
+__device__ __forceinline__ void mma_steps(floatx16 (&acc)[TM][TN], const float* ap,
+                                          const float* bp) {
+#pragma unroll
+  for (int s = S0; s < S1; ++s) {
+    float a[TM], b[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) a[i] = ap[2 * s * LDA_S + 32 * i];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) b[j] = bp[2 * s * LDB_S + 32 * j];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <class S, bool TA, bool TB, int AV, int BV>
+__global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) {
+  constexpr int BM = S::BM, BN = S::BN, BK = S::BK, NT = S::NT;
+  constexpr int TM = S::TM, TN = S::TN, WTM = S::WTM, WTN = S::WTN;
+  constexpr bool AKC = !TA;  // A is k-contiguous in memory
+  constexpr bool BKC = TB;   // B is k-contiguous in memory
+  using AIO = TileIO<AKC, AV, BK, BM, NT>;
+  using BIO = TileIO<BKC, BV, BK, BN, NT>;
+  constexpr int LDA_S = AIO::LD, LDB_S = BIO::LD;
+  constexpr int A_TILE = BK * LDA_S;
+  constexpr int B_TILE = BK * LDB_S;
+  constexpr int STAGE = A_TILE + B_TILE;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int l31 = lane & 31;
+  const int h = lane >> 5;
+  const int wid = tid >> 6;
+  const int wm = wid / S::WN, wn = wid % S::WN;
+
+  const int tiles_m = (int)((p.M + BM - 1) / BM);
+  const int tiles_n = (int)((p.N + BN - 1) / BN);
+  int tm_, tn_;
+  map_tile(blockIdx.x, tiles_m, tiles_n, tm_, tn_);
+  const int64_t m0 = (int64_t)tm_ * BM, n0 = (int64_t)tn_ * BN;
+  const int64_t bz = blockIdx.y;
+
+  const float* __restrict__ A = p.A + bz * p.strideA;
+  const float* __restrict__ B = p.B + bz * p.strideB;
+  float* __restrict__ C = p.C + bz * p.strideC;
+  const int64_t M = p.M, N = p.N, K = p.K;
+
+  // ---- accumulator init: 0, C, or beta*C (reference mulvs pre-scale) -----
+  floatx16 acc[TM][TN];
+  const int64_t row_base = m0 + wm * WTM + 4 * h;
+  const int64_t col_base = n0 + wn * WTN + l31;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+  if (p.beta_mode != BETA_ZERO) {
+    const bool scale = p.beta_mode == BETA_SCALE;
+    const float beta = p.beta;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int64_t row = row_base + i * 32 + (e & 3) + 8 * (e >> 2);
+          const int64_t col = col_base + j * 32;
+          const bool ok = row < M && col < N;
+          float v = C[ok ? row * p.ldc + col : 0];
+          v = scale ? beta * v : v;
+          acc[i][j][e] = ok ? v : 0.0f;
+        }
+  }
+
+  const int nt = (int)((K + BK - 1) / BK);
+  const bool scale_a = p.alpha != 1.0f;
+  const float alpha = p.alpha;
+  float ra[AIO::E], rb[BIO::E];
+  const int a_off = h * LDA_S + wm * WTM + l31;
+  const int b_off = h * LDB_S + wn * WTN + l31;
+
+  if (nt > 0) {
+    AIO::load(ra, A, p.lda, m0, 0, M, K, tid);
+    BIO::load(rb, B, p.ldb, n0, 0, N, K, tid);
+    if (scale_a) {
+#pragma unroll
+      for (int i = 0; i < AIO::E; ++i) ra[i] = alpha * ra[i];  // A_PART = ALPHA*A[kk]
+    }
+    AIO::store(ra, smem, tid);
+    BIO::store(rb, smem + A_TILE, tid);
+    __syncthreads();
+
+    for (int t = 0; t < nt - 1; ++t) {
+      const float* as = smem + (t & 1) * STAGE;
+      float* nxt = smem + ((t + 1) & 1) * STAGE;
+      const int64_t k0 = (int64_t)(t + 1) * BK;
+      // next tile's global loads first: their latency hides under the MFMAs
+      AIO::load(ra, A, p.lda, m0, k0, M, K, tid);
+      BIO::load(rb, B, p.ldb, n0, k0, N, K, tid);
+      mma_steps<TM, TN, LDA_S, LDB_S, 0, BK / 4>(acc, as + a_off, as + A_TILE + b_off);
+      // the other buffer was last read before the previous barrier: safe to
+      // fill it mid-tile, between two halves of this tile's MFMAs
+      if (scale_a) {
+#pragma unroll
+        for (int i = 0; i < AIO::E; ++i) ra[i] = alpha * ra[i];
+      }
+      AIO::store(ra, nxt, tid);
+      BIO::store(rb, nxt + A_TILE, tid);
+      mma_steps<TM, TN, LDA_S, LDB_S, BK / 4, BK / 2>(acc, as + a_off, as + A_TILE + b_off);
+      __syncthreads();
+    }
+    const float* as = smem + ((nt - 1) & 1) * STAGE;
+    mma_steps<TM, TN, LDA_S, LDB_S, 0, BK / 2>(acc, as + a_off, as + A_TILE + b_off);
+  }
+
+  // ---- epilogue ----------------------------------------------------------
+  const bool fuse = p.epi == EPI_BIAS_ACT;
+  const int act = p.act;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int64_t row = row_base + i * 32 + (e & 3) + 8 * (e >> 2);
+      if (row >= M) continue;
+      const float bias = fuse ? p.bias[row] : 0.0f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int64_t col = col_base + j * 32;
+        if (col >= N) continue;
+        float v = acc[i][j][e];
+        if (fuse) v = act_apply(v + bias, act);  // forwardBias then activate
+        C[row * p.ldc + col] = v;
+      }
+    }
+}
+template <class S, bool TA, bool TB, int AV, int BV>
+hipError_t launch_variant(const GemmArgs& a, hipStream_t s) {
+  const int64_t tiles = ((a.M + S::BM - 1) / S::BM) * ((a.N + S::BN - 1) / S::BN);
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  for (int64_t b0 = 0; b0 < a.batch; b0 += 65535) {
+    GemmArgs sub = a;
+    const int64_t nb = a.batch - b0 < 65535 ? a.batch - b0 : 65535;
+    sub.A = a.A + b0 * a.strideA;
+    sub.B = a.B + b0 * a.strideB;
+    sub.C = a.C + b0 * a.strideC;
+    sub.batch = nb;
+    hipLaunchKernelGGL((sgemm_mfma_kernel<S, TA, TB, AV, BV>), dim3((unsigned)tiles, (unsigned)nb),
+                       dim3(S::NT), 0, s, sub);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// all transposes x all vector widths
+template <class S>
+hipError_t launch_full(const GemmArgs& a, bool ta, bool tb, bool av, bool bv, hipStream_t s) {
+#define TNS_VEC(TA, TB)                                               \
+  do {                                                                \
+    if (av && bv) return launch_variant<S, TA, TB, 4, 4>(a, s);       \
+    if (av) return launch_variant<S, TA, TB, 4, 1>(a, s);             \
+    if (bv) return launch_variant<S, TA, TB, 1, 4>(a, s);             \
+    return launch_variant<S, TA, TB, 1, 1>(a, s);                     \
+  } while (0)
+  if (!ta && !tb) TNS_VEC(false, false);
+  if (!ta && tb) TNS_VEC(false, true);
+  if (ta && !tb) TNS_VEC(true, false);
+  TNS_VEC(true, true);
+#undef TNS_VEC
+}
+
+// all transposes, float4 operands only (large-GEMM production shape)
+template <class S>
+hipError_t launch_trans4(const GemmArgs& a, bool ta, bool tb, bool av, bool bv, hipStream_t s) {
+  if (!av || !bv) return hipErrorInvalidValue;
+  if (!ta && !tb) return launch_variant<S, false, false, 4, 4>(a, s);
+  if (!ta && tb) return launch_variant<S, false, true, 4, 4>(a, s);
+  if (ta && !tb) return launch_variant<S, true, false, 4, 4>(a, s);
+  return launch_variant<S, true, true, 4, 4>(a, s);
+}
+
+// experimental tile shapes: NN with float4 operands only
+template <class S>
+hipError_t launch_nn4(const GemmArgs& a, bool ta, bool tb, bool av, bool bv, hipStream_t s) {
+  if (ta || tb || !av || !bv) return hipErrorInvalidValue;
+  return launch_variant<S, false, false, 4, 4>(a, s);
+}
+
+//                 BM   BN  BK WM WN MINW
+using S128x128 = Shape<128, 128, 32, 2, 2, 2>;
+using S128x64 = Shape<128, 64, 32, 2, 2, 2>;
+using S64x128 = Shape<64, 128, 32, 2, 2, 2>;
+using S64x256 = Shape<64, 256, 32, 1, 4, 2>;
+using S32x256 = Shape<32, 256, 32, 1, 4, 2>;
+using S256x256 = Shape<256, 256, 32, 2, 2, 1>;
+using S256x256k16 = Shape<256, 256, 16, 2, 2, 1>;
+using S256x128 = Shape<256, 128, 32, 2, 2, 1>;
+using S128x256 = Shape<128, 256, 32, 2, 2, 1>;
+using S256x256w8 = Shape<256, 256, 32, 2, 4, 2>;
+using S256x128k16 = Shape<256, 128, 16, 2, 2, 2>;
+
+}  // namespace sgemm_detail
+
+// one launcher per shape, defined in the sgemm_*.hip translation units
+typedef hipError_t (*ShapeLauncher)(const GemmArgs&, bool, bool, bool, bool, hipStream_t);
+#define TNS_SHAPES(X)                                    \
+  X(128x128, "128x128x32_w2x2", 128, 128, launch_full)   \
+  X(128x64, "128x64x32_w2x2", 128, 64, launch_full)      \
+  X(64x128, "64x128x32_w2x2", 64, 128, launch_full)      \
+  X(64x256, "64x256x32_w1x4", 64, 256, launch_full)      \
+  X(32x256, "32x256x32_w1x4", 32, 256, launch_full)      \
+  X(256x256w8, "256x256x32_w2x4", 256, 256, launch_trans4) \
+  X(256x256, "256x256x32_w2x2", 256, 256, launch_nn4)    \
+  X(256x256k16, "256x256x16_w2x2", 256, 256, launch_nn4) \
+  X(256x128, "256x128x32_w2x2", 256, 128, launch_nn4)    \
+  X(128x256, "128x256x32_w2x2", 128, 256, launch_nn4)    \
+  X(256x128k16, "256x128x16_w2x2", 256, 128, launch_nn4)
+
+#define TNS_DECL(ID, NAME, BMv, BNv, KIND) \
+  hipError_t launch_shape_##ID(const GemmArgs&, bool, bool, bool, bool, hipStream_t);
+TNS_SHAPES(TNS_DECL)
+#undef TNS_DECL
+
+}  // namespace tns

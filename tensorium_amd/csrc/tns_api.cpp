@@ -113,7 +113,7 @@ int beta_mode_for(float beta) {
 int do_gemm(tns_ctx* c, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float alpha,
             const float* A, int64_t lda, int64_t sA, const float* B, int64_t ldb, int64_t sB,
             float beta, float* C, int64_t ldc, int64_t sC, int64_t batch, int epi,
-            const float* bias, int act) {
+            const float* bias, int act, bool c_write_only = false, int variant = -1) {
   if (M < 0 || N < 0 || K < 0 || batch < 0)
     return set_error(TNS_ERR_ARG, "gemm: negative dimension");
   if (M == 0 || N == 0 || batch == 0) return TNS_OK;
@@ -128,13 +128,18 @@ int do_gemm(tns_ctx* c, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float
     return set_error(TNS_ERR_ARG, "gemm: bad fused epilogue");
   GemmArgs a;
   a.M = M; a.N = N; a.K = K;
-  a.alpha = alpha; a.beta = beta; a.beta_mode = beta_mode_for(beta);
+  a.alpha = alpha; a.beta = beta;
+  a.beta_mode = (c_write_only && beta == 0.0f) ? BETA_ZERO : beta_mode_for(beta);
   a.A = A; a.lda = lda; a.strideA = sA;
   a.B = B; a.ldb = ldb; a.strideB = sB;
   a.C = C; a.ldc = ldc; a.strideC = sC;
   a.batch = batch; a.epi = epi; a.bias = bias; a.act = act;
   OpTimer t(c, TNS_OP_GEMM);
-  return hip_status(launch_sgemm(a, ta, tb, c->stream), "sgemm launch");
+  hipError_t e = launch_sgemm_variant(variant, a, ta, tb, c->stream);
+  if (e == hipErrorInvalidValue && variant >= 0)
+    return set_error(TNS_ERR_UNSUPPORTED, "gemm variant %d (%s) does not support this problem",
+                     variant, sgemm_variant_name(variant));
+  return hip_status(e, "sgemm launch");
 }
 
 ConvGeom geom(int64_t C, int64_t H, int64_t W, int64_t kH, int64_t kW, int64_t pH, int64_t pW,
@@ -472,8 +477,11 @@ int tns_hip_conv2d(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
   }
   // one strided-batched launch with the weights shared (strideA = 0) — the
   // GPU path of nConvolutionLayer.pas:1078; beta = 0 as in Conv2D (8328)
+  // The layer output is write-only here: beta = 0 does not read it (for any
+  // finite previous contents this equals the reference's 0*C up to the sign
+  // of an all-zero chain).
   return do_gemm(c, false, false, filters, outImg, k, 1.0f, weights, k, 0, Bp, outImg, strideB,
-                 0.0f, out, outImg, outImg * filters, batch, EPI_NONE, nullptr, 0);
+                 0.0f, out, outImg, outImg * filters, batch, EPI_NONE, nullptr, 0, true);
 }
 
 int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
@@ -519,7 +527,25 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
   }
   // conv GEMM with forwardBias + activate fused into the epilogue
   return do_gemm(c, false, false, filters, outImg, k, 1.0f, weights, k, 0, Bp, outImg, strideB,
-                 0.0f, out, outImg, outImg * filters, batch, EPI_BIAS_ACT, biases, activation);
+                 0.0f, out, outImg, outImg * filters, batch, EPI_BIAS_ACT, biases, activation,
+                 true);
+}
+
+int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
+const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }
+
+int tns_hip_gemm_variant(tns_ctx* c, int32_t variant, uint8_t transA, uint8_t transB, int64_t M,
+                         int64_t N, int64_t K, float ALPHA, const float* A, int64_t aOffset,
+                         int64_t lda, int64_t strideA, const float* B, int64_t bOffset,
+                         int64_t ldb, int64_t strideB, float BETA, float* C, int64_t cOffset,
+                         int64_t ldc, int64_t strideC, int64_t batchCount) {
+  if (int r = check_ctx(c)) return r;
+  if (variant >= sgemm_variant_count())
+    return set_error(TNS_ERR_ARG, "gemm variant %d out of range", variant);
+  return do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, A ? A + aOffset : nullptr, lda,
+                 strideA, B ? B + bOffset : nullptr, ldb, strideB, BETA,
+                 C ? C + cOffset : nullptr, ldc, strideC, batchCount, EPI_NONE, nullptr, 0, false,
+                 variant);
 }
 
 int tns_hip_set_telemetry(tns_ctx* c, int32_t enable) {

@@ -50,6 +50,11 @@ struct GemmArgs {
 };
 
 hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s);
+// variant < 0 picks the tile shape by heuristic; otherwise forces one (tuning)
+hipError_t launch_sgemm_variant(int variant, const GemmArgs& a, bool transA, bool transB,
+                                hipStream_t s);
+int sgemm_variant_count();
+const char* sgemm_variant_name(int v);
 
 // ---- im2col / col2im -------------------------------------------------------
 struct ConvGeom {

@@ -90,6 +90,19 @@ class TNNHip:
             aOffset, lda, strideA, _ptr(B), bOffset, ldb, strideB, float(BETA), _ptr(C_), cOffset,
             ldc, strideC, batchCount))
 
+    def gemmVariant(self, variant, transA, transB, M, N, K, ALPHA, A, aOffset, lda, strideA, B,
+                    bOffset, ldb, strideB, BETA, C_, cOffset, ldc, strideC, batchCount=1):
+        """Force one SGEMM tile shape (tuning sweeps); variant < 0 = heuristic."""
+        check(self.lib.tns_hip_gemm_variant(
+            self.ctx, int(variant), int(bool(transA)), int(bool(transB)), M, N, K, float(ALPHA),
+            _ptr(A), aOffset, lda, strideA, _ptr(B), bOffset, ldb, strideB, float(BETA), _ptr(C_),
+            cOffset, ldc, strideC, batchCount))
+
+    @staticmethod
+    def gemmVariants() -> list[str]:
+        lib = load()
+        return [lib.tns_gemm_variant_name(i).decode() for i in range(lib.tns_gemm_variant_count())]
+
     # -- im2col / col2im --------------------------------------------------------
     def im2col(self, aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
                strideY, strideX, dilationY, dilationX, im, imOffset, col, colOffset):
