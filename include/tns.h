@@ -222,6 +222,58 @@ int tns_hip_copy(tns_ctx* ctx, int64_t N, const float* src, int64_t srcOffset, i
 int tns_hip_clamp(tns_ctx* ctx, int64_t N, float alpha, const float* src, float* dst,
                   int64_t stride, int64_t offset);
 
+/* ---- batch norm / softmax (TNNCuda twins, nncuda.pas:1056-1510; CPU
+ * semantics ntensors.pas:7687-7830, 8693-8951, 9102-9177,
+ * nsoftmaxlayer.pas:83-137).  Data is [groups][channels][blockSize]. ---- */
+/* meansAndVars: blockSize = srcSize/(dstSize*groups); unbiased variance */
+int tns_hip_means_and_vars(tns_ctx* ctx, int64_t srcSize, int64_t dstSize, int64_t groups,
+                           const float* src, int64_t offset, float* means, float* vars);
+/* normalize: blockSize = dstSize/(srcSize*groups); bs==1: (x-m)/sqrt(max(v,eps)),
+ * bs>1: (x-m)/max(sqrt(v),eps) */
+int tns_hip_normalize(tns_ctx* ctx, int64_t srcSize, int64_t dstSize, int64_t groups,
+                      const float* means, int64_t meansStride, const float* vars,
+                      int64_t varsStride, float* dst, int64_t dstOffset);
+/* forwardScale / forwardScaleAdd: dst[(b*S+i)*bs+j] = dst*scale[i*incb] (+ bias[i*incb]) */
+int tns_hip_forward_scale(tns_ctx* ctx, int64_t dstSize, float* dst, int64_t offset,
+                          int64_t scaleSize, const float* scale, int64_t incb, int64_t batch);
+int tns_hip_forward_scale_add(tns_ctx* ctx, int64_t dstSize, float* dst, int64_t offset,
+                              int64_t scaleSize, const float* scales, const float* biases,
+                              int64_t incb, int64_t batch);
+/* meansAndVarsDelta / normalizeDelta (sMeanAndVarianceDelta / sNormalizeDelta) */
+int tns_hip_means_and_vars_delta(tns_ctx* ctx, int64_t srcSize, int64_t dstSize, int64_t groups,
+                                 const float* delta, const float* x, int64_t offset,
+                                 const float* mean, const float* variance, float* mean_delta,
+                                 float* variance_delta);
+int tns_hip_normalize_delta(tns_ctx* ctx, int64_t deltaSize, int64_t meanSize, int64_t groups,
+                            float* delta, const float* x, int64_t offset, const float* mean,
+                            const float* variance, const float* mean_delta,
+                            const float* variance_delta);
+/* addDots: dst[i] += sum x_norm*delta over (group, block) */
+int tns_hip_add_dots(tns_ctx* ctx, int64_t N, int64_t dstSize, int64_t groups,
+                     const float* src1, const float* src2, int64_t srcOffset, float* dst);
+/* TSoftmaxLayer.softmaxBatch / softmaxCrossEntropy */
+int tns_hip_softmax_batch(tns_ctx* ctx, int64_t N, const float* input, int64_t iOffset,
+                          int64_t batch, int64_t batch_size, int64_t groups, int64_t group_size,
+                          int64_t stride, float temp, float* output, int64_t oOffset);
+int tns_hip_cross_entropy_softmax(tns_ctx* ctx, int64_t N, const float* pred, const float* truth,
+                                  float* delta, float* error);
+/* TTensor.Sum in the vssum_avx2 order (cost), result written to *out (device) */
+int tns_hip_sum(tns_ctx* ctx, int64_t N, const float* src, int64_t offset, float* out);
+
+/* ---- fused connected-network train step (BASELINE config 5) ------------
+ * One TNNet.Propagate + TNNet.update (nnet.pas:275-450) for nlayers
+ * TConnectedLayer (widths[l] -> widths[l+1], activation acts[l], batch norm
+ * when bn != 0) followed by a TSoftmaxLayer, as ONE kernel launch.  buf holds
+ * the packed parameters and state (layout: oracle/tns_oracle.h
+ * ora_mlp_train_step), sized tns_mlp_buffer_floats().  *cost (device) gets
+ * the softmax layer's loss.Sum().  Limits: nlayers <= 32,
+ * 8*batch*max(widths[1..]) <= 40960. */
+int64_t tns_mlp_buffer_floats(int32_t nlayers, const int64_t* widths, int32_t bn, int64_t batch);
+int tns_hip_mlp_train_step(tns_ctx* ctx, int32_t nlayers, const int64_t* widths,
+                           const int32_t* acts, int32_t bn, int64_t batch, const float* X,
+                           const float* truth, float learningRate, float momentum, float decay,
+                           float* buf, float* cost);
+
 /* ---- layer drivers (host logic of the reference, running on device) ---- */
 
 /* TTensor.Conv2D — ntensors.pas:8252-8349.  input: batch x C x H x W,

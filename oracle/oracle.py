@@ -157,3 +157,133 @@ def conv_forward(x, w, b, filters, k, stride, pad, act, dil=1):
     lib().ora_conv_forward(batch, C_, H, W, _p(x), _p(w), _p(b), filters, k, stride, pad, dil,
                            act, _p(ws), _p(out))
     return out
+
+
+_PROTO2 = {
+    "ora_vssum": (f32, [i64, fp]),
+    "ora_means_and_vars": (None, [fp, i64, i64, i64, fp, fp]),
+    "ora_normalize": (None, [fp, i64, i64, i64, fp, fp]),
+    "ora_forward_scale": (None, [fp, i64, i64, i64, fp]),
+    "ora_add_dots": (None, [fp, fp, fp, i64, i64, i64]),
+    "ora_add_sums": (None, [fp, fp, i64, i64, i64]),
+    "ora_mean_var_delta": (None, [fp, fp, fp, fp, i64, i64, i64, fp, fp]),
+    "ora_normalize_delta": (None, [fp, fp, fp, fp, fp, fp, i64, i64, i64]),
+    "ora_softmax": (None, [i64, fp, f32, i64, fp]),
+    "ora_softmax_xent": (None, [i64, fp, fp, fp, fp]),
+    "ora_clamp": (None, [fp, i64, f32, f32]),
+    "ora_mlp_train_step": (f32, [i32, C.POINTER(i64), C.POINTER(i32), i32, i64, fp, fp, f32, f32,
+                                 f32, fp]),
+    "ora_mlp_buffer_floats": (i64, [i32, C.POINTER(i64), i32, i64]),
+}
+
+
+def _lib2():
+    L = lib()
+    if not getattr(L, "_tns_p2", False):
+        for n, (r, a) in _PROTO2.items():
+            f = getattr(L, n)
+            f.restype = r
+            f.argtypes = a
+        L._tns_p2 = True
+    return L
+
+
+def vssum(a):
+    return float(_lib2().ora_vssum(a.size, _p(a)))
+
+
+def means_and_vars(x, groups, N, bs):
+    m = np.zeros(N, np.float32)
+    v = np.zeros(N, np.float32)
+    _lib2().ora_means_and_vars(_p(x), groups, N, bs, _p(m), _p(v))
+    return m, v
+
+
+def normalize(x, groups, N, bs, m, v):
+    _lib2().ora_normalize(_p(x), groups, N, bs, _p(m), _p(v))
+    return x
+
+
+def forward_scale(x, groups, N, bs, s):
+    _lib2().ora_forward_scale(_p(x), groups, N, bs, _p(s))
+    return x
+
+
+def add_dots(dst, a, b, groups, N, bs):
+    _lib2().ora_add_dots(_p(dst), _p(a), _p(b), groups, N, bs)
+    return dst
+
+
+def add_sums(dst, src, groups, N, bs):
+    _lib2().ora_add_sums(_p(dst), _p(src), groups, N, bs)
+    return dst
+
+
+def mean_var_delta(delta, x, mean, var, groups, N, bs):
+    md = np.zeros(N, np.float32)
+    vd = np.zeros(N, np.float32)
+    _lib2().ora_mean_var_delta(_p(delta), _p(x), _p(mean), _p(var), groups, N, bs, _p(md), _p(vd))
+    return md, vd
+
+
+def normalize_delta(x, mean, var, md, vd, delta, groups, N, bs):
+    _lib2().ora_normalize_delta(_p(x), _p(mean), _p(var), _p(md), _p(vd), _p(delta), groups, N,
+                                bs)
+    return delta
+
+
+def softmax_rows(x, n, temp=1.0):
+    out = np.zeros_like(x)
+    rows = x.size // n
+    L = _lib2()
+    for r in range(rows):
+        L.ora_softmax(n, x.ctypes.data + 4 * r * n, temp, 1, out.ctypes.data + 4 * r * n)
+    return out
+
+
+def softmax_xent(pred, truth):
+    d = np.zeros_like(pred)
+    e = np.zeros_like(pred)
+    _lib2().ora_softmax_xent(pred.size, _p(pred), _p(truth), _p(d), _p(e))
+    return d, e
+
+
+def mlp_buffer_floats(widths, bn, batch):
+    w = (C.c_int64 * len(widths))(*widths)
+    return int(_lib2().ora_mlp_buffer_floats(len(widths) - 1, w, 1 if bn else 0, batch))
+
+
+def mlp_train_step(widths, acts, bn, batch, X, truth, lr, momentum, decay, buf):
+    w = (C.c_int64 * len(widths))(*widths)
+    a = (C.c_int32 * len(acts))(*acts)
+    return float(_lib2().ora_mlp_train_step(len(widths) - 1, w, a, 1 if bn else 0, batch, _p(X),
+                                            _p(truth), lr, momentum, decay, _p(buf)))
+
+
+def mlp_init(widths, bn, batch, seed=5):
+    """Buffer with parameters initialised like TConnectedLayer.Create
+    (W ~ U[-sqrt(2/inputs), sqrt(2/inputs)], biases 0, scales 1)."""
+    buf = np.zeros(mlp_buffer_floats(widths, bn, batch), np.float32)
+    off = 0
+    for l in range(len(widths) - 1):
+        I, O = widths[l], widths[l + 1]
+        r = float(np.sqrt(2.0 / I))
+        buf[off:off + I * O] = uniform(I * O, seed, 100 + l, -r, r)
+        off += I * O          # W
+        off += O              # b (zeros)
+        off += I * O + O      # dW, db
+        if bn:
+            buf[off:off + O] = 1.0   # scales
+            off += 4 * O
+        off += 2 * batch * O  # out, delta
+        if bn:
+            off += 2 * batch * O + 4 * O
+    return buf
+
+
+def mnist_batch(batch, seed=5, classes=10, inputs=784):
+    X = uniform(batch * inputs, seed, 1, 0.0, 1.0)
+    lab = (uniform(batch, seed, 2, 0.0, 1.0) * classes).astype(np.int64) % classes
+    T = np.zeros((batch, classes), np.float32)
+    T[np.arange(batch), lab] = 1.0
+    return X, T.ravel()

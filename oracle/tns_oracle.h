@@ -105,6 +105,32 @@ void    ora_fuse_batchnorm(int64_t filters, int64_t filterSize, float* weights,
                            float* biases, const float* scales, const float* rollingMean,
                            const float* rollingVariance);
 
+/* ---- batch-norm / softmax / SGD / connected-layer train step -------------
+ * (tns_oracle_train.c; tolerance oracle: exp/ln/Power evaluated in double) */
+float   ora_vssum(int64_t n, const float* a);
+void    ora_means_and_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
+                           float* vars);
+void    ora_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
+                      const float* vars);
+void    ora_forward_scale(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales);
+void    ora_add_dots(float* dst, const float* a, const float* b, int64_t groups, int64_t N,
+                     int64_t bs);
+void    ora_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs);
+void    ora_mean_var_delta(const float* delta, const float* x, const float* mean,
+                           const float* var, int64_t groups, int64_t N, int64_t bs,
+                           float* mean_delta, float* var_delta);
+void    ora_normalize_delta(const float* x, const float* mean, const float* var,
+                            const float* mean_delta, const float* var_delta, float* delta,
+                            int64_t groups, int64_t N, int64_t bs);
+void    ora_softmax(int64_t n, const float* in, float temp, int64_t stride, float* out);
+void    ora_softmax_xent(int64_t n, const float* pred, const float* truth, float* delta,
+                         float* error);
+void    ora_clamp(float* x, int64_t n, float lo, float hi);
+float   ora_mlp_train_step(int32_t nlayers, const int64_t* widths, const int32_t* acts,
+                           int32_t bn, int64_t B, const float* X, const float* truth, float lr,
+                           float momentum, float decay, float* buf);
+int64_t ora_mlp_buffer_floats(int32_t nlayers, const int64_t* widths, int32_t bn, int64_t B);
+
 /* counter-based synthetic data (splitmix64 -> u in [lo,hi)), keyed by
  * (seed, stream, index) so CPU and GPU regenerate identical tensors. */
 void    ora_fill_uniform(float* x, int64_t n, uint64_t seed, uint64_t stream,

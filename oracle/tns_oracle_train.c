@@ -1,0 +1,358 @@
+/*
+ * tns_oracle_train.c — TEST INFRASTRUCTURE ONLY (see tns_oracle.h header).
+ *
+ * CPU restatement of the reference's batch-norm, softmax / cross-entropy,
+ * SGD update and connected-layer train step (BASELINE config 5):
+ *   TTensor.MeansAndVars        ntensors.pas:9102-9177
+ *   blockNormalize/_snormvv     ntensors.pas:8693-8718, 4331-4385
+ *   forwardScale / forwardBias  ntensors.pas:7687-7727
+ *   addSums / addDots           ntensors.pas:7729-7830
+ *   sMeanAndVarianceDelta       ntensors.pas:8831-8899 (+ sVarinceDelta_avx 8721)
+ *   sNormalizeDelta             ntensors.pas:8902-8951 (+ sNormalizeDelta_avx 8761)
+ *   softmax / softmaxCrossEntropy  nsoftmaxlayer.pas:83-137
+ *   TConnectedLayer.forward/backward/update  nconnectedlayer.pas:157-359
+ *   TNNet.forward/backward/update/cost       nnet.pas:275-403, 551-564
+ *
+ * Where the reference's AVX2 kernels are approximate or buggy (snormvss_avx
+ * uses rcpss; srss drops upper lanes when N%8==0 — SURVEY Appendix B.5/B.6)
+ * the scalar Pascal form is restated instead.  Transcendentals (exp, ln,
+ * Power) are evaluated in double and rounded once, so these functions are a
+ * tolerance oracle (1e-4 relative), not a bit-exact one.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "tns_oracle.h"
+
+static const float SEPS = 0.000001f; /* sEPSILON, ntensors.pas:95 */
+
+/* vssum_avx2 (ntensors.pas:3592-3620): 8 lanes over full blocks, fold
+ * lane_l + lane_{l+4}, hadd twice, then the remainder sequentially. */
+float ora_vssum(int64_t n, const float* a) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int64_t blocks = n >> 3;
+  for (int64_t t = 0; t < blocks; t++)
+    for (int l = 0; l < 8; l++) acc[l] = acc[l] + a[8 * t + l];
+  float s0 = acc[0] + acc[4], s1 = acc[1] + acc[5], s2 = acc[2] + acc[6], s3 = acc[3] + acc[7];
+  float r = (s0 + s1) + (s2 + s3);
+  for (int64_t i = blocks * 8; i < n; i++) r = r + a[i];
+  return r;
+}
+
+/* MeansAndVars: per channel i, m = sum_b sumv(bs, x_{b,i}) / (G*bs);
+ * v = sum_b rss(bs, m, x_{b,i}) / (G*bs - 1)  (unbiased).  Scalar sums. */
+void ora_means_and_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
+                        float* vars) {
+  const float S = (float)(groups * bs), S2 = (float)(groups * bs - 1);
+  for (int64_t i = 0; i < N; i++) {
+    float m = 0.0f;
+    for (int64_t b = 0; b < groups; b++) {
+      const float* d = x + (i + b * N) * bs;
+      float s = 0.0f;
+      for (int64_t j = 0; j < bs; j++) s = s + d[j];
+      m = m + s;
+    }
+    m = m / S;
+    means[i] = m;
+    float v = 0.0f;
+    for (int64_t b = 0; b < groups; b++) {
+      const float* d = x + (i + b * N) * bs;
+      float r = 0.0f;
+      for (int64_t j = 0; j < bs; j++) {
+        float t = d[j] - m;
+        r = r + t * t;
+      }
+      v = v + r;
+    }
+    vars[i] = v / S2;
+  }
+}
+
+/* blockNormalize: bs == 1 -> _snormvv: (x-m)/sqrt(max(v,eps));
+ * bs > 1 -> _snormblkvv/snormvss: (x-m)/max(sqrt(v),eps). */
+void ora_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
+                   const float* vars) {
+  for (int64_t g = 0; g < groups; g++)
+    for (int64_t i = 0; i < N; i++) {
+      float* d = x + (g * N + i) * bs;
+      if (bs == 1) {
+        float sd = sqrtf(vars[i] > SEPS ? vars[i] : SEPS);
+        d[0] = (d[0] - means[i]) / sd;
+      } else {
+        float sd = sqrtf(vars[i]);
+        sd = sd > SEPS ? sd : SEPS;
+        for (int64_t j = 0; j < bs; j++) d[j] = (d[j] - means[i]) / sd;
+      }
+    }
+}
+
+/* forwardScale -> vsMulB: c[j] := c[j] * s[i] */
+void ora_forward_scale(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales) {
+  for (int64_t g = 0; g < groups; g++)
+    for (int64_t i = 0; i < N; i++) {
+      float* d = x + (g * N + i) * bs;
+      for (int64_t j = 0; j < bs; j++) d[j] = d[j] * scales[i];
+    }
+}
+
+/* addDots: dst[i] += sum over (group, block) of x_norm*delta.
+ * bs == 1: dotvv(groups, .., stride nDst) = strided cblas_sdot scalar loop
+ * (mul then add).  bs > 1: sdot (8-lane FMA) per block, summed. */
+void ora_add_dots(float* dst, const float* a, const float* b, int64_t groups, int64_t N,
+                  int64_t bs) {
+  for (int64_t i = 0; i < N; i++) {
+    if (bs == 1) {
+      float r = 0.0f;
+      for (int64_t g = 0; g < groups; g++) r = r + a[i + g * N] * b[i + g * N];
+      dst[i] = dst[i] + r;
+    } else {
+      float sum = 0.0f;
+      for (int64_t g = 0; g < groups; g++)
+        sum = sum + ora_sdot(bs, a + (i + g * N) * bs, b + (i + g * N) * bs);
+      dst[i] = dst[i] + sum;
+    }
+  }
+}
+
+/* addSums blockSize == 1 branch: dst[i] += sumv(groups, src+i, stride N)
+ * (strided -> scalar vsSumI loop). */
+void ora_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs) {
+  if (bs == 1) {
+    for (int64_t i = 0; i < N; i++) {
+      float r = 0.0f;
+      for (int64_t g = 0; g < groups; g++) r = r + src[i + g * N];
+      dst[i] = dst[i] + r;
+    }
+  } else {
+    ora_backward_bias(N, dst, groups, bs, src);
+  }
+}
+
+/* sMeanAndVarianceDelta with the AVX2 sVarinceDelta_avx / vssum_avx2 forms
+ * (for bs == 1 both reduce to one rounded term per group). */
+void ora_mean_var_delta(const float* delta, const float* x, const float* mean,
+                        const float* var, int64_t groups, int64_t N, int64_t bs,
+                        float* mean_delta, float* var_delta) {
+  for (int64_t i = 0; i < N; i++) {
+    float m = 0.0f, v = 0.0f;
+    for (int64_t j = 0; j < groups; j++) {
+      const float* dd = delta + (i + j * N) * bs;
+      const float* xx = x + (i + j * N) * bs;
+      m = m + ora_vssum(bs, dd);
+      float t = 0.0f;
+      for (int64_t k = 0; k < bs; k++) t = t + (xx[k] - mean[i]) * dd[k];
+      v = v + t;
+    }
+    float ve = var[i] > SEPS ? var[i] : SEPS;
+    float inv = -1.0f / sqrtf(ve);
+    mean_delta[i] = m * inv;
+    var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
+  }
+}
+
+/* sNormalizeDelta (AVX2 sNormalizeDelta_avx order):
+ * d := d/std + ((x-mean)*(2*vd/B) + md/B),  B = groups*bs */
+void ora_normalize_delta(const float* x, const float* mean, const float* var,
+                         const float* mean_delta, const float* var_delta, float* delta,
+                         int64_t groups, int64_t N, int64_t bs) {
+  const float B = (float)(groups * bs);
+  for (int64_t j = 0; j < groups; j++)
+    for (int64_t i = 0; i < N; i++) {
+      float md = mean_delta[i] / B;
+      float vd = 2.0f * var_delta[i] / B;
+      float ve = var[i] > SEPS ? var[i] : SEPS;
+      float sd = sqrtf(ve);
+      float* dd = delta + (i + j * N) * bs;
+      const float* xx = x + (i + j * N) * bs;
+      for (int64_t k = 0; k < bs; k++) {
+        float a = dd[k] / sd;
+        float t = (xx[k] - mean[i]) * vd + md;
+        dd[k] = a + t;
+      }
+    }
+}
+
+/* softmax (nsoftmaxlayer.pas:83-106) over n elements with stride. */
+void ora_softmax(int64_t n, const float* in, float temp, int64_t stride, float* out) {
+  if (n == 0) return;
+  float largest = in[0];
+  for (int64_t i = 1; i < n; i++)
+    if (in[i * stride] > largest) largest = in[i * stride];
+  float sum = 0.0f;
+  for (int64_t i = 0; i < n; i++) {
+    float e = (float)exp((double)((in[i * stride] - largest) / temp));
+    sum = sum + e;
+    out[i * stride] = e;
+  }
+  for (int64_t i = 0; i < n; i++) out[i * stride] = out[i * stride] / sum;
+}
+
+/* softmaxCrossEntropy (123-137) */
+void ora_softmax_xent(int64_t n, const float* pred, const float* truth, float* delta,
+                      float* error) {
+  for (int64_t i = 0; i < n; i++) {
+    float t = truth[i], p = pred[i];
+    error[i] = t != 0.0f ? (float)(-log((double)(p > SEPS ? p : SEPS))) : 0.0f;
+    delta[i] = t - p;
+  }
+}
+
+/* vsClamp (ntensors.pas:5235-5250) */
+void ora_clamp(float* x, int64_t n, float lo, float hi) {
+  for (int64_t i = 0; i < n; i++) {
+    if (x[i] < lo) x[i] = lo;
+    else if (x[i] > hi) x[i] = hi;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Feed-forward (connected) network train step                               */
+/* ------------------------------------------------------------------------ */
+/* Parameter / state layout per layer l (inputs I, outputs O), all float:
+ *   W[O*I], b[O], dW[O*I], db[O], and when bn: scales[O], rolling_mean[O],
+ *   rolling_var[O], dscales[O];  activations out[B*O], delta[B*O],
+ *   x[B*O], x_norm[B*O], mean[O], var[O], mean_delta[O], var_delta[O]. */
+typedef struct {
+  int64_t I, O;
+  int32_t act, bn;
+  float *W, *b, *dW, *db, *scales, *rmean, *rvar, *dscales;
+  float *out, *delta, *x, *xnorm, *mean, *var, *mdelta, *vdelta;
+} ora_fc;
+
+static void fc_forward(ora_fc* L, const float* in, int64_t B, float bn_momentum) {
+  /* gemm(NT, batch, outputs, inputs, 1, X, inputs, W, inputs, 0, out, outputs) */
+  ora_sgemm(101, 111, 112, B, L->O, L->I, 1.0f, in, L->I, L->W, L->I, 0.0f, L->out, L->O);
+  if (L->bn) {
+    ora_means_and_vars(L->out, B, L->O, 1, L->mean, L->var);
+    for (int64_t i = 0; i < L->O; i++) { /* Multiply(1-m) then axpy(m, stat) */
+      L->rmean[i] = L->rmean[i] * (1.0f - bn_momentum);
+      L->rmean[i] = fmaf(bn_momentum, L->mean[i], L->rmean[i]);
+      L->rvar[i] = L->rvar[i] * (1.0f - bn_momentum);
+      L->rvar[i] = fmaf(bn_momentum, L->var[i], L->rvar[i]);
+    }
+    memcpy(L->x, L->out, sizeof(float) * B * L->O);
+    ora_normalize(L->out, B, L->O, 1, L->mean, L->var);
+    memcpy(L->xnorm, L->out, sizeof(float) * B * L->O);
+    ora_forward_scale(L->out, B, L->O, 1, L->scales);
+  }
+  ora_add_bias(L->O, L->out, 1, L->b, 1, B);
+  ora_activate(L->out, B * L->O, L->act);
+}
+
+static void fc_backward(ora_fc* L, const float* in, float* prev_delta, int64_t B) {
+  ora_clamp(L->delta, B * L->O, -1.0f, 1.0f);
+  ora_gradient(L->out, B * L->O, L->act, L->delta);
+  ora_add_sums(L->db, L->delta, B, L->O, 1);
+  if (L->bn) {
+    ora_add_dots(L->dscales, L->xnorm, L->delta, B, L->O, 1);
+    ora_forward_scale(L->delta, B, L->O, 1, L->scales);
+    ora_mean_var_delta(L->delta, L->x, L->mean, L->var, B, L->O, 1, L->mdelta, L->vdelta);
+    ora_normalize_delta(L->x, L->mean, L->var, L->mdelta, L->vdelta, L->delta, B, L->O, 1);
+  }
+  /* gemm(TN, outputs, inputs, batch, 1, delta, outputs, X, inputs, 1, dW, inputs) */
+  ora_sgemm(101, 112, 111, L->O, L->I, B, 1.0f, L->delta, L->O, in, L->I, 1.0f, L->dW, L->I);
+  if (prev_delta) /* gemm(NN, batch, inputs, outputs, 1, delta, outputs, W, inputs, 1, prev) */
+    ora_sgemm(101, 111, 111, B, L->I, L->O, 1.0f, L->delta, L->O, L->W, L->I, 1.0f,
+              prev_delta, L->I);
+}
+
+static void axpy_(int64_t n, float a, const float* x, float* y) {
+  for (int64_t i = 0; i < n; i++) y[i] = fmaf(a, x[i], y[i]); /* saxpy_avx2 */
+}
+static void scal_(int64_t n, float a, float* x) {
+  for (int64_t i = 0; i < n; i++) x[i] = a * x[i]; /* sscal vmulps */
+}
+
+static void fc_update(ora_fc* L, float lr, float momentum, float decay, int64_t batch) {
+  const float lrb = lr / (float)batch;
+  axpy_(L->O, lrb, L->db, L->b);
+  scal_(L->O, momentum, L->db);
+  if (L->bn) {
+    axpy_(L->O, lrb, L->dscales, L->scales);
+    scal_(L->O, momentum, L->dscales);
+  }
+  axpy_(L->O * L->I, -decay * (float)batch, L->W, L->dW);
+  axpy_(L->O * L->I, lrb, L->dW, L->W);
+  scal_(L->O * L->I, momentum, L->dW);
+}
+
+/* One TNNet.Propagate + update over a stack of connected layers followed by
+ * a softmax layer (nnet.pas:405-450, 371-403).  `buf` holds, per layer, the
+ * arrays described above packed back to back in the order
+ *   W b dW db [scales rmean rvar dscales] out delta [x xnorm mean var mdelta vdelta]
+ * plus, at the end, softmax out[B*C], delta[B*C], loss[B*C].  Returns the
+ * cost (loss.Sum() via vssum_avx2; TNNet.cost divides by 1 cost layer). */
+float ora_mlp_train_step(int32_t nlayers, const int64_t* widths, const int32_t* acts,
+                         int32_t bn, int64_t B, const float* X, const float* truth, float lr,
+                         float momentum, float decay, float* buf) {
+  ora_fc L[32];
+  if (nlayers > 32) return NAN;
+  float* p = buf;
+  for (int l = 0; l < nlayers; l++) {
+    ora_fc* f = &L[l];
+    f->I = widths[l];
+    f->O = widths[l + 1];
+    f->act = acts[l];
+    f->bn = bn;
+    int64_t IO = f->I * f->O, O = f->O, BO = B * f->O;
+    f->W = p; p += IO;
+    f->b = p; p += O;
+    f->dW = p; p += IO;
+    f->db = p; p += O;
+    if (bn) {
+      f->scales = p; p += O;
+      f->rmean = p; p += O;
+      f->rvar = p; p += O;
+      f->dscales = p; p += O;
+    }
+    f->out = p; p += BO;
+    f->delta = p; p += BO;
+    if (bn) {
+      f->x = p; p += BO;
+      f->xnorm = p; p += BO;
+      f->mean = p; p += O;
+      f->var = p; p += O;
+      f->mdelta = p; p += O;
+      f->vdelta = p; p += O;
+    }
+  }
+  const int64_t C = widths[nlayers];
+  float* sm_out = p; p += B * C;
+  float* sm_delta = p; p += B * C;
+  float* sm_loss = p; p += B * C;
+
+  /* forward: each layer's delta is zeroed first (nnet.pas:287-296) */
+  const float* in = X;
+  for (int l = 0; l < nlayers; l++) {
+    memset(L[l].delta, 0, sizeof(float) * B * L[l].O);
+    fc_forward(&L[l], in, B, 0.05f); /* bnMomentum := 0.05 (nconnectedlayer.pas:67) */
+    in = L[l].out;
+  }
+  /* softmax layer: groups = 1, temperature 1 */
+  for (int64_t b = 0; b < B; b++) ora_softmax(C, in + b * C, 1.0f, 1, sm_out + b * C);
+  ora_softmax_xent(B * C, sm_out, truth, sm_delta, sm_loss);
+  float cost = ora_vssum(B * C, sm_loss);
+
+  /* backward: softmax adds its delta into the previous layer's delta */
+  for (int64_t i = 0; i < B * C; i++)
+    L[nlayers - 1].delta[i] = L[nlayers - 1].delta[i] + sm_delta[i];
+  for (int l = nlayers - 1; l >= 0; l--) {
+    const float* lin = l == 0 ? X : L[l - 1].out;
+    float* prev_delta = l == 0 ? NULL : L[l - 1].delta; /* state.delta = nil for layer 0 */
+    fc_backward(&L[l], lin, prev_delta, B);
+  }
+  /* update (constant learning-rate policy) */
+  for (int l = 0; l < nlayers; l++) fc_update(&L[l], lr, momentum, decay, B);
+  return cost;
+}
+
+int64_t ora_mlp_buffer_floats(int32_t nlayers, const int64_t* widths, int32_t bn, int64_t B) {
+  int64_t n = 0;
+  for (int l = 0; l < nlayers; l++) {
+    int64_t I = widths[l], O = widths[l + 1];
+    n += 2 * I * O + 2 * O + 2 * B * O;
+    if (bn) n += 4 * O + 2 * B * O + 4 * O;
+  }
+  return n + 3 * B * widths[nlayers];
+}

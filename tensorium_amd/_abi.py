@@ -133,3 +133,23 @@ def check(rc: int) -> None:
     if rc != TNS_OK:
         msg = load().tns_last_error().decode(errors="replace")
         raise TnsError(f"tns status {rc}: {msg}")
+
+
+PROTOTYPES.update({
+    "tns_hip_means_and_vars": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, fptr]),
+    "tns_hip_normalize": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, i64, fptr, i64]),
+    "tns_hip_forward_scale": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64]),
+    "tns_hip_forward_scale_add": (C.c_int, [vp, i64, fptr, i64, i64, fptr, fptr, i64, i64]),
+    "tns_hip_means_and_vars_delta": (C.c_int, [vp, i64, i64, i64, fptr, fptr, i64, fptr, fptr,
+                                               fptr, fptr]),
+    "tns_hip_normalize_delta": (C.c_int, [vp, i64, i64, i64, fptr, fptr, i64, fptr, fptr, fptr,
+                                          fptr]),
+    "tns_hip_add_dots": (C.c_int, [vp, i64, i64, i64, fptr, fptr, i64, fptr]),
+    "tns_hip_softmax_batch": (C.c_int, [vp, i64, fptr, i64, i64, i64, i64, i64, i64, f32, fptr,
+                                        i64]),
+    "tns_hip_cross_entropy_softmax": (C.c_int, [vp, i64, fptr, fptr, fptr, fptr]),
+    "tns_hip_sum": (C.c_int, [vp, i64, fptr, i64, fptr]),
+    "tns_mlp_buffer_floats": (i64, [i32, C.POINTER(i64), i32, i64]),
+    "tns_hip_mlp_train_step": (C.c_int, [vp, i32, C.POINTER(i64), C.POINTER(i32), i32, i64, fptr,
+                                         fptr, f32, f32, f32, fptr, fptr]),
+})

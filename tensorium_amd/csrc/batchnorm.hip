@@ -1,0 +1,358 @@
+// batchnorm.hip — batch-norm, softmax / cross-entropy and reductions for the
+// connected-layer train step (BASELINE config 5), gfx950.
+//
+// Device twins of TNNCuda.meansAndVars / normalize / forwardScale(Add) /
+// meansAndVarsDelta / normalizeDelta / addDots / softmaxBatch /
+// crossEntropySoftmax (nncuda.pas:1056-1510), with the CPU semantics of
+// ntensors.pas:7687-7830, 8693-8718, 8821-8951, 9102-9177 and
+// nsoftmaxlayer.pas:83-137 (see oracle/tns_oracle_train.c).
+//
+// Reductions over one channel run as ONE thread walking the reference's
+// sequential order when the channel has <= kSeqMax elements (the FC layers:
+// blockSize 1, groups = batch), so sums are bit-identical; larger channels
+// (conv BN) use a fixed-order workgroup tree reduction (deterministic, within
+// the 1e-4 relative bar).  Transcendentals (exp, ln, pow) are evaluated in
+// double and rounded once, as the oracle does.
+#include "tns_internal.hpp"
+
+namespace tns {
+namespace {
+
+constexpr int TPB = 256;
+constexpr int64_t kSeqMax = 8192;
+__device__ constexpr float SEPS = 0.000001f;  // sEPSILON, ntensors.pas:95
+
+inline unsigned nblk(int64_t n) {
+  int64_t g = (n + TPB - 1) / TPB;
+  return (unsigned)(g < 1 ? 1 : (g > 65535 * 4 ? 65535 * 4 : g));
+}
+
+// fixed-order block reduction of one float per thread (TPB threads)
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = 0.0f;
+  if (threadIdx.x == 0) r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  __syncthreads();
+  return r;
+}
+
+// ---- MeansAndVars --------------------------------------------------------
+__global__ void means_vars_seq(const float* __restrict__ x, int64_t groups, int64_t N, int64_t bs,
+                               float* __restrict__ means, float* __restrict__ vars) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= N) return;
+  const float S = (float)(groups * bs), S2 = (float)(groups * bs - 1);
+  float m = 0.0f;
+  for (int64_t b = 0; b < groups; ++b) {
+    const float* d = x + (i + b * N) * bs;
+    float s = 0.0f;
+    for (int64_t j = 0; j < bs; ++j) s = s + d[j];
+    m = m + s;
+  }
+  m = m / S;
+  means[i] = m;
+  float v = 0.0f;
+  for (int64_t b = 0; b < groups; ++b) {
+    const float* d = x + (i + b * N) * bs;
+    float r = 0.0f;
+    for (int64_t j = 0; j < bs; ++j) {
+      const float t = d[j] - m;
+      r = r + t * t;
+    }
+    v = v + r;
+  }
+  vars[i] = v / S2;
+}
+
+__global__ __launch_bounds__(TPB) void means_vars_blk(const float* __restrict__ x, int64_t groups,
+                                                      int64_t N, int64_t bs,
+                                                      float* __restrict__ means,
+                                                      float* __restrict__ vars) {
+  __shared__ float sh[4];
+  __shared__ float mean_s;
+  const int64_t i = blockIdx.x;
+  const int64_t per = groups * bs;
+  float s = 0.0f;
+  for (int64_t t = threadIdx.x; t < per; t += TPB) {
+    const int64_t b = t / bs, j = t - b * bs;
+    s += x[(i + b * N) * bs + j];
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    mean_s = s / (float)per;
+    means[i] = mean_s;
+  }
+  __syncthreads();
+  const float m = mean_s;
+  float r = 0.0f;
+  for (int64_t t = threadIdx.x; t < per; t += TPB) {
+    const int64_t b = t / bs, j = t - b * bs;
+    const float d = x[(i + b * N) * bs + j] - m;
+    r += d * d;
+  }
+  r = block_sum(r, sh);
+  if (threadIdx.x == 0) vars[i] = r / (float)(per - 1);
+}
+
+// ---- normalize / scale / bias ----------------------------------------------
+__global__ void normalize_k(float* __restrict__ x, int64_t total, int64_t N, int64_t bs,
+                            const float* __restrict__ means, int64_t mstride,
+                            const float* __restrict__ vars, int64_t vstride) {
+  for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * TPB) {
+    const int64_t i = (e / bs) % N;
+    const float m = means[i * mstride], v = vars[i * vstride];
+    float sd;
+    if (bs == 1) {
+      sd = sqrtf(v > SEPS ? v : SEPS);  // _snormvv
+    } else {
+      sd = sqrtf(v);                     // _snormblkvv -> snormvss
+      sd = sd > SEPS ? sd : SEPS;
+    }
+    x[e] = (x[e] - m) / sd;
+  }
+}
+
+__global__ void scale_add_k(float* __restrict__ x, int64_t total, int64_t N, int64_t bs,
+                            const float* __restrict__ scales, const float* __restrict__ biases,
+                            int64_t incb) {
+  for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * TPB) {
+    const int64_t i = (e / bs) % N;
+    float v = x[e] * scales[i * incb];            // forwardScale (vsMulB)
+    if (biases) v = v + biases[i * incb];         // forwardBias  (vsAddB)
+    x[e] = v;
+  }
+}
+
+// ---- addDots / addSums -------------------------------------------------------
+__global__ void add_dots_seq(float* __restrict__ dst, const float* __restrict__ a,
+                             const float* __restrict__ b, int64_t groups, int64_t N, int64_t bs) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= N) return;
+  if (bs == 1) {  // strided cblas_sdot: scalar mul then add
+    float r = 0.0f;
+    for (int64_t g = 0; g < groups; ++g) r = r + a[i + g * N] * b[i + g * N];
+    dst[i] = dst[i] + r;
+  } else {        // per block sdot_avx2 (8 FMA lanes), blocks summed
+    float sum = 0.0f;
+    for (int64_t g = 0; g < groups; ++g) {
+      const float* pa = a + (i + g * N) * bs;
+      const float* pb = b + (i + g * N) * bs;
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      const int64_t blocks = bs >> 3;
+      for (int64_t t = 0; t < blocks; ++t)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc[l] = fmaf(pa[8 * t + l], pb[8 * t + l], acc[l]);
+      const int64_t rem = bs & 7;
+      if (rem) {
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+          const float xa = l < rem ? pa[8 * blocks + l] : 0.0f;
+          const float xb = l < rem ? pb[8 * blocks + l] : 0.0f;
+          acc[l] = fmaf(xa, xb, acc[l]);
+        }
+      }
+      const float s0 = acc[0] + acc[4], s1 = acc[1] + acc[5], s2 = acc[2] + acc[6],
+                  s3 = acc[3] + acc[7];
+      sum = sum + ((s0 + s1) + (s2 + s3));
+    }
+    dst[i] = dst[i] + sum;
+  }
+}
+
+__global__ void add_sums_seq(float* __restrict__ dst, const float* __restrict__ src,
+                             int64_t groups, int64_t N) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= N) return;
+  float r = 0.0f;  // strided vsSumI: scalar running sum
+  for (int64_t g = 0; g < groups; ++g) r = r + src[i + g * N];
+  dst[i] = dst[i] + r;
+}
+
+// ---- MeanAndVarianceDelta / NormalizeDelta ---------------------------------
+__device__ __forceinline__ float vssum8(const float* a, int64_t n) {  // vssum_avx2 order
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t blocks = n >> 3;
+  for (int64_t t = 0; t < blocks; ++t)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc[l] = acc[l] + a[8 * t + l];
+  const float s0 = acc[0] + acc[4], s1 = acc[1] + acc[5], s2 = acc[2] + acc[6],
+              s3 = acc[3] + acc[7];
+  float r = (s0 + s1) + (s2 + s3);
+  for (int64_t i = blocks * 8; i < n; ++i) r = r + a[i];
+  return r;
+}
+
+__global__ void mean_var_delta_seq(const float* __restrict__ delta, const float* __restrict__ x,
+                                   const float* __restrict__ mean, const float* __restrict__ var,
+                                   int64_t groups, int64_t N, int64_t bs,
+                                   float* __restrict__ mean_delta, float* __restrict__ var_delta) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= N) return;
+  float m = 0.0f, v = 0.0f;
+  const float mu = mean[i];
+  for (int64_t j = 0; j < groups; ++j) {
+    const float* dd = delta + (i + j * N) * bs;
+    const float* xx = x + (i + j * N) * bs;
+    m = m + vssum8(dd, bs);
+    float t = 0.0f;
+    for (int64_t k = 0; k < bs; ++k) t = t + (xx[k] - mu) * dd[k];
+    v = v + t;
+  }
+  const float ve = var[i] > SEPS ? var[i] : SEPS;
+  const float inv = -1.0f / sqrtf(ve);
+  mean_delta[i] = m * inv;
+  var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
+}
+
+__global__ void normalize_delta_k(const float* __restrict__ x, const float* __restrict__ mean,
+                                  const float* __restrict__ var,
+                                  const float* __restrict__ mean_delta,
+                                  const float* __restrict__ var_delta, float* __restrict__ delta,
+                                  int64_t total, int64_t N, int64_t bs, float B) {
+  for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * TPB) {
+    const int64_t i = (e / bs) % N;
+    const float md = mean_delta[i] / B;
+    const float vd = 2.0f * var_delta[i] / B;
+    const float ve = var[i] > SEPS ? var[i] : SEPS;
+    const float sd = sqrtf(ve);
+    const float a = delta[e] / sd;
+    const float t = (x[e] - mean[i]) * vd + md;  // sNormalizeDelta_avx order
+    delta[e] = a + t;
+  }
+}
+
+// ---- softmax / cross-entropy ------------------------------------------------
+// one thread per (batch, group): TSoftmaxLayer.softmaxBatch / softmax
+__global__ void softmax_batch_k(int64_t n, const float* __restrict__ in, int64_t batch,
+                                int64_t batch_size, int64_t groups, int64_t group_size,
+                                int64_t stride, float temp, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t >= batch * groups || n == 0) return;
+  const int64_t b = t / groups, g = t - b * groups;
+  const float* ip = in + b * batch_size + g * group_size;
+  float* op = out + b * batch_size + g * group_size;
+  float largest = ip[0];
+  for (int64_t i = 1; i < n; ++i)
+    if (ip[i * stride] > largest) largest = ip[i * stride];
+  float sum = 0.0f;
+  for (int64_t i = 0; i < n; ++i) {
+    const float e = (float)exp((double)((ip[i * stride] - largest) / temp));
+    sum = sum + e;
+    op[i * stride] = e;
+  }
+  for (int64_t i = 0; i < n; ++i) op[i * stride] = op[i * stride] / sum;
+}
+
+__global__ void xent_softmax_k(int64_t n, const float* __restrict__ pred,
+                               const float* __restrict__ truth, float* __restrict__ delta,
+                               float* __restrict__ error) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * TPB) {
+    const float t = truth[i], p = pred[i];
+    error[i] = t != 0.0f ? (float)(-log((double)(p > SEPS ? p : SEPS))) : 0.0f;
+    delta[i] = t - p;
+  }
+}
+
+// vssum_avx2-ordered sum of a vector into *out (one thread; cost vector is
+// batch*classes elements)
+__global__ void vssum_k(int64_t n, const float* __restrict__ a, float* __restrict__ out) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *out = vssum8(a, n);
+}
+
+}  // namespace
+
+hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
+                             float* vars, hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  if (groups * bs <= kSeqMax)
+    hipLaunchKernelGGL(means_vars_seq, dim3(nblk(N)), dim3(TPB), 0, s, x, groups, N, bs, means,
+                       vars);
+  else
+    hipLaunchKernelGGL(means_vars_blk, dim3((unsigned)N), dim3(TPB), 0, s, x, groups, N, bs,
+                       means, vars);
+  return hipGetLastError();
+}
+
+hipError_t launch_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
+                            int64_t mstride, const float* vars, int64_t vstride, hipStream_t s) {
+  const int64_t total = groups * N * bs;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(normalize_k, dim3(nblk(total)), dim3(TPB), 0, s, x, total, N, bs, means,
+                     mstride, vars, vstride);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales,
+                            const float* biases, int64_t incb, hipStream_t s) {
+  const int64_t total = groups * N * bs;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scale_add_k, dim3(nblk(total)), dim3(TPB), 0, s, x, total, N, bs, scales,
+                     biases, incb);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_dots(float* dst, const float* a, const float* b, int64_t groups, int64_t N,
+                           int64_t bs, hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(add_dots_seq, dim3(nblk(N)), dim3(TPB), 0, s, dst, a, b, groups, N, bs);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs,
+                           hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  if (bs == 1) {
+    hipLaunchKernelGGL(add_sums_seq, dim3(nblk(N)), dim3(TPB), 0, s, dst, src, groups, N);
+    return hipGetLastError();
+  }
+  return launch_backward_bias(dst, N, src, bs, groups, 1, s);
+}
+
+hipError_t launch_mean_var_delta(const float* delta, const float* x, const float* mean,
+                                 const float* var, int64_t groups, int64_t N, int64_t bs,
+                                 float* mean_delta, float* var_delta, hipStream_t s) {
+  if (N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mean_var_delta_seq, dim3(nblk(N)), dim3(TPB), 0, s, delta, x, mean, var,
+                     groups, N, bs, mean_delta, var_delta);
+  return hipGetLastError();
+}
+
+hipError_t launch_normalize_delta(const float* x, const float* mean, const float* var,
+                                  const float* mean_delta, const float* var_delta, float* delta,
+                                  int64_t groups, int64_t N, int64_t bs, hipStream_t s) {
+  const int64_t total = groups * N * bs;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(normalize_delta_k, dim3(nblk(total)), dim3(TPB), 0, s, x, mean, var,
+                     mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs));
+  return hipGetLastError();
+}
+
+hipError_t launch_softmax_batch(int64_t n, const float* in, int64_t batch, int64_t batch_size,
+                                int64_t groups, int64_t group_size, int64_t stride, float temp,
+                                float* out, hipStream_t s) {
+  if (batch * groups <= 0) return hipSuccess;
+  hipLaunchKernelGGL(softmax_batch_k, dim3(nblk(batch * groups)), dim3(TPB), 0, s, n, in, batch,
+                     batch_size, groups, group_size, stride, temp, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_xent_softmax(int64_t n, const float* pred, const float* truth, float* delta,
+                               float* error, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(xent_softmax_k, dim3(nblk(n)), dim3(TPB), 0, s, n, pred, truth, delta,
+                     error);
+  return hipGetLastError();
+}
+
+hipError_t launch_vssum(int64_t n, const float* a, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(vssum_k, dim3(1), dim3(64), 0, s, n, a, out);
+  return hipGetLastError();
+}
+
+}  // namespace tns

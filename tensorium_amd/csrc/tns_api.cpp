@@ -383,6 +383,9 @@ int tns_hip_backward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t srcSi
     return set_error(TNS_ERR_ARG, "backwardBias: sizes do not align");
   const int64_t bs = srcSize / (dstSize * batch);
   OpTimer t(c, TNS_OP_BIAS);
+  if (bs == 1 && incb == 1)  // FC layers: the reference's sequential strided sum
+    return hip_status(launch_add_sums(dst, src + srcOffset, batch, dstSize, 1, c->stream),
+                      "backwardBias launch");
   return hip_status(launch_backward_bias(dst, dstSize, src + srcOffset, bs, batch, incb, c->stream),
                     "backwardBias launch");
 }
@@ -436,6 +439,155 @@ int tns_hip_clamp(tns_ctx* c, int64_t N, float alpha, const float* src, float* d
   if (int r = check_ctx(c)) return r;
   return hip_status(launch_clamp(N, alpha, src + offset, dst + offset, stride, c->stream),
                     "clamp");
+}
+
+// ---- batch norm / softmax ------------------------------------------------------
+namespace {
+int blocks_of(int64_t total, int64_t channels, int64_t groups, int64_t* bs, const char* what) {
+  if (channels <= 0 || groups <= 0 || total < 0 || total % (channels * groups) != 0)
+    return set_error(TNS_ERR_ARG, "%s: sizes do not align (total=%lld channels=%lld groups=%lld)",
+                     what, (long long)total, (long long)channels, (long long)groups);
+  *bs = total / (channels * groups);
+  return TNS_OK;
+}
+}  // namespace
+
+int tns_hip_means_and_vars(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
+                           const float* src, int64_t offset, float* means, float* vars) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(srcSize, dstSize, groups, &bs, "meansAndVars")) return r;
+  if (!src || !means || !vars) return set_error(TNS_ERR_ARG, "meansAndVars: null pointer");
+  return hip_status(launch_means_vars(src + offset, groups, dstSize, bs, means, vars, c->stream),
+                    "meansAndVars");
+}
+
+int tns_hip_normalize(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
+                      const float* means, int64_t meansStride, const float* vars,
+                      int64_t varsStride, float* dst, int64_t dstOffset) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(dstSize, srcSize, groups, &bs, "normalize")) return r;
+  if (!dst || !means || !vars) return set_error(TNS_ERR_ARG, "normalize: null pointer");
+  return hip_status(launch_normalize(dst + dstOffset, groups, srcSize, bs, means, meansStride,
+                                     vars, varsStride, c->stream),
+                    "normalize");
+}
+
+int tns_hip_forward_scale(tns_ctx* c, int64_t dstSize, float* dst, int64_t offset,
+                          int64_t scaleSize, const float* scale, int64_t incb, int64_t batch) {
+  return tns_hip_forward_scale_add(c, dstSize, dst, offset, scaleSize, scale, nullptr, incb,
+                                   batch);
+}
+
+int tns_hip_forward_scale_add(tns_ctx* c, int64_t dstSize, float* dst, int64_t offset,
+                              int64_t scaleSize, const float* scales, const float* biases,
+                              int64_t incb, int64_t batch) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(dstSize, scaleSize, batch, &bs, "forwardScale")) return r;
+  if (!dst || !scales) return set_error(TNS_ERR_ARG, "forwardScale: null pointer");
+  return hip_status(launch_scale_add(dst + offset, batch, scaleSize, bs, scales, biases, incb,
+                                     c->stream),
+                    "forwardScale");
+}
+
+int tns_hip_means_and_vars_delta(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
+                                 const float* delta, const float* x, int64_t offset,
+                                 const float* mean, const float* variance, float* mean_delta,
+                                 float* variance_delta) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(srcSize, dstSize, groups, &bs, "meansAndVarsDelta")) return r;
+  return hip_status(launch_mean_var_delta(delta + offset, x + offset, mean, variance, groups,
+                                          dstSize, bs, mean_delta, variance_delta, c->stream),
+                    "meansAndVarsDelta");
+}
+
+int tns_hip_normalize_delta(tns_ctx* c, int64_t deltaSize, int64_t meanSize, int64_t groups,
+                            float* delta, const float* x, int64_t offset, const float* mean,
+                            const float* variance, const float* mean_delta,
+                            const float* variance_delta) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(deltaSize, meanSize, groups, &bs, "normalizeDelta")) return r;
+  return hip_status(launch_normalize_delta(x + offset, mean, variance, mean_delta,
+                                           variance_delta, delta + offset, groups, meanSize, bs,
+                                           c->stream),
+                    "normalizeDelta");
+}
+
+int tns_hip_add_dots(tns_ctx* c, int64_t N, int64_t dstSize, int64_t groups, const float* src1,
+                     const float* src2, int64_t srcOffset, float* dst) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(N, dstSize, groups, &bs, "addDots")) return r;
+  return hip_status(launch_add_dots(dst, src1 + srcOffset, src2 + srcOffset, groups, dstSize, bs,
+                                    c->stream),
+                    "addDots");
+}
+
+int tns_hip_softmax_batch(tns_ctx* c, int64_t N, const float* input, int64_t iOffset,
+                          int64_t batch, int64_t batch_size, int64_t groups, int64_t group_size,
+                          int64_t stride, float temp, float* output, int64_t oOffset) {
+  if (int r = check_ctx(c)) return r;
+  if (!input || !output || N < 0) return set_error(TNS_ERR_ARG, "softmaxBatch: bad args");
+  return hip_status(launch_softmax_batch(N, input + iOffset, batch, batch_size, groups,
+                                         group_size, stride, temp, output + oOffset, c->stream),
+                    "softmaxBatch");
+}
+
+int tns_hip_cross_entropy_softmax(tns_ctx* c, int64_t N, const float* pred, const float* truth,
+                                  float* delta, float* error) {
+  if (int r = check_ctx(c)) return r;
+  if (!pred || !truth || !delta || !error) return set_error(TNS_ERR_ARG, "xent: null pointer");
+  return hip_status(launch_xent_softmax(N, pred, truth, delta, error, c->stream), "xent");
+}
+
+int tns_hip_sum(tns_ctx* c, int64_t N, const float* src, int64_t offset, float* out) {
+  if (int r = check_ctx(c)) return r;
+  if (!src || !out || N < 0) return set_error(TNS_ERR_ARG, "sum: bad args");
+  return hip_status(launch_vssum(N, src + offset, out, c->stream), "sum");
+}
+
+int64_t tns_mlp_buffer_floats(int32_t nlayers, const int64_t* widths, int32_t bn, int64_t batch) {
+  if (nlayers <= 0 || nlayers > 32 || !widths) return -1;
+  return mlp_buffer_floats(nlayers, widths, bn, batch);
+}
+
+int tns_hip_mlp_train_step(tns_ctx* c, int32_t nlayers, const int64_t* widths,
+                           const int32_t* acts, int32_t bn, int64_t batch, const float* X,
+                           const float* truth, float learningRate, float momentum, float decay,
+                           float* buf, float* cost) {
+  if (int r = check_ctx(c)) return r;
+  if (nlayers <= 0 || nlayers > 32 || !widths || !acts || !X || !truth || !buf || !cost)
+    return set_error(TNS_ERR_ARG, "mlp_train_step: bad arguments");
+  if (batch < 2) return set_error(TNS_ERR_ARG, "mlp_train_step: batch must be >= 2 (BN)");
+  MlpArgs a;
+  a.nlayers = nlayers;
+  int64_t omax = 0;
+  for (int l = 0; l <= nlayers; ++l) {
+    if (widths[l] <= 0) return set_error(TNS_ERR_ARG, "mlp_train_step: width %d <= 0", l);
+    a.widths[l] = widths[l];
+    if (l > 0 && widths[l] > omax) omax = widths[l];
+  }
+  if (8 * batch * omax > 40960)
+    return set_error(TNS_ERR_ARG, "mlp_train_step: 8*batch*max(width) exceeds LDS staging");
+  for (int l = 0; l < nlayers; ++l) {
+    if (!act_supported(acts[l]))
+      return set_error(TNS_ERR_UNSUPPORTED, "mlp_train_step: activation %d", acts[l]);
+    a.acts[l] = acts[l];
+  }
+  a.bn = bn != 0;
+  a.batch = batch;
+  a.X = X;
+  a.truth = truth;
+  a.lr = learningRate;
+  a.momentum = momentum;
+  a.decay = decay;
+  a.buf = buf;
+  a.cost = cost;
+  return hip_status(launch_mlp_train_step(a, c->stream), "mlp_train_step");
 }
 
 // ---- layer drivers ------------------------------------------------------------

@@ -86,4 +86,45 @@ hipError_t launch_copy(int64_t n, const float* src, int64_t inca, float* dst, in
 hipError_t launch_clamp(int64_t n, float alpha, const float* src, float* dst, int64_t stride,
                         hipStream_t s);
 
+// ---- batch-norm / softmax (batchnorm.hip) ----------------------------------
+// x laid out [groups][N][bs]; one statistic per channel i in [0, N)
+hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
+                             float* vars, hipStream_t s);
+hipError_t launch_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
+                            int64_t mstride, const float* vars, int64_t vstride, hipStream_t s);
+hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales,
+                            const float* biases, int64_t incb, hipStream_t s);
+hipError_t launch_add_dots(float* dst, const float* a, const float* b, int64_t groups, int64_t N,
+                           int64_t bs, hipStream_t s);
+hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs,
+                           hipStream_t s);
+hipError_t launch_mean_var_delta(const float* delta, const float* x, const float* mean,
+                                 const float* var, int64_t groups, int64_t N, int64_t bs,
+                                 float* mean_delta, float* var_delta, hipStream_t s);
+hipError_t launch_normalize_delta(const float* x, const float* mean, const float* var,
+                                  const float* mean_delta, const float* var_delta, float* delta,
+                                  int64_t groups, int64_t N, int64_t bs, hipStream_t s);
+hipError_t launch_softmax_batch(int64_t n, const float* in, int64_t batch, int64_t batch_size,
+                                int64_t groups, int64_t group_size, int64_t stride, float temp,
+                                float* out, hipStream_t s);
+hipError_t launch_xent_softmax(int64_t n, const float* pred, const float* truth, float* delta,
+                               float* error, hipStream_t s);
+hipError_t launch_vssum(int64_t n, const float* a, float* out, hipStream_t s);
+
+// ---- fused connected-network train step (mlp_train.hip) ---------------------
+struct MlpArgs {
+  int nlayers;
+  int64_t widths[33];
+  int acts[32];
+  int bn;
+  int64_t batch;
+  const float* X;
+  const float* truth;
+  float lr, momentum, decay;
+  float* buf;   // packed parameters / state, layout of ora_mlp_train_step
+  float* cost;  // one float
+};
+int64_t mlp_buffer_floats(int nlayers, const int64_t* widths, int bn, int64_t batch);
+hipError_t launch_mlp_train_step(const MlpArgs& a, hipStream_t s);
+
 }  // namespace tns

@@ -181,3 +181,65 @@ class TNNHip:
                                             _ptr(weights), _ptr(biases), filters, kSize, stride,
                                             padding, dilation, int(activation), _ptr(workspace),
                                             _ptr(out), 1 if fused else 0))
+
+    # -- batch norm / softmax (TNNCuda.meansAndVars ... crossEntropySoftmax) ----
+    def meansAndVars(self, srcSize, dstSize, groups, src, offset, means, vars_):
+        check(self.lib.tns_hip_means_and_vars(self.ctx, srcSize, dstSize, groups, _ptr(src),
+                                              offset, _ptr(means), _ptr(vars_)))
+
+    def normalize(self, srcSize, dstSize, groups, means, meansStride, vars_, varsStride, dst,
+                  dstOffset):
+        check(self.lib.tns_hip_normalize(self.ctx, srcSize, dstSize, groups, _ptr(means),
+                                         meansStride, _ptr(vars_), varsStride, _ptr(dst),
+                                         dstOffset))
+
+    def forwardScale(self, dstSize, dst, offset, scaleSize, scale, incb, batch):
+        check(self.lib.tns_hip_forward_scale(self.ctx, dstSize, _ptr(dst), offset, scaleSize,
+                                             _ptr(scale), incb, batch))
+
+    def forwardScaleAdd(self, dstSize, dst, offset, scaleSize, scales, biases, incb, batch):
+        check(self.lib.tns_hip_forward_scale_add(self.ctx, dstSize, _ptr(dst), offset, scaleSize,
+                                                 _ptr(scales), _ptr(biases), incb, batch))
+
+    def meansAndVarsDelta(self, srcSize, dstSize, groups, delta, x, offset, mean, variance,
+                          mean_delta, variance_delta):
+        check(self.lib.tns_hip_means_and_vars_delta(
+            self.ctx, srcSize, dstSize, groups, _ptr(delta), _ptr(x), offset, _ptr(mean),
+            _ptr(variance), _ptr(mean_delta), _ptr(variance_delta)))
+
+    def normalizeDelta(self, deltaSize, meanSize, groups, delta, x, offset, mean, variance,
+                       mean_delta, variance_delta):
+        check(self.lib.tns_hip_normalize_delta(
+            self.ctx, deltaSize, meanSize, groups, _ptr(delta), _ptr(x), offset, _ptr(mean),
+            _ptr(variance), _ptr(mean_delta), _ptr(variance_delta)))
+
+    def addDots(self, N, dstSize, groups, src1, src2, srcOffset, dst):
+        check(self.lib.tns_hip_add_dots(self.ctx, N, dstSize, groups, _ptr(src1), _ptr(src2),
+                                        srcOffset, _ptr(dst)))
+
+    def softmaxBatch(self, N, input, iOffset, batch, batch_size, groups, group_size, stride, temp,
+                     output, oOffset):
+        check(self.lib.tns_hip_softmax_batch(self.ctx, N, _ptr(input), iOffset, batch,
+                                             batch_size, groups, group_size, stride, float(temp),
+                                             _ptr(output), oOffset))
+
+    def crossEntropySoftmax(self, N, pred, truth, delta, error):
+        check(self.lib.tns_hip_cross_entropy_softmax(self.ctx, N, _ptr(pred), _ptr(truth),
+                                                     _ptr(delta), _ptr(error)))
+
+    def sum(self, N, src, offset, out):
+        check(self.lib.tns_hip_sum(self.ctx, N, _ptr(src), offset, _ptr(out)))
+
+    # -- fused connected-network train step (config 5) ---------------------------
+    @staticmethod
+    def mlpBufferFloats(widths, bn, batch) -> int:
+        w = (C.c_int64 * len(widths))(*widths)
+        return int(load().tns_mlp_buffer_floats(len(widths) - 1, w, 1 if bn else 0, batch))
+
+    def mlpTrainStep(self, widths, acts, bn, batch, X, truth, lr, momentum, decay, buf, cost):
+        w = (C.c_int64 * len(widths))(*widths)
+        a = (C.c_int32 * len(acts))(*acts)
+        check(self.lib.tns_hip_mlp_train_step(self.ctx, len(widths) - 1, w, a, 1 if bn else 0,
+                                              batch, _ptr(X), _ptr(truth), float(lr),
+                                              float(momentum), float(decay), _ptr(buf),
+                                              _ptr(cost)))

@@ -1,0 +1,149 @@
+"""Batch-norm, softmax / cross-entropy device ops and the fused connected-
+network train step (BASELINE config 5) vs the oracle.
+
+Bar: sums in the reference's sequential order are bit-exact; anything through
+exp / ln / pow is within 1e-4 relative (plus 4 ulp); the whole train step's
+parameters after 1 and 5 steps within 1e-4 of their scale."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(torch, x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+@pytest.mark.parametrize("groups,N,bs", [(32, 64, 1), (32, 10, 1), (4, 8, 9), (2, 3, 2704)])
+def test_means_vars_normalize_scale(hip, torch_cuda, ora, groups, N, bs):
+    x = ora.uniform(groups * N * bs, 21, N, -2.0, 3.0)
+    m, v = ora.means_and_vars(x, groups, N, bs)
+    dx = dev(torch_cuda, x)
+    dm, dv = torch_cuda.zeros(N, device="cuda"), torch_cuda.zeros(N, device="cuda")
+    hip.meansAndVars(x.size, N, groups, dx, 0, dm, dv)
+    hip.finish()
+    if groups * bs <= 8192:
+        assert np.array_equal(dm.cpu().numpy(), m) and np.array_equal(dv.cpu().numpy(), v)
+    else:
+        assert np.allclose(dm.cpu().numpy(), m, rtol=1e-5, atol=1e-6)
+        assert np.allclose(dv.cpu().numpy(), v, rtol=1e-4)
+    y = ora.normalize(x.copy(), groups, N, bs, m, v)
+    hip.normalize(N, x.size, groups, dev(torch_cuda, m), 1, dev(torch_cuda, v), 1, dx, 0)
+    hip.finish()
+    assert np.array_equal(dx.cpu().numpy(), y)
+    s = ora.uniform(N, 22, N, 0.5, 1.5)
+    b = ora.uniform(N, 23, N, -0.2, 0.2)
+    y2 = ora.forward_scale(y.copy(), groups, N, bs, s)
+    y2 = ora.add_bias(y2, b, N, bs, groups)
+    hip.forwardScaleAdd(x.size, dx, 0, N, dev(torch_cuda, s), dev(torch_cuda, b), 1, groups)
+    hip.finish()
+    assert np.array_equal(dx.cpu().numpy(), y2)
+
+
+@pytest.mark.parametrize("groups,N,bs", [(32, 64, 1), (4, 8, 9)])
+def test_bn_backward_ops(hip, torch_cuda, ora, groups, N, bs):
+    n = groups * N * bs
+    x = ora.uniform(n, 31, N, -2.0, 2.0)
+    m, v = ora.means_and_vars(x, groups, N, bs)
+    xn = ora.normalize(x.copy(), groups, N, bs, m, v)
+    delta = ora.uniform(n, 32, N)
+    dsc = ora.uniform(N, 33, N)
+    ref_dsc = ora.add_dots(dsc.copy(), xn, delta, groups, N, bs)
+    md, vd = ora.mean_var_delta(delta, x, m, v, groups, N, bs)
+    ref_delta = ora.normalize_delta(x, m, v, md, vd, delta.copy(), groups, N, bs)
+    T = torch_cuda
+    d_dsc = dev(T, dsc)
+    hip.addDots(n, N, groups, dev(T, xn), dev(T, delta), 0, d_dsc)
+    dmd, dvd = T.zeros(N, device="cuda"), T.zeros(N, device="cuda")
+    d_delta = dev(T, delta)
+    hip.meansAndVarsDelta(n, N, groups, d_delta, dev(T, x), 0, dev(T, m), dev(T, v), dmd, dvd)
+    hip.normalizeDelta(n, N, groups, d_delta, dev(T, x), 0, dev(T, m), dev(T, v), dmd, dvd)
+    hip.finish()
+    assert np.array_equal(d_dsc.cpu().numpy(), ref_dsc)
+    assert np.array_equal(dmd.cpu().numpy(), md)
+    assert np.allclose(dvd.cpu().numpy(), vd, rtol=1e-6)
+    assert np.allclose(d_delta.cpu().numpy(), ref_delta, rtol=1e-5, atol=1e-6)
+
+
+def test_softmax_xent_sum(hip, torch_cuda, ora):
+    B, C = 32, 10
+    x = ora.uniform(B * C, 41, 0, -5.0, 5.0)
+    p = ora.softmax_rows(x, C)
+    T = torch_cuda
+    dx, dp = dev(T, x), T.zeros(B * C, device="cuda")
+    hip.softmaxBatch(C, dx, 0, B, C, 1, C, 1, 1.0, dp, 0)
+    hip.finish()
+    got = dp.cpu().numpy()
+    assert np.allclose(got, p, rtol=1e-6, atol=1e-8)
+    t = np.zeros(B * C, np.float32)
+    t[3::C] = 1.0
+    d, e = ora.softmax_xent(p, t)
+    dd, de = T.zeros(B * C, device="cuda"), T.zeros(B * C, device="cuda")
+    hip.crossEntropySoftmax(B * C, dev(T, p), dev(T, t), dd, de)
+    out = T.zeros(1, device="cuda")
+    hip.sum(B * C, de, 0, out)
+    hip.finish()
+    assert np.array_equal(dd.cpu().numpy(), d)
+    assert np.allclose(de.cpu().numpy(), e, rtol=1e-6)
+    assert abs(float(out.item()) - ora.vssum(e)) <= 1e-5 * abs(ora.vssum(e))
+
+
+def test_backward_bias_fc_sequential(hip, torch_cuda, ora):
+    B, O = 32, 64
+    src = ora.uniform(B * O, 51, 0)
+    dst = ora.uniform(O, 52, 0)
+    ref = ora.add_sums(dst.copy(), src, B, O, 1)
+    d = dev(torch_cuda, dst)
+    hip.backwardBias(O, d, src.size, dev(torch_cuda, src), 0, 1, B)
+    hip.finish()
+    assert np.array_equal(d.cpu().numpy(), ref)
+
+
+MNIST = ([784, 64, 64, 64, 64, 32, 10], [1, 1, 1, 1, 1, 4])
+
+
+def unpack(widths, bn, B, buf):
+    from test_oracle_train import unpack as up
+    return up(widths, bn, B, buf)
+
+
+@pytest.mark.parametrize("bn", [0, 1])
+@pytest.mark.parametrize("steps", [1, 5])
+def test_fused_mlp_train_step(hip, torch_cuda, ora, bn, steps):
+    widths, acts = MNIST
+    B = 32
+    buf = ora.mlp_init(widths, bn, B)
+    X, T_ = ora.mnist_batch(B)
+    T = torch_cuda
+    dbuf, dX, dT = dev(T, buf), dev(T, X), dev(T, T_)
+    dcost = T.zeros(1, device="cuda")
+    costs = []
+    for _ in range(steps):
+        costs.append(ora.mlp_train_step(widths, acts, bn, B, X, T_, 1e-2, 0.9, 1e-4, buf))
+        hip.mlpTrainStep(widths, acts, bn, B, dX, dT, 1e-2, 0.9, 1e-4, dbuf, dcost)
+    hip.finish()
+    got = dbuf.cpu().numpy()
+    assert abs(float(dcost.item()) - costs[-1]) <= 1e-4 * abs(costs[-1])
+    for l, (g, r) in enumerate(zip(unpack(widths, bn, B, got), unpack(widths, bn, B, buf))):
+        for name in g:
+            scale = float(np.abs(r[name]).max()) + 1e-12
+            err = float(np.abs(g[name].astype(np.float64) - r[name]).max())
+            assert err <= 1e-4 * scale, (l, name, err / scale)
+
+
+def test_fused_mlp_no_bn_is_bit_exact_one_step(hip, torch_cuda, ora):
+    """Without BN the only transcendental is softmax's exp (in double on both
+    sides), so one step should reproduce the oracle exactly."""
+    widths, acts = MNIST
+    B = 32
+    buf = ora.mlp_init(widths, 0, B)
+    X, T_ = ora.mnist_batch(B)
+    T = torch_cuda
+    dbuf = dev(T, buf)
+    dcost = T.zeros(1, device="cuda")
+    ora.mlp_train_step(widths, acts, 0, B, X, T_, 1e-2, 0.9, 1e-4, buf)
+    hip.mlpTrainStep(widths, acts, 0, B, dev(T, X), dev(T, T_), 1e-2, 0.9, 1e-4, dbuf, dcost)
+    hip.finish()
+    got = dbuf.cpu().numpy()
+    frac = float(np.mean(got == buf))
+    assert frac == 1.0, f"{(1 - frac) * 100:.4f}% of buffer elements differ"
