@@ -49,48 +49,11 @@ def parse():
     ap.add_argument("--yolo-steps", type=int, default=5)
     ap.add_argument("--no-yolo", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-batched", action="store_true")
+    ap.add_argument("--no-mnist", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU-baseline sample duration")
     return ap.parse_args()
-
-
-def dist_setup(n_gpus):
-    import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
-        return dist, rank, world, local
-    torch.cuda.set_device(0)
-    return None, 0, 1, 0
-
-
-def barrier(dist):
-    if dist is not None:
-        dist.barrier()
-
-
-def max_over_ranks(dist, x: float) -> float:
-    if dist is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def sum_over_ranks(dist, x: float) -> float:
-    if dist is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
 
 
 def synthetic(torch, shape, seed, lo=-1.0, hi=1.0):
@@ -99,7 +62,7 @@ def synthetic(torch, shape, seed, lo=-1.0, hi=1.0):
     return torch.rand(shape, generator=g, device="cuda", dtype=torch.float32) * (hi - lo) + lo
 
 
-def bench_sgemm(torch, hip, dist, rank, n, steps, warmup):
+def bench_sgemm(torch, hip, ctx, rank, n, steps, warmup):
     A = synthetic(torch, (n, n), 2 * 1000 + rank)
     B = synthetic(torch, (n, n), 2 * 1000 + 500 + rank)
     Cm = torch.zeros((n, n), device="cuda", dtype=torch.float32)
@@ -114,7 +77,7 @@ def bench_sgemm(torch, hip, dist, rank, n, steps, warmup):
     # (TNNHip attaches torch's current stream, so torch.cuda.Event records there)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(steps)]
-    barrier(dist)
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(steps):
@@ -122,14 +85,14 @@ def bench_sgemm(torch, hip, dist, rank, n, steps, warmup):
         step()
         ev[i][1].record()
     torch.cuda.synchronize()
-    barrier(dist)
+    ctx.barrier()
     t1 = time.perf_counter()
     wall = t1 - t0
     kern_ms = [a.elapsed_time(b) for a, b in ev]
     return wall, float(np.mean(kern_ms)), float(np.min(kern_ms))
 
 
-def bench_yolo(torch, hip, dist, rank, steps, warmup=1):
+def bench_yolo(torch, hip, ctx, rank, steps, warmup=1):
     from tensorium_amd.yolo import yolov3_conv_table
     specs = yolov3_conv_table()
     batch = 8
@@ -153,12 +116,12 @@ def bench_yolo(torch, hip, dist, rank, steps, warmup=1):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    barrier(dist)
+    ctx.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    barrier(dist)
+    ctx.barrier()
     wall = (time.perf_counter() - t0) / steps
     # per-op split with telemetry (synchronous per op, separate pass)
     hip.setTelemetry(True)
@@ -175,6 +138,79 @@ def bench_yolo(torch, hip, dist, rank, steps, warmup=1):
         "gemm_tflops": gflop / gemm_ms if gemm_ms > 0 else None,
         "im2col_gbs": (col_bytes + in_bytes) / (i2c_ms * 1e6) if i2c_ms > 0 else None,
     }
+
+
+def bench_batched(torch, hip, ctx, n_gemm=1024, n=1024, steps=3):
+    """Config 4: n_gemm independent n^3 GEMMs, contiguous shard per rank, one
+    strided-batched launch per step, operands generated on each device."""
+    from tensorium_amd.shard import shard_range
+    lo, hi = shard_range(n_gemm, ctx.rank, ctx.world)
+    mine = hi - lo
+    A = synthetic(torch, (mine, n, n), 4 * 1000 + lo)
+    B = synthetic(torch, (mine, n, n), 4 * 2000 + lo)
+    Cm = torch.empty((mine, n, n), device="cuda")
+
+    def step():
+        hip.gemmStridedBatched(False, False, n, n, n, 1.0, A, 0, n, n * n, B, 0, n, n * n, 0.0,
+                               Cm, 0, n, n * n, mine)
+
+    step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = ctx.max((time.perf_counter() - t0) / steps)
+    del A, B, Cm
+    torch.cuda.empty_cache()
+    flop = 2.0 * n ** 3 * n_gemm
+    return {"gemms_total": n_gemm, "gemm_size": n, "gemms_per_rank_max": -(-n_gemm // ctx.world),
+            "ms_per_batch": round(wall * 1e3, 4), "tflops_total": round(flop / wall / 1e12, 3),
+            "scaling": "strong (fixed 1024 GEMMs split over ranks)"}
+
+
+def bench_mnist(torch, hip, ctx, steps=200):
+    """Config 5: fused connected-network train step (784-64x4-32-10, BN,
+    softmax), batch 32, replicas per rank."""
+    from tensorium_amd.nnhip import TNNHip
+    widths = [784, 64, 64, 64, 64, 32, 10]
+    acts = [1, 1, 1, 1, 1, 4]
+    B = 32
+    nbuf = TNNHip.mlpBufferFloats(widths, True, B)
+    buf = torch.zeros(nbuf, device="cuda")
+    # W ~ U[-sqrt(2/in), sqrt(2/in)], scales 1 (TConnectedLayer.Create)
+    off = 0
+    for l in range(len(widths) - 1):
+        I, O = widths[l], widths[l + 1]
+        r = float(np.sqrt(2.0 / I))
+        buf[off:off + I * O] = synthetic(torch, (I * O,), 5 * 100 + l, -r, r)
+        off += 2 * I * O + 2 * O
+        buf[off:off + O] = 1.0
+        off += 4 * O + 4 * B * O + 4 * O
+    X = synthetic(torch, (B, 784), 5 * 1000 + ctx.rank, 0.0, 1.0)
+    lab = torch.randint(0, 10, (B,), device="cuda")
+    T = torch.zeros(B, 10, device="cuda")
+    T[torch.arange(B, device="cuda"), lab] = 1.0
+    cost = torch.zeros(1, device="cuda")
+
+    def step():
+        hip.mlpTrainStep(widths, acts, True, B, X, T, 1e-3, 0.9, 1e-4, buf, cost)
+
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = ctx.max((time.perf_counter() - t0) / steps)
+    return {"batch": B, "net": "784-64-64-64-64-32-10 relu/linear + BN + softmax",
+            "us_per_step": round(wall * 1e6, 2), "steps_per_s_total": round(ctx.world / wall, 1),
+            "kernels_per_step": 1, "cost_after": round(float(cost.item()), 4)}
 
 
 def cpu_baseline(n, target_s):
@@ -223,13 +259,15 @@ def traffic_from_profiles(n):
 def main():
     args = parse()
     import torch
-    dist, rank, world, local = dist_setup(args.gpus)
+    from tensorium_amd import dist as tdist
+    ctx = tdist.init("nccl")
+    rank, world, local = ctx.rank, ctx.world, ctx.local
     from tensorium_amd.nnhip import TNNHip
     hip = TNNHip(local)
     n = args.size
 
-    wall, kern_ms, kern_min = bench_sgemm(torch, hip, dist, rank, n, args.steps, args.warmup)
-    wall = max_over_ranks(dist, wall)
+    wall, kern_ms, kern_min = bench_sgemm(torch, hip, ctx, rank, n, args.steps, args.warmup)
+    wall = ctx.max(wall)
     flop = 2.0 * n * n * n
     ms_per_step = wall / args.steps * 1e3
     value = world * flop / (ms_per_step / 1e3) / 1e9   # GFLOP/s, whole job
@@ -238,11 +276,14 @@ def main():
 
     yolo = None
     if not args.no_yolo and args.yolo_steps > 0:
-        y = bench_yolo(torch, hip, dist, rank, args.yolo_steps)
-        ms = max_over_ranks(dist, y["ms_per_batch"])
+        y = bench_yolo(torch, hip, ctx, rank, args.yolo_steps)
+        ms = ctx.max(y["ms_per_batch"])
         y["ms_per_batch"] = ms
         y["images_per_s"] = world * y["batch_per_gpu"] / (ms / 1e3)
         yolo = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in y.items()}
+
+    batched = None if args.no_batched else bench_batched(torch, hip, ctx)
+    mnist = None if args.no_mnist else bench_mnist(torch, hip, ctx)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -277,12 +318,13 @@ def main():
                          "algorithmic_flop_per_launch": flop},
             "cpu_baseline": cpu,
             "yolo": yolo,
+            "batched_gemm": batched,
+            "mnist_train": mnist,
         }
         print(json.dumps(line), flush=True)
     hip.finish()
     hip.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    ctx.close()
 
 
 if __name__ == "__main__":

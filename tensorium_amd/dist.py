@@ -1,0 +1,79 @@
+"""One-process-per-GPU plumbing for the benchmark and multi-GPU runs.
+
+torch.distributed is used only for rendezvous, barriers and scalar
+reductions (timing max, checksums): the GEMM data path has no collective
+(SURVEY §8e).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU
+tests.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+
+@dataclass
+class DistCtx:
+    dist: object | None
+    rank: int
+    world: int
+    local: int
+    device: str
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def _reduce(self, x: float, op_name: str) -> float:
+        if self.dist is None:
+            return float(x)
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op_name))
+        return float(t.item())
+
+    def max(self, x: float) -> float:
+        return self._reduce(x, "MAX")
+
+    def sum(self, x: float) -> float:
+        return self._reduce(x, "SUM")
+
+    def gather_floats(self, xs: list[float]) -> list[list[float]]:
+        """All-gather a short list of floats from every rank (equal lengths)."""
+        if self.dist is None:
+            return [list(xs)]
+        import torch
+        t = torch.tensor(xs, dtype=torch.float64, device=self.device)
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [o.tolist() for o in out]
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+            self.dist = None
+
+
+def init(backend: str | None = None) -> DistCtx:
+    """Initialise from RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* (torchrun).
+    Single process when WORLD_SIZE is unset or 1."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    device = "cpu"
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        device = f"cuda:{local}"
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local)
+    if world <= 1:
+        return DistCtx(None, 0, 1, local, device)
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {}
+    if backend == "nccl":
+        kw["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return DistCtx(dist, rank, world, local, device)
