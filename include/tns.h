@@ -290,8 +290,13 @@ int tns_hip_conv2d(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
 
 /* TConvolutionalLayer.forward / forwardGPU with fused (folded) BN —
  * nConvolutionLayer.pas:457-569 / 1022-1153: Conv2D -> forwardBias ->
- * activate.  fused=1 runs bias+activation in the SGEMM epilogue (same
- * arithmetic, one fewer HBM pass); fused=0 runs the three reference stages. */
+ * activate.  fused selects the schedule (same arithmetic, same bits, in all):
+ *   TNS_CONV_UNFUSED  (0) the three reference stages (im2col, GEMM, bias+act)
+ *   TNS_CONV_FUSED    (1) library's choice among the two below
+ *   TNS_CONV_IM2COL   (2) im2col into workspace + SGEMM with bias+act epilogue
+ *   TNS_CONV_IMPLICIT (3) implicit GEMM: the SGEMM gathers its B tiles from
+ *                         the image (no col matrix, workspace unused) */
+enum { TNS_CONV_UNFUSED = 0, TNS_CONV_FUSED = 1, TNS_CONV_IM2COL = 2, TNS_CONV_IMPLICIT = 3 };
 int tns_hip_conv_forward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
                          const float* input, const float* weights, const float* biases,
                          int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
@@ -322,8 +327,10 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
                          int64_t batchCount);
 
 /* TNS_OPT_STRICT_BETA0 (default 1): beta==0 computes 0*C like the reference
- * (NaN/Inf in C propagate).  0 = BLAS convention (C not read). */
-enum { TNS_OPT_STRICT_BETA0 = 0 };
+ * (NaN/Inf in C propagate).  0 = BLAS convention (C not read).
+ * TNS_OPT_CONV_VARIANT (default -1 = heuristic): forces the tile shape of the
+ * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name). */
+enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

@@ -24,6 +24,32 @@ int64_t out_dim(int64_t in, int64_t pad, int64_t k, int64_t dil, int64_t stride)
 }
 
 namespace {
+// k-table of the implicit-GEMM convolution: the im2col row k = (c, kr, kc)
+// reads im[c][ir0 + kr*dY][ic0 + kc*dX] for the output pixel whose window
+// starts at (ir0, ic0) — the same element sim2Col copies (ntensors.pas:11460).
+__global__ void ktab_kernel(int4* t, int K, int H, int W, int kH, int kW, int dY, int dX) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k > K) return;
+  if (k == K) {  // sentinel for k >= K: the row check always fails
+    t[k] = make_int4(0, 0x40000000, 0x40000000, 0);
+    return;
+  }
+  const int kc = k % kW, r = k / kW;
+  const int kr = r % kH, c = r / kH;
+  t[k] = make_int4(c * H * W + kr * dY * W + kc * dX, kr * dY, kc * dX, 0);
+}
+}  // namespace
+
+hipError_t launch_build_ktab(int4* ktab, int C, int H, int W, int kH, int kW, int dY, int dX,
+                             hipStream_t s) {
+  const int K = C * kH * kW;  // K + 1 entries (sentinel last)
+  if (K < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ktab_kernel, dim3((K + 256) / 256), dim3(256), 0, s, ktab, K, H, W, kH, kW,
+                     dY, dX);
+  return hipGetLastError();
+}
+
+namespace {
 
 struct I2CArgs {
   int C, H, W, kH, kW, padH, padW, sY, sX, dY, dX, oh, ow;

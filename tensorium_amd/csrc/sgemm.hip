@@ -1,6 +1,8 @@
 // sgemm.hip — SGEMM dispatch: tile-shape choice per problem and the variant
 // table used by the tuning entry point (tns_hip_gemm_variant).  The kernel
 // itself (MFMA main loop, numerics notes) is in sgemm_kernel.hpp.
+#include <cmath>
+
 #include "sgemm_kernel.hpp"
 
 namespace tns {
@@ -17,7 +19,10 @@ const VariantInfo kVariants[] = {TNS_SHAPES(TNS_ROW)};
 #undef TNS_ROW
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-enum { V_128x128 = 0, V_128x64 = 1, V_64x128 = 2, V_64x256 = 3, V_32x256 = 4, V_256x256w8 = 5 };
+enum {
+  V_128x128 = 0, V_128x64 = 1, V_64x128 = 2, V_64x256 = 3, V_32x256 = 4, V_256x256w8 = 5,
+  V_64x64 = 6
+};
 
 // float4 staging needs 16-B aligned rows and a contiguous extent that is a
 // multiple of 4 (so every float4 is wholly inside or outside the operand).
@@ -35,13 +40,58 @@ int pick_variant(const GemmArgs& a, bool av, bool bv) {
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch; };
   if (M <= 32) return V_32x256;
   if (M <= 64) return V_64x256;
-  if (blocks(256, 256) >= 240 && av && bv) return V_256x256w8;
-  if (blocks(128, 128) >= 200) return V_128x128;
-  if (blocks(128, 64) >= 200 || M <= 128) return V_128x64;
-  return V_64x128;
+  if (M >= 256 && blocks(256, 256) >= 240 && av && bv) return V_256x256w8;
+  if (N >= 1024) return V_64x128;
+  return V_128x64;
+}
+
+// Implicit-GEMM conv tile choice.  No split-K (bit-exactness), so the
+// parallelism is the output tiles alone: estimate each shape's time as
+// (rounds of resident blocks) x (tile area / relative per-CU efficiency) and
+// take the cheapest.  Two 256-thread blocks are resident per CU.
+int pick_conv_variant(const GemmArgs& a) {
+  struct Cand { int v, bm, bn; double eff; };
+  static const Cand cands[] = {{V_128x128, 128, 128, 1.00}, {V_128x64, 128, 64, 0.92},
+                               {V_64x128, 64, 128, 0.92},   {V_64x64, 64, 64, 0.70},
+                               {V_64x256, 64, 256, 0.95},   {V_32x256, 32, 256, 0.60}};
+  const double slots = 512.0;
+  int best = V_128x64;
+  double best_t = 1e300;
+  for (const Cand& c : cands) {
+    const double tiles_m = (double)((a.M + c.bm - 1) / c.bm);
+    const double tiles_n = (double)((a.N + c.bn - 1) / c.bn);
+    const double rounds = std::ceil(tiles_m * tiles_n / slots);
+    const double t = rounds * c.bm * c.bn / c.eff;
+    if (t < best_t) {
+      best_t = t;
+      best = c.v;
+    }
+  }
+  return best;
 }
 
 }  // namespace
+
+hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0 || a.batch <= 0) return hipSuccess;
+  if (!a.conv || !a.ktab) return hipErrorInvalidValue;
+  const bool av = vec4_ok(a.A, a.lda, a.strideA, a.batch, a.K);
+  const int v = variant < 0 ? pick_conv_variant(a) : variant;
+  switch (v) {
+    case V_128x128: return launch_conv_128x128(a, av, s);
+    case V_128x64: return launch_conv_128x64(a, av, s);
+    case V_64x128: return launch_conv_64x128(a, av, s);
+    case V_64x256: return launch_conv_64x256(a, av, s);
+    case V_32x256: return launch_conv_32x256(a, av, s);
+    case V_256x256w8: return launch_conv_256x256w8(a, av, s);
+    case V_64x64: return launch_conv_64x64(a, av, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s) {
+  return launch_sgemm_conv_variant(-1, a, s);
+}
 
 int sgemm_variant_count() { return kNumVariants; }
 const char* sgemm_variant_name(int v) { return (v >= 0 && v < kNumVariants) ? kVariants[v].name : ""; }

@@ -26,3 +26,4 @@ hipError_t launch_shape_256x128k16(const GemmArgs& a, bool ta, bool tb, bool av,
 }
 
 }  // namespace tns
+

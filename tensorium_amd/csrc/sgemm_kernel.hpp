@@ -25,6 +25,7 @@
 //   tile's MFMAs and written to LDS after them.  The block index is remapped
 //   so each of the 8 XCDs sweeps a contiguous, grouped region of C.
 #pragma once
+#include <type_traits>
 #include "tns_act.hpp"
 #include "tns_internal.hpp"
 
@@ -44,11 +45,17 @@ struct LdsLd {
   static constexpr int value = KCONTIG ? BMN + 1 : BMN;
 };
 
+// 16 zero bytes every out-of-range staging load reads instead of the operand.
+__device__ __attribute__((aligned(16))) static float4 g_zero_page;
+__device__ __forceinline__ const float* zero_page() {
+  return reinterpret_cast<const float*>(&g_zero_page);
+}
+
 // Loads one BK x BMN operand tile (k, mn) into E registers per thread.
 //   KCONTIG:  element (k, mn) at base[(mn0+mn)*ld + k0+k]   (A NoTrans / B Trans)
 //   else   :  element (k, mn) at base[(k0+k)*ld + mn0+mn]   (A Trans / B NoTrans)
 // Out-of-range elements read as 0.  Branch-free: an out-of-range load is
-// redirected to element 0 of the operand and its value replaced by 0.  VEC=4
+// redirected to the zero page.  VEC=4
 // is only instantiated when the contiguous extent is a multiple of 4 (the
 // host checks), so a float4 is either wholly inside or wholly outside.
 template <bool KCONTIG, int VEC, int BK, int BMN, int NT>
@@ -71,17 +78,18 @@ struct TileIO {
         gk = k0 + idx / (BMN / VEC);
         gmn = mn0 + VEC * (idx % (BMN / VEC));
       }
-      const bool ok = (gmn < MN) && (gk < K);
-      const int64_t off = ok ? (KCONTIG ? gmn * ld + gk : gk * ld + gmn) : 0;
+      const bool ok = (gmn < MN) & (gk < K);
+      // out of range: read the zero page instead (no select on the loaded
+      // value, so nothing forces an early wait on the load)
+      const float* src = ok ? base + (KCONTIG ? gmn * ld + gk : gk * ld + gmn) : zero_page();
       if constexpr (VEC == 4) {
-        float4 v = *reinterpret_cast<const float4*>(base + off);
-        r[4 * it + 0] = ok ? v.x : 0.0f;
-        r[4 * it + 1] = ok ? v.y : 0.0f;
-        r[4 * it + 2] = ok ? v.z : 0.0f;
-        r[4 * it + 3] = ok ? v.w : 0.0f;
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        r[4 * it + 0] = v.x;
+        r[4 * it + 1] = v.y;
+        r[4 * it + 2] = v.z;
+        r[4 * it + 3] = v.w;
       } else {
-        const float v = base[off];
-        r[it] = ok ? v : 0.0f;
+        r[it] = *src;
       }
     }
   }
@@ -116,6 +124,70 @@ struct TileIO {
   }
 };
 
+// Implicit-GEMM B operand of a convolution: element (k, n) of the im2col
+// matrix, k = (c, kr, kc), n = (image, orow, ocol), read straight from the
+// images.  Each thread owns one column n for the whole launch (NT % BN == 0)
+// and walks k; k is wave-uniform, so its k-table entry is a scalar load,
+// fetched one k-tile ahead.  Same values as sim2Col (zero outside the
+// image) => bit-identical GEMM.
+template <int BK, int BN, int NT>
+struct ConvBIO {
+  static_assert(NT % BN == 0, "conv staging needs NT % BN == 0");
+  static constexpr int E = BK * BN / NT;
+  static constexpr int KSTEP = NT / BN;
+  static constexpr int LD = BN;
+  struct State {
+    int base;      // image offset of the window origin (may be negative)
+    int ir0, ic0;  // window origin row / column
+    bool nok;
+  };
+  __device__ static __forceinline__ State init(const GemmArgs& p, int64_t n0, int tid) {
+    const int64_t n = n0 + tid % BN;
+    State st;
+    st.nok = n < p.N;
+    const int nn = st.nok ? (int)n : 0;
+    const int img = nn / p.conv_ohw;
+    const int pix = nn - img * p.conv_ohw;
+    const int orow = pix / p.conv_ow;
+    const int ocol = pix - orow * p.conv_ow;
+    st.ir0 = orow * p.conv_sY - p.conv_pH;
+    st.ic0 = ocol * p.conv_sX - p.conv_pW;
+    st.base = img * (int)p.strideB + st.ir0 * p.conv_W + st.ic0;
+    return st;
+  }
+  // ktab has K+1 entries; entry K is a sentinel whose row offset fails the
+  // bounds check, so k >= K needs no post-processing of the loaded entry.
+  __device__ static __forceinline__ void fetch(int4 (&tab)[E], const int4* __restrict__ ktab,
+                                               int k0, int K, int tid) {
+    const int kl = __builtin_amdgcn_readfirstlane(tid / BN);  // wave-uniform
+#pragma unroll
+    for (int it = 0; it < E; ++it) {
+      const int k = k0 + kl + KSTEP * it;
+      tab[it] = ktab[k < K ? k : K];
+    }
+  }
+  __device__ static __forceinline__ void load(float (&r)[E], const float* __restrict__ im,
+                                              const State& st, const int4 (&tab)[E], int H,
+                                              int W) {
+#pragma unroll
+    for (int it = 0; it < E; ++it) {
+      const int4 t = tab[it];
+      // bitwise &: no short-circuit control flow around the loads
+      const bool ok = st.nok & ((unsigned)(st.ir0 + t.y) < (unsigned)H) &
+                      ((unsigned)(st.ic0 + t.z) < (unsigned)W);
+      r[it] = *(ok ? im + (unsigned)(st.base + t.x) : zero_page());
+    }
+  }
+  __device__ static __forceinline__ void store(const float (&r)[E], float* __restrict__ xs,
+                                               int tid) {
+#pragma unroll
+    for (int it = 0; it < E; ++it) {
+      const int idx = tid + NT * it;
+      xs[(idx / BN) * LD + idx % BN] = r[it];
+    }
+  }
+};
+
 // XCD-aware, grouped mapping of a linear block id onto (tile_m, tile_n).
 __device__ __forceinline__ void map_tile(int bid, int tiles_m, int tiles_n, int& tm, int& tn) {
   const int nb = tiles_m * tiles_n;
@@ -133,9 +205,14 @@ __device__ __forceinline__ void map_tile(int bid, int tiles_m, int tiles_n, int&
   tn = in_group / gsize;
 }
 
-template <int BM_, int BN_, int BK_, int WM_, int WN_, int MINW_>
+// DEPTH_: how many k-tiles ahead the global loads run (register stages).
+// Small tiles spend few cycles per k-tile, so one tile of lead does not cover
+// the global-load latency; they load two tiles ahead.
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int MINW_, int DEPTH_ = 1>
 struct Shape {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_, MINW = MINW_;
+  static constexpr int DEPTH = DEPTH_;
+  static_assert(DEPTH == 1 || DEPTH == 2, "prefetch depth 1 or 2");
   static constexpr int NT = 64 * WM * WN;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -162,14 +239,14 @@ __device__ __forceinline__ void mma_steps(floatx16 (&acc)[TM][TN], const float* 
   }
 }
 
-template <class S, bool TA, bool TB, int AV, int BV>
+template <class S, bool TA, bool TB, int AV, int BV, bool CONV = false>
 __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) {
   constexpr int BM = S::BM, BN = S::BN, BK = S::BK, NT = S::NT;
   constexpr int TM = S::TM, TN = S::TN, WTM = S::WTM, WTN = S::WTN;
   constexpr bool AKC = !TA;  // A is k-contiguous in memory
   constexpr bool BKC = TB;   // B is k-contiguous in memory
   using AIO = TileIO<AKC, AV, BK, BM, NT>;
-  using BIO = TileIO<BKC, BV, BK, BN, NT>;
+  using BIO = std::conditional_t<CONV, ConvBIO<BK, BN, NT>, TileIO<BKC, BV, BK, BN, NT>>;
   constexpr int LDA_S = AIO::LD, LDB_S = BIO::LD;
   constexpr int A_TILE = BK * LDA_S;
   constexpr int B_TILE = BK * LDB_S;
@@ -190,10 +267,20 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
   const int64_t m0 = (int64_t)tm_ * BM, n0 = (int64_t)tn_ * BN;
   const int64_t bz = blockIdx.y;
 
+  // (conv: batch folded into N, launched with one z-slice)
   const float* __restrict__ A = p.A + bz * p.strideA;
-  const float* __restrict__ B = p.B + bz * p.strideB;
-  float* __restrict__ C = p.C + bz * p.strideC;
+  const float* __restrict__ B = CONV ? p.B : p.B + bz * p.strideB;
+  float* __restrict__ C = CONV ? p.C : p.C + bz * p.strideC;
   const int64_t M = p.M, N = p.N, K = p.K;
+  // element (row, col) of C; conv columns are (image, pixel)
+  auto c_at = [&](int64_t row, int64_t col) -> int64_t {
+    if constexpr (CONV) {
+      const int img = (int)col / p.conv_ohw;
+      return (int64_t)img * p.strideC + row * p.ldc + ((int)col - img * p.conv_ohw);
+    } else {
+      return row * p.ldc + col;
+    }
+  };
 
   // ---- accumulator init: 0, C, or beta*C (reference mulvs pre-scale) -----
   floatx16 acc[TM][TN];
@@ -205,7 +292,7 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-  if (p.beta_mode != BETA_ZERO) {
+  if (!CONV && p.beta_mode != BETA_ZERO) {  // (conv output is write-only)
     const bool scale = p.beta_mode == BETA_SCALE;
     const float beta = p.beta;
 #pragma unroll
@@ -217,7 +304,7 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
           const int64_t row = row_base + i * 32 + (e & 3) + 8 * (e >> 2);
           const int64_t col = col_base + j * 32;
           const bool ok = row < M && col < N;
-          float v = C[ok ? row * p.ldc + col : 0];
+          float v = C[ok ? c_at(row, col) : 0];
           v = scale ? beta * v : v;
           acc[i][j][e] = ok ? v : 0.0f;
         }
@@ -229,39 +316,80 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
   float ra[AIO::E], rb[BIO::E];
   const int a_off = h * LDA_S + wm * WTM + l31;
   const int b_off = h * LDB_S + wn * WTN + l31;
+  using CIO = ConvBIO<BK, BN, NT>;
+  [[maybe_unused]] typename CIO::State cst;
+  [[maybe_unused]] int4 ktab_next[CIO::E];
+  if constexpr (CONV) {
+    cst = CIO::init(p, n0, tid);
+    CIO::fetch(ktab_next, p.ktab, 0, (int)K, tid);
+  }
+  auto load_b = [&](float (&r)[BIO::E], int64_t k0) {
+    if constexpr (CONV) {
+      CIO::load(r, B, cst, ktab_next, p.conv_H, p.conv_W);
+      CIO::fetch(ktab_next, p.ktab, (int)k0 + BK, (int)K, tid);  // next tile's entries
+    } else {
+      BIO::load(r, B, p.ldb, n0, k0, N, K, tid);
+    }
+  };
+
+  // k-tile pipeline: tile t is multiplied out of LDS buffer t&1 while tile
+  // t+1 is written into the other buffer (from registers loaded DEPTH tiles
+  // earlier) and tile t+DEPTH is loaded into registers.  One barrier per tile.
+  // Loads past the last tile read the zero page; stores past it land in a
+  // buffer that is never read again.
+  auto scale = [&](float (&r)[AIO::E]) {
+    if (scale_a) {
+#pragma unroll
+      for (int i = 0; i < AIO::E; ++i) r[i] = alpha * r[i];  // A_PART = ALPHA*A[kk]
+    }
+  };
+  auto step = [&](float (&lra)[AIO::E], float (&lrb)[BIO::E], float (&sra)[AIO::E],
+                  float (&srb)[BIO::E], int t, auto PAR) {
+    constexpr int par = decltype(PAR)::value;  // == t & 1
+    const float* as = smem + par * STAGE;
+    float* nxt = smem + (par ^ 1) * STAGE;
+    // unconditional: past the last tile every lane reads the zero page (a
+    // branch here would merge the wait counters and force an early wait)
+    const int64_t kl = (int64_t)(t + S::DEPTH) * BK;
+    AIO::load(lra, A, p.lda, m0, kl, M, K, tid);
+    load_b(lrb, kl);
+    constexpr int SP = BK / 4;
+    mma_steps<TM, TN, LDA_S, LDB_S, 0, SP>(acc, as + a_off, as + A_TILE + b_off);
+    scale(sra);
+    AIO::store(sra, nxt, tid);
+    BIO::store(srb, nxt + A_TILE, tid);
+    mma_steps<TM, TN, LDA_S, LDB_S, SP, BK / 2>(acc, as + a_off, as + A_TILE + b_off);
+    __syncthreads();
+  };
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
 
   if (nt > 0) {
     AIO::load(ra, A, p.lda, m0, 0, M, K, tid);
-    BIO::load(rb, B, p.ldb, n0, 0, N, K, tid);
-    if (scale_a) {
-#pragma unroll
-      for (int i = 0; i < AIO::E; ++i) ra[i] = alpha * ra[i];  // A_PART = ALPHA*A[kk]
-    }
+    load_b(rb, 0);
+    scale(ra);
     AIO::store(ra, smem, tid);
     BIO::store(rb, smem + A_TILE, tid);
-    __syncthreads();
-
-    for (int t = 0; t < nt - 1; ++t) {
-      const float* as = smem + (t & 1) * STAGE;
-      float* nxt = smem + ((t + 1) & 1) * STAGE;
-      const int64_t k0 = (int64_t)(t + 1) * BK;
-      // next tile's global loads first: their latency hides under the MFMAs
-      AIO::load(ra, A, p.lda, m0, k0, M, K, tid);
-      BIO::load(rb, B, p.ldb, n0, k0, N, K, tid);
-      mma_steps<TM, TN, LDA_S, LDB_S, 0, BK / 4>(acc, as + a_off, as + A_TILE + b_off);
-      // the other buffer was last read before the previous barrier: safe to
-      // fill it mid-tile, between two halves of this tile's MFMAs
-      if (scale_a) {
-#pragma unroll
-        for (int i = 0; i < AIO::E; ++i) ra[i] = alpha * ra[i];
-      }
-      AIO::store(ra, nxt, tid);
-      BIO::store(rb, nxt + A_TILE, tid);
-      mma_steps<TM, TN, LDA_S, LDB_S, BK / 4, BK / 2>(acc, as + a_off, as + A_TILE + b_off);
+    if constexpr (S::DEPTH == 1) {
       __syncthreads();
+      // registers are reloaded each tile and stored in the same tile
+      for (int t = 0; t < nt; t += 2) {
+        step(ra, rb, ra, rb, t, P0{});
+        if (t + 1 >= nt) break;
+        step(ra, rb, ra, rb, t + 1, P1{});
+      }
+    } else {
+      float ra2[AIO::E], rb2[BIO::E];
+      AIO::load(ra2, A, p.lda, m0, BK, M, K, tid);
+      load_b(rb2, BK);
+      __syncthreads();
+      // (ra2, rb2) hold tile t+1 at even t; (ra, rb) at odd t
+      for (int t = 0; t < nt; t += 2) {
+        step(ra, rb, ra2, rb2, t, P0{});
+        if (t + 1 >= nt) break;
+        step(ra2, rb2, ra, rb, t + 1, P1{});
+      }
     }
-    const float* as = smem + ((nt - 1) & 1) * STAGE;
-    mma_steps<TM, TN, LDA_S, LDB_S, 0, BK / 2>(acc, as + a_off, as + A_TILE + b_off);
   }
 
   // ---- epilogue ----------------------------------------------------------
@@ -280,11 +408,11 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
         if (col >= N) continue;
         float v = acc[i][j][e];
         if (fuse) v = act_apply(v + bias, act);  // forwardBias then activate
-        C[row * p.ldc + col] = v;
+        C[c_at(row, col)] = v;
       }
     }
 }
-template <class S, bool TA, bool TB, int AV, int BV>
+template <class S, bool TA, bool TB, int AV, int BV, bool CONV = false>
 hipError_t launch_variant(const GemmArgs& a, hipStream_t s) {
   const int64_t tiles = ((a.M + S::BM - 1) / S::BM) * ((a.N + S::BN - 1) / S::BN);
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
@@ -295,7 +423,7 @@ hipError_t launch_variant(const GemmArgs& a, hipStream_t s) {
     sub.B = a.B + b0 * a.strideB;
     sub.C = a.C + b0 * a.strideC;
     sub.batch = nb;
-    hipLaunchKernelGGL((sgemm_mfma_kernel<S, TA, TB, AV, BV>), dim3((unsigned)tiles, (unsigned)nb),
+    hipLaunchKernelGGL((sgemm_mfma_kernel<S, TA, TB, AV, BV, CONV>), dim3((unsigned)tiles, (unsigned)nb),
                        dim3(S::NT), 0, s, sub);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -330,6 +458,13 @@ hipError_t launch_trans4(const GemmArgs& a, bool ta, bool tb, bool av, bool bv, 
   return launch_variant<S, true, true, 4, 4>(a, s);
 }
 
+// implicit-GEMM convolution: NN, A (weights) float4 or scalar, B from the image
+template <class S>
+hipError_t launch_conv(const GemmArgs& a, bool av, hipStream_t s) {
+  if (av) return launch_variant<S, false, false, 4, 1, true>(a, s);
+  return launch_variant<S, false, false, 1, 1, true>(a, s);
+}
+
 // experimental tile shapes: NN with float4 operands only
 template <class S>
 hipError_t launch_nn4(const GemmArgs& a, bool ta, bool tb, bool av, bool bv, hipStream_t s) {
@@ -339,8 +474,9 @@ hipError_t launch_nn4(const GemmArgs& a, bool ta, bool tb, bool av, bool bv, hip
 
 //                 BM   BN  BK WM WN MINW
 using S128x128 = Shape<128, 128, 32, 2, 2, 2>;
-using S128x64 = Shape<128, 64, 32, 2, 2, 2>;
-using S64x128 = Shape<64, 128, 32, 2, 2, 2>;
+using S128x64 = Shape<128, 64, 32, 2, 2, 2, 2>;
+using S64x64 = Shape<64, 64, 32, 2, 2, 2, 2>;
+using S64x128 = Shape<64, 128, 32, 2, 2, 2, 2>;
 using S64x256 = Shape<64, 256, 32, 1, 4, 2>;
 using S32x256 = Shape<32, 256, 32, 1, 4, 2>;
 using S256x256 = Shape<256, 256, 32, 2, 2, 1>;
@@ -349,6 +485,7 @@ using S256x128 = Shape<256, 128, 32, 2, 2, 1>;
 using S128x256 = Shape<128, 256, 32, 2, 2, 1>;
 using S256x256w8 = Shape<256, 256, 32, 2, 4, 2>;
 using S256x128k16 = Shape<256, 128, 16, 2, 2, 2>;
+
 
 }  // namespace sgemm_detail
 
@@ -361,6 +498,7 @@ typedef hipError_t (*ShapeLauncher)(const GemmArgs&, bool, bool, bool, bool, hip
   X(64x256, "64x256x32_w1x4", 64, 256, launch_full)      \
   X(32x256, "32x256x32_w1x4", 32, 256, launch_full)      \
   X(256x256w8, "256x256x32_w2x4", 256, 256, launch_trans4) \
+  X(64x64, "64x64x32_w2x2", 64, 64, launch_full)          \
   X(256x256, "256x256x32_w2x2", 256, 256, launch_nn4)    \
   X(256x256k16, "256x256x16_w2x2", 256, 256, launch_nn4) \
   X(256x128, "256x128x32_w2x2", 256, 128, launch_nn4)    \
@@ -371,5 +509,14 @@ typedef hipError_t (*ShapeLauncher)(const GemmArgs&, bool, bool, bool, bool, hip
   hipError_t launch_shape_##ID(const GemmArgs&, bool, bool, bool, bool, hipStream_t);
 TNS_SHAPES(TNS_DECL)
 #undef TNS_DECL
+
+// implicit-GEMM conv launchers for the production shapes
+hipError_t launch_conv_128x128(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_128x64(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x128(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x256(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_32x256(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_256x256w8(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x64(const GemmArgs&, bool, hipStream_t);
 
 }  // namespace tns

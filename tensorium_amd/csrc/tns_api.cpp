@@ -11,11 +11,14 @@
 // gfx950 kernel or fails with a status.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 
 #include "tns_internal.hpp"
 
@@ -24,6 +27,7 @@ namespace tns {
 static thread_local std::string g_err;
 static tns_error_hook_t g_hook = nullptr;
 static int64_t g_strict_beta0 = 1;
+static int64_t g_conv_variant = -1;
 
 int set_error(int code, const char* fmt, ...) {
   char buf[1024];
@@ -54,6 +58,8 @@ struct tns_ctx {
   double op_ms[TNS_OP_COUNT] = {0};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // serialises host-API use of one context
+  // implicit-GEMM conv k-tables, one per (C, H, W, kH, kW, dY, dX)
+  std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int4*> ktabs;
 };
 
 namespace {
@@ -126,7 +132,7 @@ int do_gemm(tns_ctx* c, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float
   if (!C || (K > 0 && (!A || !B))) return set_error(TNS_ERR_ARG, "gemm: null operand");
   if (epi == EPI_BIAS_ACT && (!bias || !act_supported(act)))
     return set_error(TNS_ERR_ARG, "gemm: bad fused epilogue");
-  GemmArgs a;
+  GemmArgs a{};
   a.M = M; a.N = N; a.K = K;
   a.alpha = alpha; a.beta = beta;
   a.beta_mode = (c_write_only && beta == 0.0f) ? BETA_ZERO : beta_mode_for(beta);
@@ -160,6 +166,31 @@ int check_geom(const ConvGeom& g) {
   if (g.C * g.kH * g.kW * (g.oh > 0 ? g.oh : 1) * (g.ow > 0 ? g.ow : 1) > 0x7fffffffLL ||
       g.C * g.H * g.W > 0x7fffffffLL)
     return set_error(TNS_ERR_ARG, "im2col: image too large for 32-bit indexing");
+  return TNS_OK;
+}
+
+// k-table of an implicit-GEMM convolution, built once per geometry on the
+// context's stream (stream order makes it visible to the GEMM that follows)
+int get_ktab(tns_ctx* c, const ConvGeom& g, const int4** out) {
+  auto key = std::make_tuple(g.C, g.H, g.W, g.kH, g.kW, g.dY, g.dX);
+  auto it = c->ktabs.find(key);
+  if (it != c->ktabs.end()) {
+    *out = it->second;
+    return TNS_OK;
+  }
+  const int64_t K = g.C * g.kH * g.kW;
+  int4* t = nullptr;
+  hipError_t e = hipMalloc(&t, (size_t)(K + 1) * sizeof(int4));  // + sentinel
+  if (e != hipSuccess)
+    return set_error(TNS_ERR_NOMEM, "hipMalloc(k-table) failed: %s", hipGetErrorString(e));
+  e = launch_build_ktab(t, (int)g.C, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.dY,
+                        (int)g.dX, c->stream);
+  if (e != hipSuccess) {
+    hipFree(t);
+    return set_error(TNS_ERR_HIP, "k-table launch failed: %s", hipGetErrorString(e));
+  }
+  c->ktabs.emplace(key, t);
+  *out = t;
   return TNS_OK;
 }
 
@@ -197,6 +228,9 @@ int tns_set_option(int32_t opt, int64_t value) {
     case TNS_OPT_STRICT_BETA0:
       g_strict_beta0 = value ? 1 : 0;
       return TNS_OK;
+    case TNS_OPT_CONV_VARIANT:
+      g_conv_variant = value < 0 ? -1 : value;
+      return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
   }
@@ -233,6 +267,7 @@ int tns_hip_destroy(tns_ctx* c) {
   if (c->stream) hipStreamSynchronize(c->stream);
   for (int i = 0; i < 4; ++i)
     if (c->scratch[i]) hipFree(c->scratch[i]);
+  for (auto& kv : c->ktabs) hipFree(kv.second);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -655,13 +690,48 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
                                            c->stream),
                       "bias+activate launch");
   }
+  if (fused < TNS_CONV_UNFUSED || fused > TNS_CONV_IMPLICIT)
+    return set_error(TNS_ERR_ARG, "conv_forward: unknown schedule %d", fused);
   ConvGeom g = geom(C, H, W, kSize, kSize, padding, padding, stride, stride, dilation, dilation);
   if (int r = check_geom(g)) return r;
   const int64_t outImg = oh * ow, ks = kSize * kSize, k = C * ks;
   if (oh <= 0 || ow <= 0 || batch <= 0) return TNS_OK;
+  const bool needs_col = ks != 1 || dilation != 1 || stride != 1;
+  if (fused == TNS_CONV_IMPLICIT || (fused == TNS_CONV_FUSED && needs_col)) {
+    // implicit GEMM: batch folded into N, images gathered in the B staging
+    if (!input || !weights || !out || !biases)
+      return set_error(TNS_ERR_ARG, "conv_forward: null operand");
+    const int4* kt = nullptr;
+    if (int r = get_ktab(c, g, &kt)) return r;
+    const int64_t img = C * H * W;
+    // 32-bit offsets inside one launch (ConvBIO): split the batch
+    const int64_t per = std::max<int64_t>(img, outImg);
+    const int64_t chunk = std::max<int64_t>(1, (int64_t)0x7fffffff / std::max<int64_t>(per, 1));
+    for (int64_t b0 = 0; b0 < batch; b0 += chunk) {
+      const int64_t nb = std::min(chunk, batch - b0);
+      GemmArgs a{};
+      a.M = filters; a.N = nb * outImg; a.K = k;
+      a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_ZERO;
+      a.A = weights; a.lda = k; a.strideA = 0;
+      a.B = input + b0 * img; a.ldb = outImg; a.strideB = img;
+      a.C = out + b0 * outImg * filters; a.ldc = outImg; a.strideC = outImg * filters;
+      a.batch = 1; a.epi = EPI_BIAS_ACT; a.bias = biases; a.act = activation;
+      a.conv = 1; a.ktab = kt;
+      a.conv_H = (int)H; a.conv_W = (int)W; a.conv_ow = (int)ow; a.conv_ohw = (int)outImg;
+      a.conv_sY = (int)stride; a.conv_sX = (int)stride;
+      a.conv_pH = (int)padding; a.conv_pW = (int)padding;
+      OpTimer t(c, TNS_OP_GEMM);
+      hipError_t e = launch_sgemm_conv_variant((int)g_conv_variant, a, c->stream);
+      if (e == hipErrorInvalidValue)
+        return set_error(TNS_ERR_UNSUPPORTED, "conv variant %lld unsupported",
+                         (long long)g_conv_variant);
+      if (int r = hip_status(e, "implicit conv launch")) return r;
+    }
+    return TNS_OK;
+  }
   const float* Bp;
   int64_t strideB;
-  if (ks != 1 || dilation != 1 || stride != 1) {
+  if (needs_col) {
     strideB = k * outImg;
     float* ws = workspace;
     if (!ws)

@@ -47,9 +47,26 @@ struct GemmArgs {
   int epi;
   const float* bias;  // per row of C (filters)
   int act;            // TActivationType ordinal
+  // implicit-GEMM convolution: when conv != 0 the batch is
+  // folded into N (column n = image n / conv_ohw, pixel n % conv_ohw; the
+  // launch has batch == 1) and B is the im2col matrix of the images at
+  // B + image*strideB, generated inside the GEMM's staging loads and never
+  // written to memory; C of image i starts at C + i*strideC.  ktab[k] for
+  // k = (c*kH + kr)*kW + kc holds {c*H*W + kr*dY*W + kc*dX, kr*dY, kc*dX, 0};
+  // ktab[K] is a sentinel that fails the bounds check.
+  // All image offsets fit in 32 bits (the host splits the batch).
+  int conv;
+  const int4* ktab;
+  int conv_H, conv_W, conv_ow, conv_ohw, conv_sY, conv_sX, conv_pH, conv_pW;
 };
 
 hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s);
+// implicit-GEMM convolution: NN, B generated from the image (a.conv must be set)
+hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s);
+hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s);
+// builds the k-table of an implicit-GEMM convolution on the stream
+hipError_t launch_build_ktab(int4* ktab, int C, int H, int W, int kH, int kW, int dY, int dX,
+                             hipStream_t s);
 // variant < 0 picks the tile shape by heuristic; otherwise forces one (tuning)
 hipError_t launch_sgemm_variant(int variant, const GemmArgs& a, bool transA, bool transB,
                                 hipStream_t s);

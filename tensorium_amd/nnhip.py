@@ -20,6 +20,9 @@ except Exception:  # pragma: no cover
     torch = None
 
 
+CONV_UNFUSED, CONV_FUSED, CONV_IM2COL, CONV_IMPLICIT = 0, 1, 2, 3
+
+
 def _ptr(x):
     if x is None:
         return None
@@ -177,10 +180,17 @@ class TNNHip:
 
     def convForward(self, batch, C_, H, W, input, weights, biases, filters, kSize, stride,
                     padding, dilation, activation, workspace, out, fused=True):
+        """fused: False/0 reference stages, True/1 library choice, 2 im2col +
+        fused epilogue, 3 implicit GEMM (CONV_* constants)."""
+        mode = int(fused) if not isinstance(fused, bool) else (CONV_FUSED if fused else 0)
         check(self.lib.tns_hip_conv_forward(self.ctx, batch, C_, H, W, _ptr(input),
                                             _ptr(weights), _ptr(biases), filters, kSize, stride,
                                             padding, dilation, int(activation), _ptr(workspace),
-                                            _ptr(out), 1 if fused else 0))
+                                            _ptr(out), mode))
+
+    def setConvVariant(self, variant: int = -1):
+        """Force the implicit-GEMM tile shape (-1 = heuristic); process-wide."""
+        check(self.lib.tns_set_option(1, int(variant)))
 
     # -- batch norm / softmax (TNNCuda.meansAndVars ... crossEntropySoftmax) ----
     def meansAndVars(self, srcSize, dstSize, groups, src, offset, means, vars_):

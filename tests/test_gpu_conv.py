@@ -10,20 +10,21 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def conv_case(hip, torch, ora, batch, C, H, F, k, s, p, act, fused, seed=0):
+def conv_case(hip, torch, ora, batch, C, H, F, k, s, p, act, fused, seed=0, dil=1):
     x = ora.uniform(batch * C * H * H, 3, seed, 0.0, 1.0).reshape(batch, C, H, H)
     sc = float(np.sqrt(2.0 / (k * k * C)))
     w = ora.uniform(F * C * k * k, 30 + seed, seed, -sc, sc)
     b = ora.uniform(F, 60 + seed, seed, -0.1, 0.1)
-    ref = ora.conv_forward(x, w, b, F, k, s, p, act)
+    ref = ora.conv_forward(x, w, b, F, k, s, p, act, dil) if dil != 1 else \
+        ora.conv_forward(x, w, b, F, k, s, p, act)
     dx, dw, db = (torch.from_numpy(t).cuda() for t in (x, w, b))
     out = torch.full(ref.shape, float("nan"), device="cuda")
-    hip.convForward(batch, C, H, H, dx, dw, db, F, k, s, p, 1, act, None, out, fused=fused)
+    hip.convForward(batch, C, H, H, dx, dw, db, F, k, s, p, dil, act, None, out, fused=fused)
     hip.finish()
     return out.cpu().numpy(), ref
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [0, 1, 2, 3])
 @pytest.mark.parametrize("batch,C,H,F,k,s,p,act", [
     (2, 3, 17, 8, 3, 1, 1, 9), (3, 5, 12, 7, 3, 2, 1, 9), (2, 16, 9, 5, 1, 1, 0, 4),
     (1, 4, 20, 33, 3, 2, 1, 1), (2, 3, 13, 6, 5, 1, 2, 0)])
@@ -61,4 +62,42 @@ def test_yolov3_layers_batch8_full_size(hip, torch_cuda, ora, idx):
     spec = yolov3_conv_table()[idx]
     got, ref = conv_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,
                          spec.stride, spec.pad, spec.activation, True, seed=spec.index)
+    assert np.array_equal(got, ref), spec
+
+
+# implicit GEMM: every tile shape, ragged N (oh*ow not a multiple of BN),
+# K = C*k*k not a multiple of 32, strides, padding, and filter counts
+# straddling the tile rows
+IMPLICIT_CASES = [
+    (2, 3, 17, 8, 3, 1, 1, 9), (3, 5, 12, 70, 3, 2, 1, 9), (1, 7, 31, 129, 3, 1, 1, 9),
+    (2, 13, 26, 40, 3, 2, 1, 1), (1, 2, 9, 300, 5, 1, 2, 4), (2, 33, 19, 64, 3, 1, 1, 9),
+    (1, 64, 52, 128, 3, 1, 1, 9), (1, 32, 53, 256, 3, 2, 1, 9)]
+
+
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6])
+def test_conv_implicit_variants_bit_exact(hip, torch_cuda, ora, variant):
+    hip.setConvVariant(variant)
+    try:
+        for i, case in enumerate(IMPLICIT_CASES):
+            got, ref = conv_case(hip, torch_cuda, ora, *case, fused=3, seed=i)
+            assert np.array_equal(got, ref), (variant, case)
+    finally:
+        hip.setConvVariant(-1)
+
+
+def test_conv_implicit_dilation(hip, torch_cuda, ora):
+    for i, (batch, C, H, F, k, s, p, d) in enumerate([(2, 4, 21, 12, 3, 1, 2, 2),
+                                                      (1, 3, 30, 40, 3, 2, 2, 3)]):
+        got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, 9, 3, seed=i, dil=d)
+        got2, _ = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, 9, 2, seed=i, dil=d)
+        assert np.array_equal(got, ref)
+        assert np.array_equal(got2, ref)
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2, 11, 62, 74])
+def test_yolov3_layers_batch8_implicit(hip, torch_cuda, ora, idx):
+    from tensorium_amd.yolo import yolov3_conv_table
+    spec = yolov3_conv_table()[idx]
+    got, ref = conv_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,
+                         spec.stride, spec.pad, spec.activation, 3, seed=spec.index)
     assert np.array_equal(got, ref), spec

@@ -182,3 +182,24 @@ def test_4096_cubed_sampled_rows_bit_exact(hip, torch_cuda, ora):
     rhs = A.astype(np.float64).sum(axis=0) @ B.astype(np.float64)
     scale = np.abs(A).astype(np.float64).sum(axis=0) @ np.abs(B).astype(np.float64)
     assert np.all(np.abs(lhs - rhs) <= 1e-4 * scale)
+
+
+def test_every_tile_variant_bit_exact(hip, torch_cuda, ora):
+    """Each tile shape of the tuning table, forced, on ragged shapes: NN/TN
+    bit-exact; variants limited to float4/NN report UNSUPPORTED otherwise."""
+    from tensorium_amd._abi import TnsError
+    names = hip.gemmVariants()
+    for v, name in enumerate(names):
+        for (M, N, K) in [(37, 53, 61), (129, 130, 33), (256, 260, 96), (64, 512, 40)]:
+            for ta in (0, 1):
+                rng = np.random.default_rng(v * 1000 + M + ta)
+                A, B, C0 = operands(rng, ta, 0, M, N, K)
+                dA, dB, dC = (torch_cuda.from_numpy(x).cuda() for x in (A, B, C0.copy()))
+                try:
+                    hip.gemmVariant(v, bool(ta), False, M, N, K, 0.5, dA, 0, A.shape[1], 0,
+                                    dB, 0, B.shape[1], 0, 2.0, dC, 0, N, 0, 1)
+                except TnsError:
+                    continue
+                hip.finish()
+                ref = run_ref(ora, ta, 0, A, B, C0, 0.5, 2.0)
+                assert np.array_equal(dC.cpu().numpy(), ref), (name, M, N, K, ta)
