@@ -303,6 +303,20 @@ int tns_hip_conv_forward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int6
                          int64_t dilation, int32_t activation, float* workspace,
                          float* out, int32_t fused);
 
+/* TConvolutionalLayer.backward without batch-norm (nConvolutionLayer.pas:
+ * 571-671): delta *= f'(output) (Derivative), bias_updates += addSums(delta),
+ * im2col(input), weight_updates += delta_b . col_b^T per image (NT, beta 1),
+ * and if state_delta != NULL: col = W^T . delta (TN strided batched, beta 0)
+ * then col2im accumulates into state_delta.  delta is updated in place.
+ * workspace (batch*C*k*k*outH*outW floats) may be NULL (context scratch).
+ * dilation must be 1 (TNS_ERR_UNSUPPORTED otherwise). */
+int tns_hip_conv_backward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
+                          const float* input, const float* weights, int64_t filters,
+                          int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                          int32_t activation, const float* output, float* delta,
+                          float* bias_updates, float* weight_updates, float* workspace,
+                          float* state_delta);
+
 /* Multi-GPU batched GEMM (config 4): batchCount independent GEMMs on the
  * caller's device; sharding across ranks is done by the caller (one process
  * per GPU) — see bench.py.  Provided for completeness with the ctx API. */

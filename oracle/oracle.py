@@ -41,6 +41,8 @@ _PROTO = {
     "ora_conv_forward": (None, [i64, i64, i64, i64, fp, fp, fp, i64, i64, i64, i64, i64, i32, fp,
                                 fp]),
     "ora_fuse_batchnorm": (None, [i64, i64, fp, fp, fp, fp, fp]),
+    "ora_conv_backward": (C.c_int, [i64, i64, i64, i64, fp, fp, i64, i64, i64, i64, i64, i32,
+                                    fp, fp, fp, fp, fp, fp]),
     "ora_fill_uniform": (None, [fp, i64, C.c_uint64, C.c_uint64, f32, f32]),
 }
 
@@ -157,6 +159,19 @@ def conv_forward(x, w, b, filters, k, stride, pad, act, dil=1):
     lib().ora_conv_forward(batch, C_, H, W, _p(x), _p(w), _p(b), filters, k, stride, pad, dil,
                            act, _p(ws), _p(out))
     return out
+
+
+def conv_backward(x, w, filters, k, stride, pad, act, output, delta, bias_updates,
+                  weight_updates, state_delta=None):
+    """Restated TConvolutionalLayer.backward; updates delta, bias_updates,
+    weight_updates (and state_delta if given) in place."""
+    batch, C_, H, W = x.shape
+    oh, ow = out_dim(H, pad, k, 1, stride), out_dim(W, pad, k, 1, stride)
+    ws = np.zeros(max(batch * C_ * k * k * oh * ow, 1), np.float32)
+    rc = lib().ora_conv_backward(batch, C_, H, W, _p(x), _p(w), filters, k, stride, pad, 1, act,
+                                 _p(output), _p(delta), _p(bias_updates), _p(weight_updates),
+                                 _p(ws), _p(state_delta) if state_delta is not None else None)
+    assert rc == 0, rc
 
 
 _PROTO2 = {

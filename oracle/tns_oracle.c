@@ -506,6 +506,40 @@ void ora_conv_forward(int64_t batch, int64_t C, int64_t H, int64_t W, const floa
   ora_activate(out, batch * filters * oh * ow, act);
 }
 
+int ora_conv_backward(int64_t batch, int64_t C, int64_t H, int64_t W, const float* input,
+                      const float* weights, int64_t filters, int64_t kSize, int64_t stride,
+                      int64_t padding, int64_t dilation, int32_t act, const float* output,
+                      float* delta, float* bias_updates, float* weight_updates,
+                      float* workspace, float* state_delta) {
+  /* TConvolutionalLayer.backward, no batch-norm (nConvolutionLayer.pas:571-671) */
+  if (dilation != 1) return -1; /* backward pads with padding*dilation (632) while the
+                                   forward pads with padding (508): only d=1 is consistent */
+  int64_t oh = out_dim(H, padding, kSize, dilation, stride);
+  int64_t ow = out_dim(W, padding, kSize, dilation, stride);
+  int64_t i_m = filters, i_n = kSize * kSize * C, i_k = oh * ow, colSize = i_n * i_k;
+  /* Derivative(): delta *= f'(output) */
+  if (ora_gradient(output, batch * filters * i_k, act, delta)) return -2;
+  /* bias_updates.addSums(delta) */
+  ora_add_sums(bias_updates, delta, batch, filters, i_k);
+  /* state.input.im2Col(k, k, p*d, p*d, stride_y, stride_x, d, d, workspace) */
+  ora_im2col_strided_batched(C, H, W, kSize, kSize, padding * dilation, padding * dilation,
+                             stride, stride, dilation, dilation, input, C * H * W, 0, workspace,
+                             colSize, 0, batch);
+  /* weight_updates += delta_b . col_b^T, one NT gemm per image, beta = 1 */
+  for (int64_t b = 0; b < batch; b++)
+    ora_sgemm(101, 111, 112, i_m, i_n, i_k, 1.0f, delta + b * i_m * i_k, i_k,
+              workspace + b * colSize, i_k, 1.0f, weight_updates, i_n);
+  if (state_delta) {
+    /* col_b = W^T . delta_b (TN, strideA 0, beta 0), then col2im accumulate */
+    ora_sgemm_batch_strided(101, 112, 111, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,
+                            i_m * i_k, 0.0f, workspace, i_k, colSize, batch);
+    ora_col2im_strided_batched(C, H, W, kSize, kSize, padding * dilation, padding * dilation,
+                               stride, stride, dilation, dilation, workspace, colSize, 0,
+                               state_delta, C * H * W, 0, batch);
+  }
+  return 0;
+}
+
 void ora_fuse_batchnorm(int64_t filters, int64_t filterSize, float* weights, float* biases,
                         const float* scales, const float* rollingMean,
                         const float* rollingVariance) {

@@ -100,6 +100,17 @@ void    ora_conv_forward(int64_t batch, int64_t C, int64_t H, int64_t W,
                          const float* input, const float* weights, const float* biases,
                          int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
                          int64_t dilation, int32_t act, float* workspace, float* out);
+/* TConvolutionalLayer.backward without batch-norm (nConvolutionLayer.pas:
+ * 571-671): delta *= f'(output); bias_updates.addSums(delta); im2col(input);
+ * weight_updates += delta_b.col_b^T per image (NT, beta 1); if state_delta:
+ * col = W^T.delta (TN strided batched, beta 0) and col2im-accumulate.
+ * Returns -1 for dilation != 1 (the reference pads the backward im2col with
+ * padding*dilation but the forward with padding). */
+int     ora_conv_backward(int64_t batch, int64_t C, int64_t H, int64_t W,
+                          const float* input, const float* weights, int64_t filters,
+                          int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                          int32_t act, const float* output, float* delta, float* bias_updates,
+                          float* weight_updates, float* workspace, float* state_delta);
 /* fuseBatchNorm (nConvolutionLayer.pas:102-126). */
 void    ora_fuse_batchnorm(int64_t filters, int64_t filterSize, float* weights,
                            float* biases, const float* scales, const float* rollingMean,

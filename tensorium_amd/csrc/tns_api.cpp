@@ -753,6 +753,67 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
                  true);
 }
 
+int tns_hip_conv_backward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                          const float* input, const float* weights, int64_t filters,
+                          int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                          int32_t activation, const float* output, float* delta,
+                          float* bias_updates, float* weight_updates, float* workspace,
+                          float* state_delta) {
+  if (int r = check_ctx(c)) return r;
+  if (dilation != 1)
+    return set_error(TNS_ERR_UNSUPPORTED,
+                     "conv_backward: dilation %lld (the reference pads the backward im2col "
+                     "with padding*dilation, nConvolutionLayer.pas:632, but the forward with "
+                     "padding; only dilation 1 is consistent)",
+                     (long long)dilation);
+  if (!act_supported(activation))
+    return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
+  ConvGeom g = geom(C, H, W, kSize, kSize, padding, padding, stride, stride, 1, 1);
+  if (int r = check_geom(g)) return r;
+  const int64_t i_m = filters, i_n = kSize * kSize * C, i_k = g.oh * g.ow;
+  const int64_t colSize = i_n * i_k;
+  if (batch <= 0 || i_k <= 0 || filters <= 0) return TNS_OK;
+  if (!input || !weights || !output || !delta || !bias_updates || !weight_updates)
+    return set_error(TNS_ERR_ARG, "conv_backward: null operand");
+  // Derivative(): delta *= f'(output)
+  if (int r = hip_status(launch_derive(output, batch * filters * i_k, activation, delta,
+                                       c->stream), "derive launch"))
+    return r;
+  // bias_updates.addSums(delta)
+  if (int r = hip_status(launch_add_sums(bias_updates, delta, batch, filters, i_k, c->stream),
+                         "addSums launch"))
+    return r;
+  // state.input.im2Col(...) — a 1x1/s1/p0 col matrix is the input itself
+  const bool needs_col = kSize != 1 || stride != 1 || padding != 0;
+  float* ws = workspace;
+  if (!ws && (needs_col || state_delta))
+    if (int r = ensure_scratch(c, 0, batch * colSize, &ws)) return r;
+  const float* col = input;
+  if (needs_col) {
+    OpTimer t(c, TNS_OP_IM2COL);
+    if (int r = hip_status(launch_im2col(g, input, C * H * W, ws, colSize, batch, c->stream),
+                           "im2col launch"))
+      return r;
+    col = ws;
+  }
+  // weight_updates += delta_b . col_b^T, one NT GEMM per image (beta = 1),
+  // in image order as the reference loop (nConvolutionLayer.pas:636-640)
+  for (int64_t b = 0; b < batch; ++b)
+    if (int r = do_gemm(c, false, true, i_m, i_n, i_k, 1.0f, delta + b * i_m * i_k, i_k, 0,
+                        col + b * colSize, i_k, 0, 1.0f, weight_updates, i_n, 0, 1, EPI_NONE,
+                        nullptr, 0))
+      return r;
+  if (!state_delta) return TNS_OK;
+  // col_b = W^T . delta_b (TN strided batched, weights shared, beta = 0 into
+  // the workspace), then col2im accumulates into state.delta (646-660)
+  if (int r = do_gemm(c, true, false, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,
+                      i_m * i_k, 0.0f, ws, i_k, colSize, batch, EPI_NONE, nullptr, 0, true))
+    return r;
+  OpTimer t(c, TNS_OP_COL2IM);
+  return hip_status(launch_col2im(g, ws, colSize, state_delta, C * H * W, batch, c->stream),
+                    "col2im launch");
+}
+
 int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }
 

@@ -188,6 +188,15 @@ class TNNHip:
                                             padding, dilation, int(activation), _ptr(workspace),
                                             _ptr(out), mode))
 
+    def convBackward(self, batch, C_, H, W, input, weights, filters, kSize, stride, padding,
+                     dilation, activation, output, delta, bias_updates, weight_updates,
+                     workspace=None, state_delta=None):
+        """TConvolutionalLayer.backward (no BN); delta is updated in place."""
+        check(self.lib.tns_hip_conv_backward(
+            self.ctx, batch, C_, H, W, _ptr(input), _ptr(weights), filters, kSize, stride,
+            padding, dilation, int(activation), _ptr(output), _ptr(delta), _ptr(bias_updates),
+            _ptr(weight_updates), _ptr(workspace), _ptr(state_delta)))
+
     def setConvVariant(self, variant: int = -1):
         """Force the implicit-GEMM tile shape (-1 = heuristic); process-wide."""
         check(self.lib.tns_set_option(1, int(variant)))

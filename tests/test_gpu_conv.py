@@ -101,3 +101,44 @@ def test_yolov3_layers_batch8_implicit(hip, torch_cuda, ora, idx):
     got, ref = conv_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,
                          spec.stride, spec.pad, spec.activation, 3, seed=spec.index)
     assert np.array_equal(got, ref), spec
+
+
+@pytest.mark.parametrize("batch,C,H,F,k,s,p,act", [
+    (2, 3, 17, 8, 3, 1, 1, 9), (3, 5, 12, 7, 3, 2, 1, 9), (2, 16, 9, 5, 1, 1, 0, 4),
+    (2, 6, 13, 33, 3, 1, 1, 1), (1, 32, 26, 64, 3, 2, 1, 9)])
+def test_conv_backward_matches_oracle(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act):
+    """delta (derived) and state_delta (TN + col2im) bit-exact; weight_updates
+    (NT, reference sdot order) within the componentwise GEMM bound; bias
+    sums within 1e-5 relative."""
+    rng = np.random.default_rng(batch * 1000 + C * 10 + H)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.3, 0.3, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    sd0 = rng.uniform(-1, 1, x.shape).astype(np.float32)
+    rd, rbu, rwu, rsd = d0.copy(), bu0.copy(), wu0.copy(), sd0.copy()
+    ora.conv_backward(x, w, F, k, s, p, act, out, rd, rbu, rwu, rsd)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    dx, dw, dout, dd, dbu, dwu, dsd = map(t, (x, w, out, d0, bu0, wu0, sd0))
+    hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, act, dout, dd, dbu, dwu, None, dsd)
+    hip.finish()
+    assert np.array_equal(dd.cpu().numpy(), rd)
+    assert np.array_equal(dsd.cpu().numpy(), rsd)
+    # weight_updates bound: |A||B| over the batch-concatenated NT product
+    i_k = oh * oh
+    cols = ora.im2col(C, H, H, k, k, p, p, s, s, 1, 1, x, batch)
+    bnd = sum(np.abs(rd[b].reshape(F, -1)).astype(np.float64) @ np.abs(cols[b]).T
+              for b in range(batch)) + np.abs(wu0.reshape(F, -1))
+    err = np.abs(dwu.cpu().numpy().reshape(F, -1).astype(np.float64) - rwu.reshape(F, -1))
+    assert np.all(err <= 1e-4 * bnd + 1e-30)
+    assert np.allclose(dbu.cpu().numpy(), rbu, rtol=1e-5, atol=1e-5)
+
+
+def test_conv_backward_rejects_dilation(hip, torch_cuda):
+    from tensorium_amd._abi import TnsError
+    z = torch_cuda.zeros(4096, device="cuda")
+    with pytest.raises(TnsError):
+        hip.convBackward(1, 1, 9, 9, z, z, 1, 3, 1, 2, 2, 9, z, z, z, z, None, None)
