@@ -343,8 +343,10 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
 /* TNS_OPT_STRICT_BETA0 (default 1): beta==0 computes 0*C like the reference
  * (NaN/Inf in C propagate).  0 = BLAS convention (C not read).
  * TNS_OPT_CONV_VARIANT (default -1 = heuristic): forces the tile shape of the
- * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name). */
-enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1 };
+ * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name).
+ * TNS_OPT_CONV_PAD (default -1 = by cost): 1 gathers from a zero-padded copy
+ * of the images, 0 bounds-checks the window inside the GEMM. */
+enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

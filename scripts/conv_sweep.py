@@ -19,12 +19,13 @@ sys.path.insert(0, str(ROOT))
 from tensorium_amd.nnhip import TNNHip  # noqa: E402
 from tensorium_amd.yolo import yolov3_conv_table  # noqa: E402
 
-IMPLICIT_VARIANTS = [0, 1, 2, 3, 4, 5, 6]
+IMPLICIT_VARIANTS = [1, 2, 4, 6]
 
 
-def time_conv(hip, layer, mode, variant, reps):
+def time_conv(hip, layer, mode, variant, reps, pad=-1):
     s, x, w, b, ws, out, batch = layer
     hip.setConvVariant(variant)
+    hip.setConvPad(pad)
     run = lambda: hip.convForward(batch, s.c, s.h, s.h, x, w, b, s.filters, s.size, s.stride,
                                   s.pad, 1, s.activation, ws, out, fused=mode)
     run()
@@ -36,6 +37,7 @@ def time_conv(hip, layer, mode, variant, reps):
     e1.record()
     torch.cuda.synchronize()
     hip.setConvVariant(-1)
+    hip.setConvPad(-1)
     return e0.elapsed_time(e1) / reps
 
 
@@ -59,15 +61,16 @@ def main():
         out = torch.empty(args.batch, s.filters, s.N, device="cuda")
         layers[f"L{s.index}_c{s.c}_h{s.h}_f{s.filters}_k{s.size}s{s.stride}"] = (
             (s, x, w, b, ws, out, args.batch), s)
-    cfgs = [("im2col", 2, -1), ("implicit_auto", 3, -1)] + \
-        [(f"implicit_{names[v]}", 3, v) for v in IMPLICIT_VARIANTS]
+    cfgs = [("im2col", 2, -1, -1), ("implicit_auto", 3, -1, -1),
+            ("implicit_64x64_checked", 3, 6, 0), ("implicit_64x64_padded", 3, 6, 1)] + \
+        [(f"implicit_{names[v]}", 3, v, -1) for v in IMPLICIT_VARIANTS]
     res = {k: {c[0]: [] for c in cfgs} for k in layers}
     for _ in range(args.rounds):
         for k, (layer, s) in layers.items():
             flop = 2.0 * s.M * s.N * s.K * args.batch
             reps = max(3, min(40, int(2e10 / flop)))
-            for name, mode, v in cfgs:
-                res[k][name].append(time_conv(hip, layer, mode, v, reps))
+            for name, mode, v, pad in cfgs:
+                res[k][name].append(time_conv(hip, layer, mode, v, reps, pad))
     out = {}
     tot = {c[0]: 0.0 for c in cfgs}
     best_tot = 0.0

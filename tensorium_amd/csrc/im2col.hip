@@ -25,27 +25,57 @@ int64_t out_dim(int64_t in, int64_t pad, int64_t k, int64_t dil, int64_t stride)
 
 namespace {
 // k-table of the implicit-GEMM convolution: the im2col row k = (c, kr, kc)
-// reads im[c][ir0 + kr*dY][ic0 + kc*dX] for the output pixel whose window
-// starts at (ir0, ic0) — the same element sim2Col copies (ntensors.pas:11460).
-__global__ void ktab_kernel(int4* t, int K, int H, int W, int kH, int kW, int dY, int dX) {
+// reads padded image element [c][orow*sY + kr*dY][ocol*sX + kc*dX] — the same
+// element sim2Col copies (ntensors.pas:11460), shifted by the padding.
+__global__ void ktab_kernel(int4* t, int K, int total, int Hs, int Ws, int kH, int kW, int dY,
+                            int dX) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k > K) return;
-  if (k == K) {  // sentinel for k >= K: the row check always fails
-    t[k] = make_int4(0, 0x40000000, 0x40000000, 0);
+  if (k >= total) return;
+  if (k >= K) {  // sentinel: out of the buffer's range and of any window
+    t[k] = make_int4((int)0x80000000u, 0x40000000, 0x40000000, 0);
     return;
   }
   const int kc = k % kW, r = k / kW;
   const int kr = r % kH, c = r / kH;
-  t[k] = make_int4(c * H * W + kr * dY * W + kc * dX, kr * dY, kc * dX, 0);
+  t[k] = make_int4(4 * (c * Hs * Ws + kr * dY * Ws + kc * dX), kr * dY, kc * dX, 0);
+}
+
+__global__ void pad_kernel(const float* __restrict__ im, float* __restrict__ out, int64_t planes,
+                           int H, int W, int pH, int pW) {
+  const int Hp = H + 2 * pH, Wp = W + 2 * pW;
+  const int64_t total = planes * Hp * Wp;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % Wp);
+    const int64_t t = i / Wp;
+    const int y = (int)(t % Hp);
+    const int64_t pl = t / Hp;
+    const int iy = y - pH, ix = x - pW;
+    out[i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                 ? im[(pl * H + iy) * W + ix]
+                 : 0.0f;
+  }
 }
 }  // namespace
 
-hipError_t launch_build_ktab(int4* ktab, int C, int H, int W, int kH, int kW, int dY, int dX,
+hipError_t launch_build_ktab(int4* ktab, int C, int Hp, int Wp, int kH, int kW, int dY, int dX,
                              hipStream_t s) {
-  const int K = C * kH * kW;  // K + 1 entries (sentinel last)
+  const int K = C * kH * kW;
   if (K < 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ktab_kernel, dim3((K + 256) / 256), dim3(256), 0, s, ktab, K, H, W, kH, kW,
-                     dY, dX);
+  const int total = K + KTAB_PAD;
+  hipLaunchKernelGGL(ktab_kernel, dim3((total + 255) / 256), dim3(256), 0, s, ktab, K, total, Hp,
+                     Wp, kH, kW, dY, dX);
+  return hipGetLastError();
+}
+
+hipError_t launch_pad_images(const float* im, int64_t batch, int64_t C, int64_t H, int64_t W,
+                             int64_t pH, int64_t pW, float* out, hipStream_t s) {
+  const int64_t total = batch * C * (H + 2 * pH) * (W + 2 * pW);
+  if (total <= 0) return hipSuccess;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(pad_kernel, dim3((unsigned)blocks), dim3(256), 0, s, im, out, batch * C,
+                     (int)H, (int)W, (int)pH, (int)pW);
   return hipGetLastError();
 }
 

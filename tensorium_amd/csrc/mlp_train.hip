@@ -26,61 +26,67 @@ constexpr int NT = 1024;
 constexpr int NWAVES = NT / 64;
 __device__ constexpr float SEPS = 0.000001f;
 
+// Per-layer views into the packed buffer.  The element offsets are computed
+// on the host (MlpArgs::off) and read from the kernel arguments on each use,
+// so no pointer set stays live in registers across the stages.
+enum { F_W, F_B, F_DW, F_DB, F_SCALES, F_RMEAN, F_RVAR, F_DSCALES, F_OUT, F_DELTA, F_X, F_XNORM,
+       F_MEAN, F_VAR, F_MDELTA, F_VDELTA };
 struct Layer {
+  const MlpArgs* a;
+  int l;
   int64_t I, O;
   int act;
-  float *W, *b, *dW, *db, *scales, *rmean, *rvar, *dscales, *out, *delta, *x, *xnorm, *mean,
-      *var, *mdelta, *vdelta;
+  __device__ Layer(const MlpArgs& args, int layer)
+      : a(&args), l(layer), I(args.widths[layer]), O(args.widths[layer + 1]),
+        act(args.acts[layer]) {}
+  __device__ float* f(int which) const { return a->buf + a->off[l][which]; }
+  __device__ float* W() const { return f(F_W); }
+  __device__ float* b() const { return f(F_B); }
+  __device__ float* dW() const { return f(F_DW); }
+  __device__ float* db() const { return f(F_DB); }
+  __device__ float* scales() const { return f(F_SCALES); }
+  __device__ float* rmean() const { return f(F_RMEAN); }
+  __device__ float* rvar() const { return f(F_RVAR); }
+  __device__ float* dscales() const { return f(F_DSCALES); }
+  __device__ float* out() const { return f(F_OUT); }
+  __device__ float* delta() const { return f(F_DELTA); }
+  __device__ float* x() const { return f(F_X); }
+  __device__ float* xnorm() const { return f(F_XNORM); }
+  __device__ float* mean() const { return f(F_MEAN); }
+  __device__ float* var() const { return f(F_VAR); }
+  __device__ float* mdelta() const { return f(F_MDELTA); }
+  __device__ float* vdelta() const { return f(F_VDELTA); }
 };
 
-__device__ void layer_at(const MlpArgs& a, int want, Layer& L, float** softmax_base) {
-  float* p = a.buf;
-  const int64_t B = a.batch;
-  for (int l = 0; l < a.nlayers; ++l) {
-    Layer t;
-    t.I = a.widths[l];
-    t.O = a.widths[l + 1];
-    t.act = a.acts[l];
-    const int64_t IO = t.I * t.O, O = t.O, BO = B * t.O;
-    t.W = p; p += IO;
-    t.b = p; p += O;
-    t.dW = p; p += IO;
-    t.db = p; p += O;
-    t.scales = t.rmean = t.rvar = t.dscales = nullptr;
-    t.x = t.xnorm = t.mean = t.var = t.mdelta = t.vdelta = nullptr;
-    if (a.bn) {
-      t.scales = p; p += O;
-      t.rmean = p; p += O;
-      t.rvar = p; p += O;
-      t.dscales = p; p += O;
+// One 32x32 MFMA output tile as an ascending chain: step s feeds lane
+// (l31, h) the operands pa[s*sa] / pb[s*sb] for k = k0 + s*kstep (k0 already
+// includes the lane half h); operands with k >= K or an out-of-range row
+// (va / vb false) are 0.  Operands of U steps are loaded together (one memory
+// latency per U steps), then consumed by U dependent MFMAs in step order.
+template <int U = 8>
+__device__ __forceinline__ void mfma_chain(floatx16& acc, int steps, const float* pa, int64_t sa,
+                                           bool va, const float* pb, int64_t sb, bool vb,
+                                           int64_t k0, int64_t kstep, int64_t K) {
+  int s = 0;
+  for (; s + U <= steps; s += U) {
+    float av[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = k0 + (int64_t)(s + u) * kstep < K;
+      const int64_t ia = ok ? (int64_t)(s + u) * sa : 0, ib = ok ? (int64_t)(s + u) * sb : 0;
+      const float x = pa[ia], y = pb[ib];
+      av[u] = (ok && va) ? x : 0.0f;
+      bv[u] = (ok && vb) ? y : 0.0f;
     }
-    t.out = p; p += BO;
-    t.delta = p; p += BO;
-    if (a.bn) {
-      t.x = p; p += BO;
-      t.xnorm = p; p += BO;
-      t.mean = p; p += O;
-      t.var = p; p += O;
-      t.mdelta = p; p += O;
-      t.vdelta = p; p += O;
-    }
-    if (l == want) L = t;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
   }
-  if (softmax_base) *softmax_base = p;
-}
-
-// One 32x32 MFMA output tile: acc += sum over steps s of A[m][k(s,h)]*B[k(s,h)][n]
-// with the lane maps of v_mfma_f32_32x32x2_f32 (lane l: m = l&31 of A, n = l&31
-// of B, k-slot h = l>>5).  kfun(s, h) gives the k consumed in step s by half h
-// (ascending per accumulator); out-of-range values are supplied as 0 by fa/fb.
-template <class FA, class FB>
-__device__ __forceinline__ void mfma_tile(floatx16& acc, int steps, FA fa, FB fb) {
-  const int lane = threadIdx.x & 63;
-  const int l31 = lane & 31, h = lane >> 5;
-  for (int s = 0; s < steps; ++s) {
-    const float av = fa(l31, s, h);
-    const float bv = fb(l31, s, h);
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+  for (; s < steps; ++s) {
+    const bool ok = k0 + (int64_t)s * kstep < K;
+    const float x = pa[ok ? (int64_t)s * sa : 0], y = pb[ok ? (int64_t)s * sb : 0];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32((ok && va) ? x : 0.0f, (ok && vb) ? y : 0.0f,
+                                               acc, 0, 0, 0);
   }
 }
 
@@ -109,9 +115,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   const int64_t B = a.batch;
   const int L = a.nlayers;
   const int64_t C = a.widths[L];
-  float* smx;
-  Layer lay;
-  layer_at(a, 0, lay, &smx);
+  float* smx = a.buf + a.softmax_off;
   float* sm_out = smx;
   float* sm_delta = smx + B * C;
   float* sm_loss = smx + 2 * B * C;
@@ -119,9 +123,9 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   // ---- forward ------------------------------------------------------------
   const float* in = a.X;
   for (int l = 0; l < L; ++l) {
-    layer_at(a, l, lay, nullptr);
+    const Layer lay(a, l);
     const int64_t I = lay.I, O = lay.O, BO = B * O;
-    for (int64_t e = tid; e < BO; e += NT) lay.delta[e] = 0.0f;  // nnet.pas:287-296
+    for (int64_t e = tid; e < BO; e += NT) lay.delta()[e] = 0.0f;  // nnet.pas:287-296
 
     // gemm(RowMajor, NoTrans, Trans, B, O, I, 1, in, I, W, I, 0, out, O):
     // sdot_avx2 residue classes r = k mod 8, each an ascending MFMA chain
@@ -133,15 +137,13 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       const int64_t m0 = (int64_t)(tile / tn) * 32, n0 = (int64_t)(tile % tn) * 32;
       floatx16 acc;
       for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-      mfma_tile(acc, steps,
-                [&](int l31, int s, int h) {
-                  const int64_t m = m0 + l31, k = r + 8 * (2 * (int64_t)s + h);
-                  return (m < B && k < I) ? in[m * I + k] : 0.0f;
-                },
-                [&](int l31, int s, int h) {
-                  const int64_t n = n0 + l31, k = r + 8 * (2 * (int64_t)s + h);
-                  return (n < O && k < I) ? lay.W[n * I + k] : 0.0f;
-                });
+      {
+        const int l31 = lane & 31, h = lane >> 5;
+        const int64_t m = m0 + l31, n = n0 + l31, k0 = r + 8 * h;
+        // step s consumes k = r + 8*(2s + h) of residue class r
+        mfma_chain(acc, steps, in + (m < B ? m : 0) * I + k0, 16, m < B,
+                   lay.W() + (n < O ? n : 0) * I + k0, 16, n < O, k0, 16, I);
+      }
       for (int e = 0; e < 16; ++e) {
         const int64_t m = m0 + acc_row(e), n = n0 + (lane & 31);
         if (m < B && n < O) lds[(r * B + m) * O + n] = acc[e];
@@ -153,44 +155,47 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       for (int q = 0; q < 8; ++q) p[q] = lds[q * BO + e];
       const float s0 = p[0] + p[4], s1 = p[1] + p[5], s2 = p[2] + p[6], s3 = p[3] + p[7];
       const float dot = (s0 + s1) + (s2 + s3);
-      const float c0 = 0.0f * lay.out[e];  // beta = 0 => 0*C (mulvs)
-      lay.out[e] = c0 + 1.0f * dot;        // C := C + ALPHA*sdot
+      const float c0 = 0.0f * lay.out()[e];  // beta = 0 => 0*C (mulvs)
+      lay.out()[e] = c0 + 1.0f * dot;        // C := C + ALPHA*sdot
     }
     __syncthreads();
     if (a.bn) {
       // per channel: MeansAndVars, rolling stats, x, normalize, x_norm, scale
       for (int64_t o = tid; o < O; o += NT) {
         float m = 0.0f;
-        for (int64_t b = 0; b < B; ++b) m = m + lay.out[b * O + o];
+#pragma unroll 8
+        for (int64_t b = 0; b < B; ++b) m = m + lay.out()[b * O + o];
         m = m / (float)B;
         float v = 0.0f;
+#pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float t = lay.out[b * O + o] - m;
+          const float t = lay.out()[b * O + o] - m;
           v = v + t * t;
         }
         v = v / (float)(B - 1);
-        lay.mean[o] = m;
-        lay.var[o] = v;
+        lay.mean()[o] = m;
+        lay.var()[o] = v;
         const float mom = 0.05f;  // bnMomentum, nconnectedlayer.pas:67
-        lay.rmean[o] = fmaf(mom, m, lay.rmean[o] * (1.0f - mom));
-        lay.rvar[o] = fmaf(mom, v, lay.rvar[o] * (1.0f - mom));
+        lay.rmean()[o] = fmaf(mom, m, lay.rmean()[o] * (1.0f - mom));
+        lay.rvar()[o] = fmaf(mom, v, lay.rvar()[o] * (1.0f - mom));
         const float sd = sqrtf(v > SEPS ? v : SEPS);
+#pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float xv = lay.out[b * O + o];
-          lay.x[b * O + o] = xv;
+          const float xv = lay.out()[b * O + o];
+          lay.x()[b * O + o] = xv;
           const float xn = (xv - m) / sd;
-          lay.xnorm[b * O + o] = xn;
-          lay.out[b * O + o] = xn * lay.scales[o];
+          lay.xnorm()[b * O + o] = xn;
+          lay.out()[b * O + o] = xn * lay.scales()[o];
         }
       }
       __syncthreads();
     }
     for (int64_t e = tid; e < BO; e += NT) {
       const int64_t o = e % O;
-      lay.out[e] = act_apply(lay.out[e] + lay.b[o], lay.act);  // forwardBias, activate
+      lay.out()[e] = act_apply(lay.out()[e] + lay.b()[o], lay.act);  // forwardBias, activate
     }
     __syncthreads();
-    in = lay.out;
+    in = lay.out();
   }
 
   // ---- softmax + cross-entropy (groups 1, temperature 1) ----------------------
@@ -219,51 +224,54 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
 
   // ---- backward ---------------------------------------------------------------
   for (int l = L - 1; l >= 0; --l) {
-    layer_at(a, l, lay, nullptr);
+    const Layer lay(a, l);
     const int64_t I = lay.I, O = lay.O, BO = B * O;
-    Layer prev;
     const float* lin = a.X;
     float* prev_delta = nullptr;
     if (l > 0) {
-      layer_at(a, l - 1, prev, nullptr);
-      lin = prev.out;
-      prev_delta = prev.delta;  // state.delta = nil for layer 0 (nnet.pas:332-335)
+      const Layer prev(a, l - 1);
+      lin = prev.out();
+      prev_delta = prev.delta();  // state.delta = nil for layer 0 (nnet.pas:332-335)
     }
-    // softmax backward: prev.delta += delta; then clamp + activation gradient
+    // softmax backward: prev.delta() += delta; then clamp + activation gradient
     for (int64_t e = tid; e < BO; e += NT) {
-      float d = lay.delta[e];
+      float d = lay.delta()[e];
       if (l == L - 1) d = d + sm_delta[e];
       d = d < -1.0f ? -1.0f : (d > 1.0f ? 1.0f : d);  // delta.Clamp(-1, 1)
-      lay.delta[e] = d * grad_apply(lay.out[e], lay.act);
+      lay.delta()[e] = d * grad_apply(lay.out()[e], lay.act);
     }
     __syncthreads();
     // per channel: bias_updates.addSums, then the BN backward chain
     for (int64_t o = tid; o < O; o += NT) {
       float r = 0.0f;
-      for (int64_t b = 0; b < B; ++b) r = r + lay.delta[b * O + o];
-      lay.db[o] = lay.db[o] + r;
+#pragma unroll 8
+      for (int64_t b = 0; b < B; ++b) r = r + lay.delta()[b * O + o];
+      lay.db()[o] = lay.db()[o] + r;
       if (a.bn) {
         float dd = 0.0f;  // addDots (strided sdot: mul then add)
-        for (int64_t b = 0; b < B; ++b) dd = dd + lay.xnorm[b * O + o] * lay.delta[b * O + o];
-        lay.dscales[o] = lay.dscales[o] + dd;
-        const float sc = lay.scales[o], mu = lay.mean[o];
+#pragma unroll 8
+        for (int64_t b = 0; b < B; ++b) dd = dd + lay.xnorm()[b * O + o] * lay.delta()[b * O + o];
+        lay.dscales()[o] = lay.dscales()[o] + dd;
+        const float sc = lay.scales()[o], mu = lay.mean()[o];
         float m = 0.0f, v = 0.0f;
+#pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float d = lay.delta[b * O + o] * sc;  // forwardScale
-          lay.delta[b * O + o] = d;
+          const float d = lay.delta()[b * O + o] * sc;  // forwardScale
+          lay.delta()[b * O + o] = d;
           m = m + d;
-          v = v + (lay.x[b * O + o] - mu) * d;
+          v = v + (lay.x()[b * O + o] - mu) * d;
         }
-        const float ve = lay.var[o] > SEPS ? lay.var[o] : SEPS;
+        const float ve = lay.var()[o] > SEPS ? lay.var()[o] : SEPS;
         const float md = m * (-1.0f / sqrtf(ve));
         const float vd = (float)((double)v * -0.5 * pow((double)ve, -1.5));
-        lay.mdelta[o] = md;
-        lay.vdelta[o] = vd;
+        lay.mdelta()[o] = md;
+        lay.vdelta()[o] = vd;
         const float mdb = md / (float)B, vdb = 2.0f * vd / (float)B, sd = sqrtf(ve);
+#pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float q = lay.delta[b * O + o] / sd;
-          const float t = (lay.x[b * O + o] - mu) * vdb + mdb;
-          lay.delta[b * O + o] = q + t;
+          const float q = lay.delta()[b * O + o] / sd;
+          const float t = (lay.x()[b * O + o] - mu) * vdb + mdb;
+          lay.delta()[b * O + o] = q + t;
         }
       }
     }
@@ -278,31 +286,21 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       const int t = is_dw ? w : w - nw_dw;
       const int64_t m0 = (int64_t)(t / tni) * 32, n0 = (int64_t)(t % tni) * 32;
       const int64_t Mx = is_dw ? O : B;
-      float* Cp = is_dw ? lay.dW : prev_delta;
+      float* Cp = is_dw ? lay.dW() : prev_delta;
       for (int e = 0; e < 16; ++e) {
         const int64_t m = m0 + acc_row(e), n = n0 + (lane & 31);
         acc[e] = (m < Mx && n < I) ? Cp[m * I + n] : 0.0f;
       }
-      if (is_dw) {
-        mfma_tile(acc, (int)((B + 1) / 2),
-                  [&](int l31, int s, int h) {
-                    const int64_t m = m0 + l31, k = 2 * (int64_t)s + h;
-                    return (m < O && k < B) ? lay.delta[k * O + m] : 0.0f;
-                  },
-                  [&](int l31, int s, int h) {
-                    const int64_t n = n0 + l31, k = 2 * (int64_t)s + h;
-                    return (n < I && k < B) ? lin[k * I + n] : 0.0f;
-                  });
-      } else {
-        mfma_tile(acc, (int)((O + 1) / 2),
-                  [&](int l31, int s, int h) {
-                    const int64_t m = m0 + l31, k = 2 * (int64_t)s + h;
-                    return (m < B && k < O) ? lay.delta[m * O + k] : 0.0f;
-                  },
-                  [&](int l31, int s, int h) {
-                    const int64_t n = n0 + l31, k = 2 * (int64_t)s + h;
-                    return (n < I && k < O) ? lay.W[k * I + n] : 0.0f;
-                  });
+      const int l31 = lane & 31, h = lane >> 5;
+      const int64_t m = m0 + l31, n = n0 + l31, nc = n < I ? n : 0;
+      if (is_dw) {  // a = delta[k][m], b = in[k][n], k = 2s + h over the batch
+        const int64_t mc = m < O ? m : 0;
+        mfma_chain(acc, (int)((B + 1) / 2), lay.delta() + h * O + mc, 2 * O, m < O,
+                   lin + h * I + nc, 2 * I, n < I, h, 2, B);
+      } else {      // a = delta[m][k], b = W[k][n], k = 2s + h over the outputs
+        const int64_t mc = m < B ? m : 0;
+        mfma_chain(acc, (int)((O + 1) / 2), lay.delta() + mc * O + h, 2, m < B,
+                   lay.W() + h * I + nc, 2 * I, n < I, h, 2, O);
       }
       for (int e = 0; e < 16; ++e) {
         const int64_t m = m0 + acc_row(e), n = n0 + (lane & 31);
@@ -316,21 +314,21 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   const float lrb = a.lr / (float)B;
   const float wdec = -a.decay * (float)B;
   for (int l = 0; l < L; ++l) {
-    layer_at(a, l, lay, nullptr);
+    const Layer lay(a, l);
     const int64_t O = lay.O, IO = lay.I * lay.O;
     for (int64_t o = tid; o < O; o += NT) {
-      lay.b[o] = fmaf(lrb, lay.db[o], lay.b[o]);
-      lay.db[o] = a.momentum * lay.db[o];
+      lay.b()[o] = fmaf(lrb, lay.db()[o], lay.b()[o]);
+      lay.db()[o] = a.momentum * lay.db()[o];
       if (a.bn) {
-        lay.scales[o] = fmaf(lrb, lay.dscales[o], lay.scales[o]);
-        lay.dscales[o] = a.momentum * lay.dscales[o];
+        lay.scales()[o] = fmaf(lrb, lay.dscales()[o], lay.scales()[o]);
+        lay.dscales()[o] = a.momentum * lay.dscales()[o];
       }
     }
     for (int64_t e = tid; e < IO; e += NT) {
-      float dw = fmaf(wdec, lay.W[e], lay.dW[e]);  // weight_updates.axpy(-decay*batch, W)
-      const float w = fmaf(lrb, dw, lay.W[e]);     // weights.axpy(lr/batch, dW)
-      lay.W[e] = w;
-      lay.dW[e] = a.momentum * dw;                  // weight_updates.Multiply(momentum)
+      float dw = fmaf(wdec, lay.W()[e], lay.dW()[e]);  // weight_updates.axpy(-decay*batch, W)
+      const float w = fmaf(lrb, dw, lay.W()[e]);     // weights.axpy(lr/batch, dW)
+      lay.W()[e] = w;
+      lay.dW()[e] = a.momentum * dw;                  // weight_updates.Multiply(momentum)
     }
   }
 }
@@ -347,7 +345,37 @@ int64_t mlp_buffer_floats(int nlayers, const int64_t* widths, int bn, int64_t B)
   return n + 3 * B * widths[nlayers];
 }
 
-hipError_t launch_mlp_train_step(const MlpArgs& a, hipStream_t s) {
+hipError_t launch_mlp_train_step(const MlpArgs& args, hipStream_t s) {
+  if (args.nlayers < 1 || args.nlayers > MLP_MAX_LAYERS) return hipErrorInvalidValue;
+  MlpArgs a = args;
+  int64_t p = 0;
+  const int64_t B = a.batch;
+  for (int l = 0; l < a.nlayers; ++l) {  // packed layout of ora_mlp_train_step
+    const int64_t I = a.widths[l], O = a.widths[l + 1], IO = I * O, BO = B * O;
+    int64_t* o = a.off[l];
+    for (int f = 0; f < 16; ++f) o[f] = 0;
+    o[F_W] = p; p += IO;
+    o[F_B] = p; p += O;
+    o[F_DW] = p; p += IO;
+    o[F_DB] = p; p += O;
+    if (a.bn) {
+      o[F_SCALES] = p; p += O;
+      o[F_RMEAN] = p; p += O;
+      o[F_RVAR] = p; p += O;
+      o[F_DSCALES] = p; p += O;
+    }
+    o[F_OUT] = p; p += BO;
+    o[F_DELTA] = p; p += BO;
+    if (a.bn) {
+      o[F_X] = p; p += BO;
+      o[F_XNORM] = p; p += BO;
+      o[F_MEAN] = p; p += O;
+      o[F_VAR] = p; p += O;
+      o[F_MDELTA] = p; p += O;
+      o[F_VDELTA] = p; p += O;
+    }
+  }
+  a.softmax_off = p;
   int64_t omax = 0;
   for (int l = 0; l < a.nlayers; ++l) omax = a.widths[l + 1] > omax ? a.widths[l + 1] : omax;
   const size_t lds = (size_t)(8 * a.batch * omax) * sizeof(float);

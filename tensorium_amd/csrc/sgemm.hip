@@ -46,28 +46,12 @@ int pick_variant(const GemmArgs& a, bool av, bool bv) {
 }
 
 // Implicit-GEMM conv tile choice.  No split-K (bit-exactness), so the
-// parallelism is the output tiles alone: estimate each shape's time as
-// (rounds of resident blocks) x (tile area / relative per-CU efficiency) and
-// take the cheapest.  Two 256-thread blocks are resident per CU.
+// parallelism is the output tiles alone; the YOLOv3 sweep (scripts/
+// conv_sweep.py) has the 64x64 tile best or within a few percent
+// on every layer with more than 32 filters, and 32x256 for the 32-filter one.
 int pick_conv_variant(const GemmArgs& a) {
-  struct Cand { int v, bm, bn; double eff; };
-  static const Cand cands[] = {{V_128x128, 128, 128, 1.00}, {V_128x64, 128, 64, 0.92},
-                               {V_64x128, 64, 128, 0.92},   {V_64x64, 64, 64, 0.70},
-                               {V_64x256, 64, 256, 0.95},   {V_32x256, 32, 256, 0.60}};
-  const double slots = 512.0;
-  int best = V_128x64;
-  double best_t = 1e300;
-  for (const Cand& c : cands) {
-    const double tiles_m = (double)((a.M + c.bm - 1) / c.bm);
-    const double tiles_n = (double)((a.N + c.bn - 1) / c.bn);
-    const double rounds = std::ceil(tiles_m * tiles_n / slots);
-    const double t = rounds * c.bm * c.bn / c.eff;
-    if (t < best_t) {
-      best_t = t;
-      best = c.v;
-    }
-  }
-  return best;
+  if (a.M <= 32) return V_32x256;
+  return V_64x64;
 }
 
 }  // namespace
@@ -78,14 +62,11 @@ hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t
   const bool av = vec4_ok(a.A, a.lda, a.strideA, a.batch, a.K);
   const int v = variant < 0 ? pick_conv_variant(a) : variant;
   switch (v) {
-    case V_128x128: return launch_conv_128x128(a, av, s);
     case V_128x64: return launch_conv_128x64(a, av, s);
     case V_64x128: return launch_conv_64x128(a, av, s);
-    case V_64x256: return launch_conv_64x256(a, av, s);
     case V_32x256: return launch_conv_32x256(a, av, s);
-    case V_256x256w8: return launch_conv_256x256w8(a, av, s);
     case V_64x64: return launch_conv_64x64(a, av, s);
-    default: return hipErrorInvalidValue;
+    default: return hipErrorInvalidValue;  // no implicit-conv instantiation
   }
 }
 

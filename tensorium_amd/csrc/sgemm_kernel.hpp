@@ -126,65 +126,72 @@ struct TileIO {
 
 // Implicit-GEMM B operand of a convolution: element (k, n) of the im2col
 // matrix, k = (c, kr, kc), n = (image, orow, ocol), read straight from the
-// images.  Each thread owns one column n for the whole launch (NT % BN == 0)
-// and walks k; k is wave-uniform, so its k-table entry is a scalar load,
-// fetched one k-tile ahead.  Same values as sim2Col (zero outside the
-// image) => bit-identical GEMM.
-template <int BK, int BN, int NT>
+// images.  Each thread owns one column n for the whole launch (NT % BN == 0);
+// the BN threads of a row group walk E consecutive k, so a wave's k-table
+// entries are one contiguous, wave-uniform run (scalar loads, fetched one
+// k-tile ahead).  Loads are buffer loads whose out-of-range offsets return 0:
+//   PADDED   the images were copied with their zero border materialised, and
+//            the k >= K sentinel is out of range: one add per element;
+//   checked  the window row/column are bounds-checked against H x W and a
+//            failing element gets an out-of-range offset.
+// Same values as sim2Col => bit-identical GEMM.
+template <int BK, int BN, int NT, bool PADDED>
 struct ConvBIO {
   static_assert(NT % BN == 0, "conv staging needs NT % BN == 0");
   static constexpr int E = BK * BN / NT;
-  static constexpr int KSTEP = NT / BN;
   static constexpr int LD = BN;
   struct State {
-    int base;      // image offset of the window origin (may be negative)
-    int ir0, ic0;  // window origin row / column
-    bool nok;
+    unsigned vbase;  // byte offset of this column's window origin
+    int ir0, ic0;    // window origin (checked form)
+    __amdgpu_buffer_rsrc_t rsrc;
   };
-  __device__ static __forceinline__ State init(const GemmArgs& p, int64_t n0, int tid) {
-    const int64_t n = n0 + tid % BN;
-    State st;
-    st.nok = n < p.N;
-    const int nn = st.nok ? (int)n : 0;
-    const int img = nn / p.conv_ohw;
-    const int pix = nn - img * p.conv_ohw;
+  __device__ static __forceinline__ State init(const GemmArgs& p, const float* im, int64_t n0,
+                                               int tid) {
+    int n = (int)(n0 + tid % BN);
+    n = n < (int)p.N ? n : (int)p.N - 1;  // columns past N: any valid pixel (not stored)
+    const int img = n / p.conv_ohw;
+    const int pix = n - img * p.conv_ohw;
     const int orow = pix / p.conv_ow;
     const int ocol = pix - orow * p.conv_ow;
-    st.ir0 = orow * p.conv_sY - p.conv_pH;
+    State st;
+    st.ir0 = orow * p.conv_sY - p.conv_pH;  // pH = pW = 0 for padded images
     st.ic0 = ocol * p.conv_sX - p.conv_pW;
-    st.base = img * (int)p.strideB + st.ir0 * p.conv_W + st.ic0;
+    st.vbase = 4u * (unsigned)(img * (int)p.strideB + st.ir0 * p.conv_W + st.ic0);
+    st.rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(im), 0, p.conv_bytes,
+                                                0x00020000);
     return st;
   }
-  // ktab has K+1 entries; entry K is a sentinel whose row offset fails the
-  // bounds check, so k >= K needs no post-processing of the loaded entry.
+  // entries k0 + kl*E + it, it < E (the table is padded past K with sentinels)
   __device__ static __forceinline__ void fetch(int4 (&tab)[E], const int4* __restrict__ ktab,
-                                               int k0, int K, int tid) {
+                                               int k0, int tid) {
     const int kl = __builtin_amdgcn_readfirstlane(tid / BN);  // wave-uniform
+    const int4* t = ktab + k0 + kl * E;
 #pragma unroll
     for (int it = 0; it < E; ++it) {
-      const int k = k0 + kl + KSTEP * it;
-      tab[it] = ktab[k < K ? k : K];
+      if constexpr (PADDED)
+        tab[it].x = t[it].x;
+      else
+        tab[it] = t[it];
     }
   }
-  __device__ static __forceinline__ void load(float (&r)[E], const float* __restrict__ im,
-                                              const State& st, const int4 (&tab)[E], int H,
-                                              int W) {
+  __device__ static __forceinline__ void load(float (&r)[E], const State& st, const int4 (&tab)[E],
+                                              const GemmArgs& p) {
 #pragma unroll
     for (int it = 0; it < E; ++it) {
-      const int4 t = tab[it];
-      // bitwise &: no short-circuit control flow around the loads
-      const bool ok = st.nok & ((unsigned)(st.ir0 + t.y) < (unsigned)H) &
-                      ((unsigned)(st.ic0 + t.z) < (unsigned)W);
-      r[it] = *(ok ? im + (unsigned)(st.base + t.x) : zero_page());
+      unsigned off = st.vbase + (unsigned)tab[it].x;
+      if constexpr (!PADDED) {
+        const bool ok = ((unsigned)(st.ir0 + tab[it].y) < (unsigned)p.conv_H) &
+                        ((unsigned)(st.ic0 + tab[it].z) < (unsigned)p.conv_W);
+        off = ok ? off : 0x80000000u;
+      }
+      r[it] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(st.rsrc, off, 0, 0));
     }
   }
   __device__ static __forceinline__ void store(const float (&r)[E], float* __restrict__ xs,
                                                int tid) {
+    const int kl = tid / BN, n = tid % BN;
 #pragma unroll
-    for (int it = 0; it < E; ++it) {
-      const int idx = tid + NT * it;
-      xs[(idx / BN) * LD + idx % BN] = r[it];
-    }
+    for (int it = 0; it < E; ++it) xs[(kl * E + it) * LD + n] = r[it];
   }
 };
 
@@ -239,14 +246,17 @@ __device__ __forceinline__ void mma_steps(floatx16 (&acc)[TM][TN], const float* 
   }
 }
 
-template <class S, bool TA, bool TB, int AV, int BV, bool CONV = false>
+// CONV: 0 = plain GEMM, 1 = implicit conv on padded images, 2 = implicit conv
+// with bounds checks
+template <class S, bool TA, bool TB, int AV, int BV, int CONV = 0>
 __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) {
   constexpr int BM = S::BM, BN = S::BN, BK = S::BK, NT = S::NT;
   constexpr int TM = S::TM, TN = S::TN, WTM = S::WTM, WTN = S::WTN;
   constexpr bool AKC = !TA;  // A is k-contiguous in memory
   constexpr bool BKC = TB;   // B is k-contiguous in memory
   using AIO = TileIO<AKC, AV, BK, BM, NT>;
-  using BIO = std::conditional_t<CONV, ConvBIO<BK, BN, NT>, TileIO<BKC, BV, BK, BN, NT>>;
+  using CIO = ConvBIO<BK, BN, NT, CONV == 1>;
+  using BIO = std::conditional_t<CONV != 0, CIO, TileIO<BKC, BV, BK, BN, NT>>;
   constexpr int LDA_S = AIO::LD, LDB_S = BIO::LD;
   constexpr int A_TILE = BK * LDA_S;
   constexpr int B_TILE = BK * LDB_S;
@@ -316,17 +326,16 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
   float ra[AIO::E], rb[BIO::E];
   const int a_off = h * LDA_S + wm * WTM + l31;
   const int b_off = h * LDB_S + wn * WTN + l31;
-  using CIO = ConvBIO<BK, BN, NT>;
   [[maybe_unused]] typename CIO::State cst;
   [[maybe_unused]] int4 ktab_next[CIO::E];
   if constexpr (CONV) {
-    cst = CIO::init(p, n0, tid);
-    CIO::fetch(ktab_next, p.ktab, 0, (int)K, tid);
+    cst = CIO::init(p, B, n0, tid);
+    CIO::fetch(ktab_next, p.ktab, 0, tid);
   }
   auto load_b = [&](float (&r)[BIO::E], int64_t k0) {
     if constexpr (CONV) {
-      CIO::load(r, B, cst, ktab_next, p.conv_H, p.conv_W);
-      CIO::fetch(ktab_next, p.ktab, (int)k0 + BK, (int)K, tid);  // next tile's entries
+      CIO::load(r, cst, ktab_next, p);
+      CIO::fetch(ktab_next, p.ktab, (int)k0 + BK, tid);  // next tile's entries
     } else {
       BIO::load(r, B, p.ldb, n0, k0, N, K, tid);
     }
@@ -412,7 +421,7 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
       }
     }
 }
-template <class S, bool TA, bool TB, int AV, int BV, bool CONV = false>
+template <class S, bool TA, bool TB, int AV, int BV, int CONV = 0>
 hipError_t launch_variant(const GemmArgs& a, hipStream_t s) {
   const int64_t tiles = ((a.M + S::BM - 1) / S::BM) * ((a.N + S::BN - 1) / S::BN);
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
@@ -458,11 +467,16 @@ hipError_t launch_trans4(const GemmArgs& a, bool ta, bool tb, bool av, bool bv, 
   return launch_variant<S, true, true, 4, 4>(a, s);
 }
 
-// implicit-GEMM convolution: NN, A (weights) float4 or scalar, B from the image
+// implicit-GEMM convolution: NN, A (weights) float4 or scalar, B from the
+// images (a.conv: 1 padded, 2 checked)
 template <class S>
 hipError_t launch_conv(const GemmArgs& a, bool av, hipStream_t s) {
-  if (av) return launch_variant<S, false, false, 4, 1, true>(a, s);
-  return launch_variant<S, false, false, 1, 1, true>(a, s);
+  if (a.conv == 1) {
+    if (av) return launch_variant<S, false, false, 4, 1, 1>(a, s);
+    return launch_variant<S, false, false, 1, 1, 1>(a, s);
+  }
+  if (av) return launch_variant<S, false, false, 4, 1, 2>(a, s);
+  return launch_variant<S, false, false, 1, 1, 2>(a, s);
 }
 
 // experimental tile shapes: NN with float4 operands only
@@ -510,13 +524,10 @@ typedef hipError_t (*ShapeLauncher)(const GemmArgs&, bool, bool, bool, bool, hip
 TNS_SHAPES(TNS_DECL)
 #undef TNS_DECL
 
-// implicit-GEMM conv launchers for the production shapes
-hipError_t launch_conv_128x128(const GemmArgs&, bool, hipStream_t);
+// implicit-GEMM conv launchers (the shapes the YOLOv3 sweep keeps)
 hipError_t launch_conv_128x64(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_64x128(const GemmArgs&, bool, hipStream_t);
-hipError_t launch_conv_64x256(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_32x256(const GemmArgs&, bool, hipStream_t);
-hipError_t launch_conv_256x256w8(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_64x64(const GemmArgs&, bool, hipStream_t);
 
 }  // namespace tns

@@ -16,9 +16,6 @@ hipError_t launch_shape_64x128(const GemmArgs& a, bool ta, bool tb, bool av, boo
   return sgemm_detail::launch_full<sgemm_detail::S64x128>(a, ta, tb, av, bv, s);
 }
 
-hipError_t launch_conv_128x128(const GemmArgs& a, bool av, hipStream_t s) {
-  return sgemm_detail::launch_conv<sgemm_detail::S128x128>(a, av, s);
-}
 
 hipError_t launch_conv_128x64(const GemmArgs& a, bool av, hipStream_t s) {
   return sgemm_detail::launch_conv<sgemm_detail::S128x64>(a, av, s);

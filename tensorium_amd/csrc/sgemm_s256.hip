@@ -8,8 +8,5 @@ hipError_t launch_shape_256x256w8(const GemmArgs& a, bool ta, bool tb, bool av, 
   return sgemm_detail::launch_trans4<sgemm_detail::S256x256w8>(a, ta, tb, av, bv, s);
 }
 
-hipError_t launch_conv_256x256w8(const GemmArgs& a, bool av, hipStream_t s) {
-  return sgemm_detail::launch_conv<sgemm_detail::S256x256w8>(a, av, s);
-}
 
 }  // namespace tns

@@ -12,9 +12,6 @@ hipError_t launch_shape_32x256(const GemmArgs& a, bool ta, bool tb, bool av, boo
   return sgemm_detail::launch_full<sgemm_detail::S32x256>(a, ta, tb, av, bv, s);
 }
 
-hipError_t launch_conv_64x256(const GemmArgs& a, bool av, hipStream_t s) {
-  return sgemm_detail::launch_conv<sgemm_detail::S64x256>(a, av, s);
-}
 
 hipError_t launch_conv_32x256(const GemmArgs& a, bool av, hipStream_t s) {
   return sgemm_detail::launch_conv<sgemm_detail::S32x256>(a, av, s);

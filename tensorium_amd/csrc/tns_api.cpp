@@ -28,6 +28,7 @@ static thread_local std::string g_err;
 static tns_error_hook_t g_hook = nullptr;
 static int64_t g_strict_beta0 = 1;
 static int64_t g_conv_variant = -1;
+static int64_t g_conv_pad = -1;
 
 int set_error(int code, const char* fmt, ...) {
   char buf[1024];
@@ -169,22 +170,24 @@ int check_geom(const ConvGeom& g) {
   return TNS_OK;
 }
 
-// k-table of an implicit-GEMM convolution, built once per geometry on the
-// context's stream (stream order makes it visible to the GEMM that follows)
-int get_ktab(tns_ctx* c, const ConvGeom& g, const int4** out) {
-  auto key = std::make_tuple(g.C, g.H, g.W, g.kH, g.kW, g.dY, g.dX);
+// k-table of an implicit-GEMM convolution over Hp x Wp padded images, built
+// once per geometry on the context's stream (stream order makes it visible to
+// the GEMM that follows)
+int get_ktab(tns_ctx* c, int64_t C, int64_t Hp, int64_t Wp, int64_t kH, int64_t kW, int64_t dY,
+             int64_t dX, const int4** out) {
+  auto key = std::make_tuple(C, Hp, Wp, kH, kW, dY, dX);
   auto it = c->ktabs.find(key);
   if (it != c->ktabs.end()) {
     *out = it->second;
     return TNS_OK;
   }
-  const int64_t K = g.C * g.kH * g.kW;
+  const int64_t K = C * kH * kW;
   int4* t = nullptr;
-  hipError_t e = hipMalloc(&t, (size_t)(K + 1) * sizeof(int4));  // + sentinel
+  hipError_t e = hipMalloc(&t, (size_t)(K + KTAB_PAD) * sizeof(int4));
   if (e != hipSuccess)
     return set_error(TNS_ERR_NOMEM, "hipMalloc(k-table) failed: %s", hipGetErrorString(e));
-  e = launch_build_ktab(t, (int)g.C, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.dY,
-                        (int)g.dX, c->stream);
+  e = launch_build_ktab(t, (int)C, (int)Hp, (int)Wp, (int)kH, (int)kW, (int)dY, (int)dX,
+                        c->stream);
   if (e != hipSuccess) {
     hipFree(t);
     return set_error(TNS_ERR_HIP, "k-table launch failed: %s", hipGetErrorString(e));
@@ -230,6 +233,9 @@ int tns_set_option(int32_t opt, int64_t value) {
       return TNS_OK;
     case TNS_OPT_CONV_VARIANT:
       g_conv_variant = value < 0 ? -1 : value;
+      return TNS_OK;
+    case TNS_OPT_CONV_PAD:
+      g_conv_pad = value < 0 ? -1 : (value ? 1 : 0);
       return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
@@ -595,7 +601,8 @@ int tns_hip_mlp_train_step(tns_ctx* c, int32_t nlayers, const int64_t* widths,
                            const float* truth, float learningRate, float momentum, float decay,
                            float* buf, float* cost) {
   if (int r = check_ctx(c)) return r;
-  if (nlayers <= 0 || nlayers > 32 || !widths || !acts || !X || !truth || !buf || !cost)
+  if (nlayers <= 0 || nlayers > MLP_MAX_LAYERS || !widths || !acts || !X || !truth || !buf ||
+      !cost)
     return set_error(TNS_ERR_ARG, "mlp_train_step: bad arguments");
   if (batch < 2) return set_error(TNS_ERR_ARG, "mlp_train_step: batch must be >= 2 (BN)");
   MlpArgs a;
@@ -697,29 +704,59 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
   const int64_t outImg = oh * ow, ks = kSize * kSize, k = C * ks;
   if (oh <= 0 || ow <= 0 || batch <= 0) return TNS_OK;
   const bool needs_col = ks != 1 || dilation != 1 || stride != 1;
-  if (fused == TNS_CONV_IMPLICIT || (fused == TNS_CONV_FUSED && needs_col)) {
-    // implicit GEMM: batch folded into N, images gathered in the B staging
+  // TNS_CONV_FUSED: implicit GEMM whenever a col matrix would be needed, and
+  // for 1x1 convolutions with small images (batch folded into N fills the
+  // tiles that a per-image GEMM with N = outH*outW < 1024 leaves ragged)
+  // (a padded 1x1/s1 convolution is left to the reference's direct path,
+  // which ignores the padding — ntensors.pas:8286)
+  const bool direct_ok = needs_col || padding == 0;
+  const bool implicit = direct_ok && (fused == TNS_CONV_IMPLICIT ||
+                                      (fused == TNS_CONV_FUSED && (needs_col || outImg < 1024)));
+  if (implicit) {
+    // implicit GEMM: batch folded into N, B gathered from zero-padded images
     if (!input || !weights || !out || !biases)
       return set_error(TNS_ERR_ARG, "conv_forward: null operand");
+    // Materialise the zero border (padded images, no bounds checks in the
+    // GEMM) when that copy costs under ~5% of the GEMM: copy time
+    // ~bytes/4 TB/s vs GEMM ~flops/80 TF/s.
+    const double flops = 2.0 * (double)filters * (double)(batch * outImg) * (double)k;
+    const int64_t Hpad = H + 2 * padding, Wpad = W + 2 * padding;
+    const bool padded = padding == 0 ||
+                        (g_conv_pad < 0 ? 8.0 * (double)(batch * C * Hpad * Wpad) * 400.0 < flops
+                                        : g_conv_pad == 1);
+    const int64_t Hs = padded ? Hpad : H, Ws = padded ? Wpad : W, img = C * Hs * Ws;
+    if (k > 0x7fffffffLL - KTAB_PAD || img * 4 > 0x7fffffffLL)
+      return set_error(TNS_ERR_ARG, "conv_forward: image too large for the implicit GEMM");
     const int4* kt = nullptr;
-    if (int r = get_ktab(c, g, &kt)) return r;
-    const int64_t img = C * H * W;
-    // 32-bit offsets inside one launch (ConvBIO): split the batch
-    const int64_t per = std::max<int64_t>(img, outImg);
-    const int64_t chunk = std::max<int64_t>(1, (int64_t)0x7fffffff / std::max<int64_t>(per, 1));
+    if (int r = get_ktab(c, C, Hs, Ws, kSize, kSize, dilation, dilation, &kt)) return r;
+    const float* src = input;
+    if (padded && padding > 0) {
+      float* pbuf = nullptr;
+      if (int r = ensure_scratch(c, 1, batch * img, &pbuf)) return r;
+      OpTimer t(c, TNS_OP_IM2COL);
+      if (int r = hip_status(launch_pad_images(input, batch, C, H, W, padding, padding, pbuf,
+                                               c->stream), "pad launch"))
+        return r;
+      src = pbuf;
+    }
+    // buffer offsets are 32-bit: images per launch such that the B extent
+    // stays below 2^31 bytes (and N below 2^31)
+    const int64_t chunk = std::max<int64_t>(
+        1, std::min<int64_t>(0x7fffffffLL / (4 * img), 0x7fffffffLL / std::max<int64_t>(outImg, 1)));
     for (int64_t b0 = 0; b0 < batch; b0 += chunk) {
       const int64_t nb = std::min(chunk, batch - b0);
       GemmArgs a{};
       a.M = filters; a.N = nb * outImg; a.K = k;
       a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_ZERO;
       a.A = weights; a.lda = k; a.strideA = 0;
-      a.B = input + b0 * img; a.ldb = outImg; a.strideB = img;
+      a.B = src + b0 * img; a.ldb = outImg; a.strideB = img;
       a.C = out + b0 * outImg * filters; a.ldc = outImg; a.strideC = outImg * filters;
       a.batch = 1; a.epi = EPI_BIAS_ACT; a.bias = biases; a.act = activation;
-      a.conv = 1; a.ktab = kt;
-      a.conv_H = (int)H; a.conv_W = (int)W; a.conv_ow = (int)ow; a.conv_ohw = (int)outImg;
+      a.conv = padded ? 1 : 2; a.ktab = kt;
+      a.conv_H = (int)Hs; a.conv_W = (int)Ws; a.conv_ow = (int)ow; a.conv_ohw = (int)outImg;
       a.conv_sY = (int)stride; a.conv_sX = (int)stride;
-      a.conv_pH = (int)padding; a.conv_pW = (int)padding;
+      a.conv_pH = padded ? 0 : (int)padding; a.conv_pW = a.conv_pH;
+      a.conv_bytes = (int)(4 * nb * img);
       OpTimer t(c, TNS_OP_GEMM);
       hipError_t e = launch_sgemm_conv_variant((int)g_conv_variant, a, c->stream);
       if (e == hipErrorInvalidValue)

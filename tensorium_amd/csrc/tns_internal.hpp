@@ -50,23 +50,32 @@ struct GemmArgs {
   // implicit-GEMM convolution: when conv != 0 the batch is
   // folded into N (column n = image n / conv_ohw, pixel n % conv_ohw; the
   // launch has batch == 1) and B is the im2col matrix of the images at
-  // B + image*strideB, generated inside the GEMM's staging loads and never
-  // written to memory; C of image i starts at C + i*strideC.  ktab[k] for
-  // k = (c*kH + kr)*kW + kc holds {c*H*W + kr*dY*W + kc*dX, kr*dY, kc*dX, 0};
-  // ktab[K] is a sentinel that fails the bounds check.
-  // All image offsets fit in 32 bits (the host splits the batch).
+  // B + image*strideB (conv_H x conv_W each), generated inside the GEMM's
+  // staging loads (buffer loads over conv_bytes) and never written to memory;
+  // C of image i starts at C + i*strideC.
+  //   conv == 1: the images are zero-padded copies (conv_pH = conv_pW = 0);
+  //   conv == 2: unpadded images, window bounds checked (pads conv_pH/pW).
+  // ktab[k] = {4*(c*H*W + kr*dY*W + kc*dX), kr*dY, kc*dX, 0} for the stored
+  // image size and k = (c*kH + kr)*kW + kc; entries k >= K are sentinels
+  // {0x80000000, 2^30, 2^30, 0} (out of range: the buffer load returns 0).
   int conv;
   const int4* ktab;
   int conv_H, conv_W, conv_ow, conv_ohw, conv_sY, conv_sX, conv_pH, conv_pW;
+  int conv_bytes;
 };
 
 hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s);
 // implicit-GEMM convolution: NN, B generated from the image (a.conv must be set)
 hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s);
 hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s);
-// builds the k-table of an implicit-GEMM convolution on the stream
-hipError_t launch_build_ktab(int4* ktab, int C, int H, int W, int kH, int kW, int dY, int dX,
+// k-table of an implicit-GEMM convolution over stored Hs x Ws images (padded
+// or not): K = C*kH*kW entries plus KTAB_PAD sentinels
+constexpr int KTAB_PAD = 256;
+hipError_t launch_build_ktab(int4* ktab, int C, int Hs, int Ws, int kH, int kW, int dY, int dX,
                              hipStream_t s);
+// zero-padded copy of a batch of images: [batch][C][H+2pH][W+2pW]
+hipError_t launch_pad_images(const float* im, int64_t batch, int64_t C, int64_t H, int64_t W,
+                             int64_t pH, int64_t pW, float* out, hipStream_t s);
 // variant < 0 picks the tile shape by heuristic; otherwise forces one (tuning)
 hipError_t launch_sgemm_variant(int variant, const GemmArgs& a, bool transA, bool transB,
                                 hipStream_t s);
@@ -129,10 +138,11 @@ hipError_t launch_xent_softmax(int64_t n, const float* pred, const float* truth,
 hipError_t launch_vssum(int64_t n, const float* a, float* out, hipStream_t s);
 
 // ---- fused connected-network train step (mlp_train.hip) ---------------------
+constexpr int MLP_MAX_LAYERS = 16;
 struct MlpArgs {
   int nlayers;
-  int64_t widths[33];
-  int acts[32];
+  int64_t widths[MLP_MAX_LAYERS + 1];
+  int acts[MLP_MAX_LAYERS];
   int bn;
   int64_t batch;
   const float* X;
@@ -140,6 +150,9 @@ struct MlpArgs {
   float lr, momentum, decay;
   float* buf;   // packed parameters / state, layout of ora_mlp_train_step
   float* cost;  // one float
+  // filled by launch_mlp_train_step: element offsets of each layer's arrays
+  int64_t off[MLP_MAX_LAYERS][16];
+  int64_t softmax_off;
 };
 int64_t mlp_buffer_floats(int nlayers, const int64_t* widths, int bn, int64_t batch);
 hipError_t launch_mlp_train_step(const MlpArgs& a, hipStream_t s);

@@ -201,6 +201,10 @@ class TNNHip:
         """Force the implicit-GEMM tile shape (-1 = heuristic); process-wide."""
         check(self.lib.tns_set_option(1, int(variant)))
 
+    def setConvPad(self, mode: int = -1):
+        """Implicit-GEMM gather: 1 padded copy, 0 bounds-checked, -1 by cost."""
+        check(self.lib.tns_set_option(2, int(mode)))
+
     # -- batch norm / softmax (TNNCuda.meansAndVars ... crossEntropySoftmax) ----
     def meansAndVars(self, srcSize, dstSize, groups, src, offset, means, vars_):
         check(self.lib.tns_hip_means_and_vars(self.ctx, srcSize, dstSize, groups, _ptr(src),
