@@ -133,7 +133,9 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
 
 def check(rc: int) -> None:
     if rc != TNS_OK:
-        msg = load().tns_last_error().decode(errors="replace")
+        lib = load()
+        msg = lib.tns_last_error().decode(errors="replace")
+        lib.tns_clear_error()  # consumed: a later op-table call starts clean
         raise TnsError(f"tns status {rc}: {msg}")
 
 
