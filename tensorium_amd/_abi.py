@@ -117,7 +117,8 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # TNS_LIB: an alternative build of the same library (A/B perf runs)
+    p = Path(path) if path else Path(os.environ.get("TNS_LIB") or LIB_PATH)
     if not p.exists():
         raise TnsError(f"{p} not built — run `python -m tensorium_amd.build` "
                        "(the HIP backend has no CPU fallback)")

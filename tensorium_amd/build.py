@@ -54,13 +54,17 @@ def _run(cmd: list[str], verbose: bool) -> None:
         sys.stderr.write(r.stdout + r.stderr)
 
 
-def build_hip(verbose: bool = False, force: bool = False) -> Path:
-    BUILD.mkdir(exist_ok=True)
+def build_hip(verbose: bool = False, force: bool = False, out: Path | None = None) -> Path:
+    """Compile csrc/ into LIB (or into out/libtensorium_hip.so, objects under
+    out/_build — side builds for A/B perf runs)."""
+    build = (out / "_build") if out else BUILD
+    lib_path = (out / "libtensorium_hip.so") if out else LIB
+    build.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.hpp")) + [ROOT / "include" / "tns.h"]
     objs: list[Path] = []
     jobs = []
     for src in _sources():
-        obj = BUILD / (src.name + ".o")
+        obj = build / (src.name + ".o")
         objs.append(obj)
         if force or _newer(obj, [src, *headers]):
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
@@ -68,12 +72,12 @@ def build_hip(verbose: bool = False, force: bool = False) -> Path:
     if jobs:
         with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs))
-    if force or jobs or _newer(LIB, objs):
-        tmp = LIB.with_suffix(".so.tmp")
+    if force or jobs or _newer(lib_path, objs):
+        tmp = lib_path.with_suffix(".so.tmp")
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o",
               str(tmp)], verbose)
-        os.replace(tmp, LIB)
-    return LIB
+        os.replace(tmp, lib_path)
+    return lib_path
 
 
 def build_oracle(verbose: bool = False) -> Path:
@@ -89,5 +93,8 @@ def build_all(verbose: bool = False, force: bool = False) -> None:
 
 
 if __name__ == "__main__":
-    build_all(verbose=True, force="--force" in sys.argv)
-    print(LIB)
+    if "--out" in sys.argv:
+        print(build_hip(True, "--force" in sys.argv, Path(sys.argv[sys.argv.index("--out") + 1])))
+    else:
+        build_all(verbose=True, force="--force" in sys.argv)
+        print(LIB)
