@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 from tensorium_amd.nnhip import TNNHip  # noqa: E402
 from tensorium_amd.yolo import yolov3_conv_table  # noqa: E402
 
-IMPLICIT_VARIANTS = [1, 2, 4, 6]
+IMPLICIT_VARIANTS = [2, 6, 12, 13, 14, 15]
 
 
 def time_conv(hip, layer, mode, variant, reps, pad=-1):
@@ -61,8 +61,7 @@ def main():
         out = torch.empty(args.batch, s.filters, s.N, device="cuda")
         layers[f"L{s.index}_c{s.c}_h{s.h}_f{s.filters}_k{s.size}s{s.stride}"] = (
             (s, x, w, b, ws, out, args.batch), s)
-    cfgs = [("im2col", 2, -1, -1), ("implicit_auto", 3, -1, -1),
-            ("implicit_64x64_checked", 3, 6, 0), ("implicit_64x64_padded", 3, 6, 1)] + \
+    cfgs = [("im2col", 2, -1, -1), ("implicit_auto", 3, -1, -1)] + \
         [(f"implicit_{names[v]}", 3, v, -1) for v in IMPLICIT_VARIANTS]
     res = {k: {c[0]: [] for c in cfgs} for k in layers}
     for _ in range(args.rounds):

@@ -18,13 +18,19 @@ from tensorium_amd.nnhip import TNNHip  # noqa: E402
 from tensorium_amd.yolo import yolov3_conv_table  # noqa: E402
 
 
+_warned = set()
+
+
 def time_variant(hip, v, prob, reps):
     M, N, K, batch, A, B, C = prob
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     try:
         hip.gemmVariant(v, False, False, M, N, K, 1.0, A, 0, K, 0 if batch > 1 else 0, B, 0, N,
                         K * N, 0.0, C, 0, N, M * N, batch)
-    except Exception:
+    except Exception as e:
+        if v not in _warned:
+            _warned.add(v)
+            print(f"variant {v}: {e}", flush=True)
         return None
     torch.cuda.synchronize()
     ev0.record()

@@ -68,7 +68,8 @@ def build_hip(verbose: bool = False, force: bool = False, out: Path | None = Non
         objs.append(obj)
         if force or _newer(obj, [src, *headers]):
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
-            jobs.append([HIPCC, *CXXFLAGS, *lang, "-c", str(src), "-o", str(obj)])
+            extra = os.environ.get("TNS_EXTRA_CFLAGS", "").split()  # A/B side builds
+            jobs.append([HIPCC, *CXXFLAGS, *extra, *lang, "-c", str(src), "-o", str(obj)])
     if jobs:
         with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs))

@@ -27,17 +27,19 @@ namespace {
 // k-table of the implicit-GEMM convolution: the im2col row k = (c, kr, kc)
 // reads padded image element [c][orow*sY + kr*dY][ocol*sX + kc*dX] — the same
 // element sim2Col copies (ntensors.pas:11460), shifted by the padding.
-__global__ void ktab_kernel(int4* t, int K, int total, int Hs, int Ws, int kH, int kW, int dY,
+__global__ void ktab_kernel(int* t, int K, int total, int Hs, int Ws, int kH, int kW, int dY,
                             int dX) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= total) return;
   if (k >= K) {  // sentinel: out of the buffer's range and of any window
-    t[k] = make_int4((int)0x80000000u, 0x40000000, 0x40000000, 0);
+    t[k] = (int)0x80000000u;
+    t[total + k] = 0x4000 | (0x4000 << 16);
     return;
   }
   const int kc = k % kW, r = k / kW;
   const int kr = r % kH, c = r / kH;
-  t[k] = make_int4(4 * (c * Hs * Ws + kr * dY * Ws + kc * dX), kr * dY, kc * dX, 0);
+  t[k] = 4 * (c * Hs * Ws + kr * dY * Ws + kc * dX);
+  t[total + k] = (kr * dY) | ((kc * dX) << 16);
 }
 
 __global__ void pad_kernel(const float* __restrict__ im, float* __restrict__ out, int64_t planes,
@@ -58,7 +60,7 @@ __global__ void pad_kernel(const float* __restrict__ im, float* __restrict__ out
 }
 }  // namespace
 
-hipError_t launch_build_ktab(int4* ktab, int C, int Hp, int Wp, int kH, int kW, int dY, int dX,
+hipError_t launch_build_ktab(int* ktab, int C, int Hp, int Wp, int kH, int kW, int dY, int dX,
                              hipStream_t s) {
   const int K = C * kH * kW;
   if (K < 0) return hipErrorInvalidValue;

@@ -33,16 +33,19 @@ namespace tns {
 namespace sgemm_detail {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int GROUP_M = 8;
 
 // LDS row length of a k-major operand image.  K-contiguous operands are
 // transposed on the way in (scalar ds_writes); a row length ≡ 1 (mod 32)
 // makes those writes conflict-free.  MN-contiguous operands are written with
-// ds_write_b128 and keep the plain length.
-template <bool KCONTIG, int BMN>
+// ds_write_b128 and keep the plain length.  With 16x16 MFMA fragments the two
+// 16-lane halves of a ds_read_b32 group read consecutive k rows, so the rows
+// are also shifted by 16 banks (≡ 16 or 17 mod 32).
+template <bool KCONTIG, int BMN, int MF>
 struct LdsLd {
-  static constexpr int value = KCONTIG ? BMN + 1 : BMN;
+  static constexpr int value = (KCONTIG ? BMN + 1 : BMN) + (MF == 16 ? 16 : 0);
 };
 
 // 16 zero bytes every out-of-range staging load reads instead of the operand.
@@ -58,11 +61,11 @@ __device__ __forceinline__ const float* zero_page() {
 // redirected to the zero page.  VEC=4
 // is only instantiated when the contiguous extent is a multiple of 4 (the
 // host checks), so a float4 is either wholly inside or wholly outside.
-template <bool KCONTIG, int VEC, int BK, int BMN, int NT>
+template <bool KCONTIG, int VEC, int BK, int BMN, int NT, int MF>
 struct TileIO {
   static constexpr int E = BK * BMN / NT;
   static_assert(E % VEC == 0, "tile not divisible");
-  static constexpr int LD = LdsLd<KCONTIG, BMN>::value;
+  static constexpr int LD = LdsLd<KCONTIG, BMN, MF>::value;
 
   __device__ static __forceinline__ void load(float (&r)[E], const float* __restrict__ base,
                                               int64_t ld, int64_t mn0, int64_t k0, int64_t MN,
@@ -135,11 +138,11 @@ struct TileIO {
 //   checked  the window row/column are bounds-checked against H x W and a
 //            failing element gets an out-of-range offset.
 // Same values as sim2Col => bit-identical GEMM.
-template <int BK, int BN, int NT, bool PADDED>
+template <int BK, int BN, int NT, bool PADDED, int MF>
 struct ConvBIO {
   static_assert(NT % BN == 0, "conv staging needs NT % BN == 0");
   static constexpr int E = BK * BN / NT;
-  static constexpr int LD = BN;
+  static constexpr int LD = LdsLd<false, BN, MF>::value;
   struct State {
     unsigned vbase;  // byte offset of this column's window origin
     int ir0, ic0;    // window origin (checked form)
@@ -161,27 +164,40 @@ struct ConvBIO {
                                                 0x00020000);
     return st;
   }
-  // entries k0 + kl*E + it, it < E (the table is padded past K with sentinels)
-  __device__ static __forceinline__ void fetch(int4 (&tab)[E], const int4* __restrict__ ktab,
-                                               int k0, int tid) {
-    const int kl = __builtin_amdgcn_readfirstlane(tid / BN);  // wave-uniform
-    const int4* t = ktab + k0 + kl * E;
+  // entries k0 + kl*E + it, it < E (the table is padded past K with
+  // sentinels).  Fetched with vector buffer loads (E/4 x dwordx4): scalar
+  // loads would share lgkmcnt with the LDS traffic and force full drains.
+  struct Tab {
+    int x[E];
+    int yz[E];  // checked form only: kr*dY | kc*dX << 16
+  };
+  static_assert(E % 4 == 0, "k-table fetched as dwordx4");
+  __device__ static __forceinline__ void fetch(Tab& tab, const GemmArgs& p,
+                                               __amdgpu_buffer_rsrc_t trs, int k0, int tid) {
+    // wave-uniform when a wave's 64 lanes lie in one row group (BN >= 64)
+    const int kl = tid / BN;
+    const int off = 4 * (k0 + kl * E);
 #pragma unroll
-    for (int it = 0; it < E; ++it) {
-      if constexpr (PADDED)
-        tab[it].x = t[it].x;
-      else
-        tab[it] = t[it];
+    for (int q = 0; q < E / 4; ++q) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(trs, off + 16 * q, 0, 0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) tab.x[4 * q + c] = (int)v[c];
+      if constexpr (!PADDED) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b128(trs, off + 16 * q, 4 * p.ktab_n, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) tab.yz[4 * q + c] = (int)w[c];
+      }
     }
   }
-  __device__ static __forceinline__ void load(float (&r)[E], const State& st, const int4 (&tab)[E],
+  __device__ static __forceinline__ void load(float (&r)[E], const State& st, const Tab& tab,
                                               const GemmArgs& p) {
 #pragma unroll
     for (int it = 0; it < E; ++it) {
-      unsigned off = st.vbase + (unsigned)tab[it].x;
+      unsigned off = st.vbase + (unsigned)tab.x[it];
       if constexpr (!PADDED) {
-        const bool ok = ((unsigned)(st.ir0 + tab[it].y) < (unsigned)p.conv_H) &
-                        ((unsigned)(st.ic0 + tab[it].z) < (unsigned)p.conv_W);
+        const int y = tab.yz[it] & 0xffff, z = (int)((unsigned)tab.yz[it] >> 16);
+        const bool ok = ((unsigned)(st.ir0 + y) < (unsigned)p.conv_H) &
+                        ((unsigned)(st.ic0 + z) < (unsigned)p.conv_W);
         off = ok ? off : 0x80000000u;
       }
       r[it] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(st.rsrc, off, 0, 0));
@@ -215,34 +231,89 @@ __device__ __forceinline__ void map_tile(int bid, int tiles_m, int tiles_n, int&
 // DEPTH_: how many k-tiles ahead the global loads run (register stages).
 // Small tiles spend few cycles per k-tile, so one tile of lead does not cover
 // the global-load latency; they load two tiles ahead.
-template <int BM_, int BN_, int BK_, int WM_, int WN_, int MINW_, int DEPTH_ = 1>
+// MF: MFMA tile, 32 (v_mfma_f32_32x32x2_f32: 2 k per step, lane half h = k)
+// or 16 (v_mfma_f32_16x16x4_f32: 4 k per step, lane quarter q = k).  Both are
+// bit-exact ascending-k fmaf chains on gfx950 (profiles/r01_mfma_order_probe.txt).
+// 16x16 tiles give four times as many independent accumulator chains per
+// output area: finer work granularity for GEMMs with few output tiles.
+template <int BM_, int BN_, int BK_, int WM_, int WN_, int MINW_, int DEPTH_ = 1, int MF_ = 32>
 struct Shape {
   static constexpr int BM = BM_, BN = BN_, BK = BK_, WM = WM_, WN = WN_, MINW = MINW_;
   static constexpr int DEPTH = DEPTH_;
+  static constexpr int MF = MF_;
+  static_assert(MF == 32 || MF == 16, "MFMA tile 32x32x2 or 16x16x4");
   static_assert(DEPTH == 1 || DEPTH == 2, "prefetch depth 1 or 2");
   static constexpr int NT = 64 * WM * WN;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
-  static constexpr int TM = WTM / 32, TN = WTN / 32;
-  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0, "bad wave tile");
+  static constexpr int TM = WTM / MF, TN = WTN / MF;
+  static constexpr int KS = 64 / MF;        // k per MFMA step
+  static constexpr int NE = MF * MF / 64;   // accumulator registers per lane
+  static_assert(TM >= 1 && TN >= 1 && WTM % MF == 0 && WTN % MF == 0, "bad wave tile");
+  static_assert(BK % (2 * KS) == 0, "k-tile = two halves of MFMA steps");
 };
 
-// MFMA steps [S0, S1) of one k-tile: step s consumes k = 2s (lanes 0-31) and
-// 2s+1 (lanes 32-63) — ascending k per accumulator.
-template <int TM, int TN, int LDA_S, int LDB_S, int S0, int S1>
-__device__ __forceinline__ void mma_steps(floatx16 (&acc)[TM][TN], const float* ap,
+template <int MF>
+struct Acc;
+template <>
+struct Acc<32> {
+  typedef floatx16 type;
+  __device__ static __forceinline__ type mma(float a, float b, type c) {
+    return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct Acc<16> {
+  typedef floatx4 type;
+  __device__ static __forceinline__ type mma(float a, float b, type c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+};
+
+// MFMA steps [S0, S1) of one k-tile: step s consumes k = KS*s + lane/MF
+// (lane half for 32x32x2, lane quarter for 16x16x4) — ascending k per
+// accumulator (the MFMA chains its k in lane-group order).
+// TNS_PREREAD: issue every fragment read of the half-tile before its first
+// MFMA (the waits then drain progressively instead of one full LDS latency
+// per step pair).
+#ifndef TNS_PREREAD
+#define TNS_PREREAD 0
+#endif
+template <int MF, int TM, int TN, int LDA_S, int LDB_S, int S0, int S1>
+__device__ __forceinline__ void mma_steps(typename Acc<MF>::type (&acc)[TM][TN], const float* ap,
                                           const float* bp) {
+  constexpr int KS = 64 / MF;
+  // small wave tiles: all reads first (registers are plentiful there)
+  constexpr bool PRE = TNS_PREREAD && (TM + TN) * (S1 - S0) <= 24;
+  if constexpr (PRE) {
+    float a[S1 - S0][TM], b[S1 - S0][TN];
 #pragma unroll
-  for (int s = S0; s < S1; ++s) {
-    float a[TM], b[TN];
+    for (int s = S0; s < S1; ++s) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i) a[i] = ap[2 * s * LDA_S + 32 * i];
+      for (int i = 0; i < TM; ++i) a[s - S0][i] = ap[KS * s * LDA_S + MF * i];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) b[j] = bp[2 * s * LDB_S + 32 * j];
+      for (int j = 0; j < TN; ++j) b[s - S0][j] = bp[KS * s * LDB_S + MF * j];
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int s = S0; s < S1; ++s)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = Acc<MF>::mma(a[s - S0][i], b[s - S0][j], acc[i][j]);
+  } else {
+#pragma unroll
+    for (int s = S0; s < S1; ++s) {
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = ap[KS * s * LDA_S + MF * i];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = bp[KS * s * LDB_S + MF * j];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = Acc<MF>::mma(a[i], b[j], acc[i][j]);
+    }
   }
 }
 
@@ -252,11 +323,12 @@ template <class S, bool TA, bool TB, int AV, int BV, int CONV = 0>
 __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) {
   constexpr int BM = S::BM, BN = S::BN, BK = S::BK, NT = S::NT;
   constexpr int TM = S::TM, TN = S::TN, WTM = S::WTM, WTN = S::WTN;
+  constexpr int MF = S::MF, KS = S::KS, NE = S::NE;
   constexpr bool AKC = !TA;  // A is k-contiguous in memory
   constexpr bool BKC = TB;   // B is k-contiguous in memory
-  using AIO = TileIO<AKC, AV, BK, BM, NT>;
-  using CIO = ConvBIO<BK, BN, NT, CONV == 1>;
-  using BIO = std::conditional_t<CONV != 0, CIO, TileIO<BKC, BV, BK, BN, NT>>;
+  using AIO = TileIO<AKC, AV, BK, BM, NT, S::MF>;
+  using CIO = ConvBIO<BK, BN, NT, CONV == 1, S::MF>;
+  using BIO = std::conditional_t<CONV != 0, CIO, TileIO<BKC, BV, BK, BN, NT, S::MF>>;
   constexpr int LDA_S = AIO::LD, LDB_S = BIO::LD;
   constexpr int A_TILE = BK * LDA_S;
   constexpr int B_TILE = BK * LDB_S;
@@ -265,8 +337,8 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int l31 = lane & 31;
-  const int h = lane >> 5;
+  const int lc = lane % MF;  // accumulator column / operand row of this lane
+  const int h = lane / MF;   // k within an MFMA step; 4h = first output row
   const int wid = tid >> 6;
   const int wm = wid / S::WN, wn = wid % S::WN;
 
@@ -293,15 +365,17 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
   };
 
   // ---- accumulator init: 0, C, or beta*C (reference mulvs pre-scale) -----
-  floatx16 acc[TM][TN];
+  // accumulator register e of tile (i, j) holds C[row_base + i*MF + erow(e)]
+  // [col_base + j*MF]; erow(e) = (e & 3) + 8*(e >> 2) (e < 4 for 16x16)
+  typename Acc<MF>::type acc[TM][TN];
   const int64_t row_base = m0 + wm * WTM + 4 * h;
-  const int64_t col_base = n0 + wn * WTN + l31;
+  const int64_t col_base = n0 + wn * WTN + lc;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+      for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.0f;
   if (!CONV && p.beta_mode != BETA_ZERO) {  // (conv output is write-only)
     const bool scale = p.beta_mode == BETA_SCALE;
     const float beta = p.beta;
@@ -310,9 +384,9 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int64_t row = row_base + i * 32 + (e & 3) + 8 * (e >> 2);
-          const int64_t col = col_base + j * 32;
+        for (int e = 0; e < NE; ++e) {
+          const int64_t row = row_base + i * MF + (e & 3) + 8 * (e >> 2);
+          const int64_t col = col_base + j * MF;
           const bool ok = row < M && col < N;
           float v = C[ok ? c_at(row, col) : 0];
           v = scale ? beta * v : v;
@@ -324,18 +398,25 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
   const bool scale_a = p.alpha != 1.0f;
   const float alpha = p.alpha;
   float ra[AIO::E], rb[BIO::E];
-  const int a_off = h * LDA_S + wm * WTM + l31;
-  const int b_off = h * LDB_S + wn * WTN + l31;
+  const int a_off = h * LDA_S + wm * WTM + lc;
+  const int b_off = h * LDB_S + wn * WTN + lc;
   [[maybe_unused]] typename CIO::State cst;
-  [[maybe_unused]] int4 ktab_next[CIO::E];
+  // k-table entries of two consecutive tiles (ping-pong by tile parity):
+  // the next tile's are fetched BEFORE this tile's gathers are issued, so
+  // waiting for them never drains this tile's loads
+  [[maybe_unused]] typename CIO::Tab tabs[2];
+  [[maybe_unused]] __amdgpu_buffer_rsrc_t trs;
   if constexpr (CONV) {
     cst = CIO::init(p, B, n0, tid);
-    CIO::fetch(ktab_next, p.ktab, 0, tid);
+    trs = __builtin_amdgcn_make_buffer_rsrc(const_cast<int*>(p.ktab), 0, 8 * p.ktab_n,
+                                            0x00020000);
+    CIO::fetch(tabs[0], p, trs, 0, tid);
   }
-  auto load_b = [&](float (&r)[BIO::E], int64_t k0) {
+  auto load_b = [&](float (&r)[BIO::E], int64_t k0, auto TP) {  // TP: tile parity
     if constexpr (CONV) {
-      CIO::load(r, cst, ktab_next, p);
-      CIO::fetch(ktab_next, p.ktab, (int)k0 + BK, tid);  // next tile's entries
+      constexpr int tp = decltype(TP)::value;
+      CIO::fetch(tabs[tp ^ 1], p, trs, (int)k0 + BK, tid);  // next tile's entries
+      CIO::load(r, cst, tabs[tp], p);
     } else {
       BIO::load(r, B, p.ldb, n0, k0, N, K, tid);
     }
@@ -361,13 +442,13 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
     // branch here would merge the wait counters and force an early wait)
     const int64_t kl = (int64_t)(t + S::DEPTH) * BK;
     AIO::load(lra, A, p.lda, m0, kl, M, K, tid);
-    load_b(lrb, kl);
-    constexpr int SP = BK / 4;
-    mma_steps<TM, TN, LDA_S, LDB_S, 0, SP>(acc, as + a_off, as + A_TILE + b_off);
+    load_b(lrb, kl, std::integral_constant<int, (par + S::DEPTH) & 1>{});
+    constexpr int SP = BK / (2 * KS);  // half of the k-tile's MFMA steps
+    mma_steps<MF, TM, TN, LDA_S, LDB_S, 0, SP>(acc, as + a_off, as + A_TILE + b_off);
     scale(sra);
     AIO::store(sra, nxt, tid);
     BIO::store(srb, nxt + A_TILE, tid);
-    mma_steps<TM, TN, LDA_S, LDB_S, SP, BK / 2>(acc, as + a_off, as + A_TILE + b_off);
+    mma_steps<MF, TM, TN, LDA_S, LDB_S, SP, 2 * SP>(acc, as + a_off, as + A_TILE + b_off);
     __syncthreads();
   };
   using P0 = std::integral_constant<int, 0>;
@@ -375,29 +456,33 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
 
   if (nt > 0) {
     AIO::load(ra, A, p.lda, m0, 0, M, K, tid);
-    load_b(rb, 0);
+    load_b(rb, 0, std::integral_constant<int, 0>{});
     scale(ra);
     AIO::store(ra, smem, tid);
     BIO::store(rb, smem + A_TILE, tid);
     if constexpr (S::DEPTH == 1) {
       __syncthreads();
-      // registers are reloaded each tile and stored in the same tile
-      for (int t = 0; t < nt; t += 2) {
+      // registers are reloaded each tile and stored in the same tile.  Pairs
+      // of tiles, then the odd last one outside the loop (an exit inside the
+      // body would make the compiler copy the accumulators every iteration)
+      int t = 0;
+      for (; t + 1 < nt; t += 2) {
         step(ra, rb, ra, rb, t, P0{});
-        if (t + 1 >= nt) break;
         step(ra, rb, ra, rb, t + 1, P1{});
       }
+      if (t < nt) step(ra, rb, ra, rb, t, P0{});
     } else {
       float ra2[AIO::E], rb2[BIO::E];
       AIO::load(ra2, A, p.lda, m0, BK, M, K, tid);
-      load_b(rb2, BK);
+      load_b(rb2, BK, std::integral_constant<int, 1>{});
       __syncthreads();
       // (ra2, rb2) hold tile t+1 at even t; (ra, rb) at odd t
-      for (int t = 0; t < nt; t += 2) {
+      int t = 0;
+      for (; t + 1 < nt; t += 2) {
         step(ra, rb, ra2, rb2, t, P0{});
-        if (t + 1 >= nt) break;
         step(ra2, rb2, ra, rb, t + 1, P1{});
       }
+      if (t < nt) step(ra, rb, ra2, rb2, t, P0{});
     }
   }
 
@@ -407,13 +492,13 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int64_t row = row_base + i * 32 + (e & 3) + 8 * (e >> 2);
+    for (int e = 0; e < NE; ++e) {
+      const int64_t row = row_base + i * MF + (e & 3) + 8 * (e >> 2);
       if (row >= M) continue;
       const float bias = fuse ? p.bias[row] : 0.0f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int64_t col = col_base + j * 32;
+        const int64_t col = col_base + j * MF;
         if (col >= N) continue;
         float v = acc[i][j][e];
         if (fuse) v = act_apply(v + bias, act);  // forwardBias then activate
@@ -499,6 +584,13 @@ using S256x128 = Shape<256, 128, 32, 2, 2, 1>;
 using S128x256 = Shape<128, 256, 32, 2, 2, 1>;
 using S256x256w8 = Shape<256, 256, 32, 2, 4, 2>;
 using S256x128k16 = Shape<256, 128, 16, 2, 2, 2>;
+// 16x16x4 MFMA tiles                     BM   BN  BK WM WN MINW DEPTH MF
+using S64x64m16 = Shape<64, 64, 32, 2, 2, 2, 2, 16>;
+using S32x32m16 = Shape<32, 32, 32, 2, 2, 2, 2, 16>;
+using S64x32m16 = Shape<64, 32, 32, 2, 2, 2, 2, 16>;
+using S32x64m16 = Shape<32, 64, 32, 2, 2, 2, 2, 16>;
+using S128x128m16 = Shape<128, 128, 32, 2, 2, 2, 1, 16>;
+using S256x256w8m16 = Shape<256, 256, 32, 2, 4, 2, 1, 16>;
 
 
 }  // namespace sgemm_detail
@@ -517,7 +609,13 @@ typedef hipError_t (*ShapeLauncher)(const GemmArgs&, bool, bool, bool, bool, hip
   X(256x256k16, "256x256x16_w2x2", 256, 256, launch_nn4) \
   X(256x128, "256x128x32_w2x2", 256, 128, launch_nn4)    \
   X(128x256, "128x256x32_w2x2", 128, 256, launch_nn4)    \
-  X(256x128k16, "256x128x16_w2x2", 256, 128, launch_nn4)
+  X(256x128k16, "256x128x16_w2x2", 256, 128, launch_nn4) \
+  X(64x64m16, "64x64x32_w2x2_m16", 64, 64, launch_full)  \
+  X(32x32m16, "32x32x32_w2x2_m16", 32, 32, launch_full)  \
+  X(64x32m16, "64x32x32_w2x2_m16", 64, 32, launch_nn4)   \
+  X(32x64m16, "32x64x32_w2x2_m16", 32, 64, launch_nn4)   \
+  X(128x128m16, "128x128x32_w2x2_m16", 128, 128, launch_nn4) \
+  X(256x256w8m16, "256x256x32_w2x4_m16", 256, 256, launch_trans4)
 
 #define TNS_DECL(ID, NAME, BMv, BNv, KIND) \
   hipError_t launch_shape_##ID(const GemmArgs&, bool, bool, bool, bool, hipStream_t);
@@ -529,5 +627,9 @@ hipError_t launch_conv_128x64(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_64x128(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_32x256(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_64x64(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x64m16(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_32x32m16(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x32m16(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_32x64m16(const GemmArgs&, bool, hipStream_t);
 
 }  // namespace tns

@@ -60,7 +60,7 @@ struct tns_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // serialises host-API use of one context
   // implicit-GEMM conv k-tables, one per (C, H, W, kH, kW, dY, dX)
-  std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int4*> ktabs;
+  std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int*> ktabs;
 };
 
 namespace {
@@ -174,7 +174,7 @@ int check_geom(const ConvGeom& g) {
 // once per geometry on the context's stream (stream order makes it visible to
 // the GEMM that follows)
 int get_ktab(tns_ctx* c, int64_t C, int64_t Hp, int64_t Wp, int64_t kH, int64_t kW, int64_t dY,
-             int64_t dX, const int4** out) {
+             int64_t dX, const int** out) {
   auto key = std::make_tuple(C, Hp, Wp, kH, kW, dY, dX);
   auto it = c->ktabs.find(key);
   if (it != c->ktabs.end()) {
@@ -182,8 +182,8 @@ int get_ktab(tns_ctx* c, int64_t C, int64_t Hp, int64_t Wp, int64_t kH, int64_t 
     return TNS_OK;
   }
   const int64_t K = C * kH * kW;
-  int4* t = nullptr;
-  hipError_t e = hipMalloc(&t, (size_t)(K + KTAB_PAD) * sizeof(int4));
+  int* t = nullptr;
+  hipError_t e = hipMalloc(&t, (size_t)(K + KTAB_PAD) * 2 * sizeof(int));
   if (e != hipSuccess)
     return set_error(TNS_ERR_NOMEM, "hipMalloc(k-table) failed: %s", hipGetErrorString(e));
   e = launch_build_ktab(t, (int)C, (int)Hp, (int)Wp, (int)kH, (int)kW, (int)dY, (int)dX,
@@ -704,14 +704,13 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
   const int64_t outImg = oh * ow, ks = kSize * kSize, k = C * ks;
   if (oh <= 0 || ow <= 0 || batch <= 0) return TNS_OK;
   const bool needs_col = ks != 1 || dilation != 1 || stride != 1;
-  // TNS_CONV_FUSED: implicit GEMM whenever a col matrix would be needed, and
-  // for 1x1 convolutions with small images (batch folded into N fills the
-  // tiles that a per-image GEMM with N = outH*outW < 1024 leaves ragged)
+  // TNS_CONV_FUSED: implicit GEMM (batch folded into N: one launch with the
+  // tile shapes of pick_conv_variant, measured at or ahead of the per-image
+  // GEMM on every YOLOv3 layer, 1x1 ones included)
   // (a padded 1x1/s1 convolution is left to the reference's direct path,
   // which ignores the padding — ntensors.pas:8286)
   const bool direct_ok = needs_col || padding == 0;
-  const bool implicit = direct_ok && (fused == TNS_CONV_IMPLICIT ||
-                                      (fused == TNS_CONV_FUSED && (needs_col || outImg < 1024)));
+  const bool implicit = direct_ok && (fused == TNS_CONV_IMPLICIT || fused == TNS_CONV_FUSED);
   if (implicit) {
     // implicit GEMM: batch folded into N, B gathered from zero-padded images
     if (!input || !weights || !out || !biases)
@@ -725,9 +724,11 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
                         (g_conv_pad < 0 ? 8.0 * (double)(batch * C * Hpad * Wpad) * 400.0 < flops
                                         : g_conv_pad == 1);
     const int64_t Hs = padded ? Hpad : H, Ws = padded ? Wpad : W, img = C * Hs * Ws;
-    if (k > 0x7fffffffLL - KTAB_PAD || img * 4 > 0x7fffffffLL)
+    // (k-table: 8-byte entries in one buffer resource, window offsets packed
+    // in 16 bits)
+    if (k > 0x0fffffffLL - KTAB_PAD || img * 4 > 0x7fffffffLL || (kSize - 1) * dilation >= 0x8000)
       return set_error(TNS_ERR_ARG, "conv_forward: image too large for the implicit GEMM");
-    const int4* kt = nullptr;
+    const int* kt = nullptr;
     if (int r = get_ktab(c, C, Hs, Ws, kSize, kSize, dilation, dilation, &kt)) return r;
     const float* src = input;
     if (padded && padding > 0) {
@@ -752,7 +753,7 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
       a.B = src + b0 * img; a.ldb = outImg; a.strideB = img;
       a.C = out + b0 * outImg * filters; a.ldc = outImg; a.strideC = outImg * filters;
       a.batch = 1; a.epi = EPI_BIAS_ACT; a.bias = biases; a.act = activation;
-      a.conv = padded ? 1 : 2; a.ktab = kt;
+      a.conv = padded ? 1 : 2; a.ktab = kt; a.ktab_n = (int)(k + KTAB_PAD);
       a.conv_H = (int)Hs; a.conv_W = (int)Ws; a.conv_ow = (int)ow; a.conv_ohw = (int)outImg;
       a.conv_sY = (int)stride; a.conv_sX = (int)stride;
       a.conv_pH = padded ? 0 : (int)padding; a.conv_pW = a.conv_pH;

@@ -55,11 +55,15 @@ struct GemmArgs {
   // C of image i starts at C + i*strideC.
   //   conv == 1: the images are zero-padded copies (conv_pH = conv_pW = 0);
   //   conv == 2: unpadded images, window bounds checked (pads conv_pH/pW).
-  // ktab[k] = {4*(c*H*W + kr*dY*W + kc*dX), kr*dY, kc*dX, 0} for the stored
-  // image size and k = (c*kH + kr)*kW + kc; entries k >= K are sentinels
-  // {0x80000000, 2^30, 2^30, 0} (out of range: the buffer load returns 0).
+  // k-table, two int arrays of ktab_n = K + KTAB_PAD entries for the stored
+  // image size and k = (c*kH + kr)*kW + kc:
+  //   ktab[k]          = 4*(c*H*W + kr*dY*W + kc*dX)   (byte offset)
+  //   ktab[ktab_n + k] = kr*dY | (kc*dX) << 16          (window offsets)
+  // entries k >= K are sentinels {0x80000000, 0x4000 | 0x4000 << 16} (out of
+  // range: the buffer load returns 0).
   int conv;
-  const int4* ktab;
+  const int* ktab;
+  int ktab_n;
   int conv_H, conv_W, conv_ow, conv_ohw, conv_sY, conv_sX, conv_pH, conv_pW;
   int conv_bytes;
 };
@@ -71,7 +75,7 @@ hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t
 // k-table of an implicit-GEMM convolution over stored Hs x Ws images (padded
 // or not): K = C*kH*kW entries plus KTAB_PAD sentinels
 constexpr int KTAB_PAD = 256;
-hipError_t launch_build_ktab(int4* ktab, int C, int Hs, int Ws, int kH, int kW, int dY, int dX,
+hipError_t launch_build_ktab(int* ktab, int C, int Hs, int Ws, int kH, int kW, int dY, int dX,
                              hipStream_t s);
 // zero-padded copy of a batch of images: [batch][C][H+2pH][W+2pW]
 hipError_t launch_pad_images(const float* im, int64_t batch, int64_t C, int64_t H, int64_t W,
