@@ -19,7 +19,7 @@ sys.path.insert(0, str(ROOT))
 from tensorium_amd.nnhip import TNNHip  # noqa: E402
 from tensorium_amd.yolo import yolov3_conv_table  # noqa: E402
 
-IMPLICIT_VARIANTS = [2, 6, 12, 13, 14, 15]
+IMPLICIT_VARIANTS = [int(v) for v in __import__('os').environ.get('CONV_VARIANTS', '6,12,13,14,15,18,19,20,21,22').split(',')]
 
 
 def time_conv(hip, layer, mode, variant, reps, pad=-1):

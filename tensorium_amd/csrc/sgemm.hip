@@ -22,7 +22,8 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 enum {
   V_128x128 = 0, V_128x64 = 1, V_64x128 = 2, V_64x256 = 3, V_32x256 = 4, V_256x256w8 = 5,
   V_64x64 = 6, V_64x64m16 = 12, V_32x32m16 = 13, V_64x32m16 = 14, V_32x64m16 = 15,
-  V_128x128m16 = 16, V_256x256w8m16 = 17
+  V_128x128m16 = 16, V_256x256w8m16 = 17, V_128x64w8 = 18, V_64x128w8 = 19, V_128x128w8 = 20,
+  V_64x64d1 = 21, V_64x64w8m16 = 22
 };
 
 // float4 staging needs 16-B aligned rows and a contiguous extent that is a
@@ -48,15 +49,18 @@ int pick_variant(const GemmArgs& a, bool av, bool bv) {
 
 // Implicit-GEMM conv tile choice.  No split-K (bit-exactness), so the
 // parallelism is the output tiles alone.  From the YOLOv3 sweep (scripts/
-// conv_sweep.py): the 64x64 32x32-MFMA tile wherever it already
-// yields >= 600 blocks; below that the 16x16-MFMA tiles, whose four times as
-// many accumulator chains per output area keep 256 CUs busy — 64x32 for deep
-// K (the 1024-filter 3x3 layers), 32x32 for the fewest blocks, else 32x64.
+// conv_sweep.py; b64 = blocks a 64x64 tile would give):
+//   b64 >= 1200, filters % 128 == 0  128x64, 8 waves of 32x32
+//   b64 >= 600 (or 64 filters)       64x64, 8 waves of 32x16 (16x16 MFMA)
+//   fewer blocks: 16x16-MFMA tiles, whose four times as many accumulator
+//   chains per output area keep 256 CUs busy — 64x32 for deep K (the
+//   1024-filter 3x3 layers), 32x32 for the fewest blocks, else 32x64.
 int pick_conv_variant(const GemmArgs& a) {
   const int64_t M = a.M, N = a.N, K = a.K;
-  if (M <= 32) return V_32x64m16;
+  if (M <= 32) return V_32x32m16;
   const int64_t b64 = ((M + 63) / 64) * ((N + 63) / 64);
-  if (b64 >= 600) return V_64x64;
+  if (b64 >= 1200 && M % 128 == 0) return V_128x64w8;
+  if (b64 >= 600) return V_64x64w8m16;
   if (K >= 2048) return V_64x32m16;
   if (b64 <= 200) return V_32x32m16;
   return V_32x64m16;
@@ -78,6 +82,11 @@ hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t
     case V_32x32m16: return launch_conv_32x32m16(a, av, s);
     case V_64x32m16: return launch_conv_64x32m16(a, av, s);
     case V_32x64m16: return launch_conv_32x64m16(a, av, s);
+    case V_128x64w8: return launch_conv_128x64w8(a, av, s);
+    case V_64x128w8: return launch_conv_64x128w8(a, av, s);
+    case V_128x128w8: return launch_conv_128x128w8(a, av, s);
+    case V_64x64d1: return launch_conv_64x64d1(a, av, s);
+    case V_64x64w8m16: return launch_conv_64x64w8m16(a, av, s);
     default: return hipErrorInvalidValue;  // no implicit-conv instantiation
   }
 }

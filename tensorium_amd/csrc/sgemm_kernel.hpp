@@ -18,7 +18,7 @@
 //
 // Structure (one template, several tile shapes picked per problem):
 //   block tile BM x BN, k-tile BK, WM x WN waves, each wave owning
-//   (BM/WM) x (BN/WN) as a grid of 32x32 MFMA accumulators.  Operands are
+//   (BM/WM) x (BN/WN) as a grid of 32x32 (or 16x16) MFMA accumulators.  Operands are
 //   staged global -> registers (float4 where the layout allows) -> LDS in
 //   k-major [k][m] / [k][n] images, double-buffered with one barrier per
 //   k-tile; the next tile's global loads are issued before the current
@@ -131,8 +131,8 @@ struct TileIO {
 // matrix, k = (c, kr, kc), n = (image, orow, ocol), read straight from the
 // images.  Each thread owns one column n for the whole launch (NT % BN == 0);
 // the BN threads of a row group walk E consecutive k, so a wave's k-table
-// entries are one contiguous, wave-uniform run (scalar loads, fetched one
-// k-tile ahead).  Loads are buffer loads whose out-of-range offsets return 0:
+// entries are one contiguous run (vector dwordx4 loads, fetched one k-tile
+// ahead).  Image loads are buffer loads whose out-of-range offsets return 0:
 //   PADDED   the images were copied with their zero border materialised, and
 //            the k >= K sentinel is out of range: one add per element;
 //   checked  the window row/column are bounds-checked against H x W and a
@@ -591,6 +591,12 @@ using S64x32m16 = Shape<64, 32, 32, 2, 2, 2, 2, 16>;
 using S32x64m16 = Shape<32, 64, 32, 2, 2, 2, 2, 16>;
 using S128x128m16 = Shape<128, 128, 32, 2, 2, 2, 1, 16>;
 using S256x256w8m16 = Shape<256, 256, 32, 2, 4, 2, 1, 16>;
+// conv tile experiments: 8-wave blocks, prefetch depth 1
+using S128x64w8 = Shape<128, 64, 32, 4, 2, 2, 2>;
+using S64x128w8 = Shape<64, 128, 32, 2, 4, 2, 2>;
+using S128x128w8 = Shape<128, 128, 32, 4, 2, 2, 1>;
+using S64x64d1 = Shape<64, 64, 32, 2, 2, 2, 1>;
+using S64x64w8m16 = Shape<64, 64, 32, 2, 4, 2, 2, 16>;
 
 
 }  // namespace sgemm_detail
@@ -615,7 +621,12 @@ typedef hipError_t (*ShapeLauncher)(const GemmArgs&, bool, bool, bool, bool, hip
   X(64x32m16, "64x32x32_w2x2_m16", 64, 32, launch_nn4)   \
   X(32x64m16, "32x64x32_w2x2_m16", 32, 64, launch_nn4)   \
   X(128x128m16, "128x128x32_w2x2_m16", 128, 128, launch_nn4) \
-  X(256x256w8m16, "256x256x32_w2x4_m16", 256, 256, launch_trans4)
+  X(256x256w8m16, "256x256x32_w2x4_m16", 256, 256, launch_trans4) \
+  X(128x64w8, "128x64x32_w4x2", 128, 64, launch_nn4)     \
+  X(64x128w8, "64x128x32_w2x4", 64, 128, launch_nn4)     \
+  X(128x128w8, "128x128x32_w4x2", 128, 128, launch_nn4)  \
+  X(64x64d1, "64x64x32_w2x2_d1", 64, 64, launch_nn4)     \
+  X(64x64w8m16, "64x64x32_w2x4_m16", 64, 64, launch_nn4)
 
 #define TNS_DECL(ID, NAME, BMv, BNv, KIND) \
   hipError_t launch_shape_##ID(const GemmArgs&, bool, bool, bool, bool, hipStream_t);
@@ -631,5 +642,10 @@ hipError_t launch_conv_64x64m16(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_32x32m16(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_64x32m16(const GemmArgs&, bool, hipStream_t);
 hipError_t launch_conv_32x64m16(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_128x64w8(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x128w8(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_128x128w8(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x64d1(const GemmArgs&, bool, hipStream_t);
+hipError_t launch_conv_64x64w8m16(const GemmArgs&, bool, hipStream_t);
 
 }  // namespace tns

@@ -74,11 +74,12 @@ IMPLICIT_CASES = [
     (1, 64, 52, 128, 3, 1, 1, 9), (1, 32, 53, 256, 3, 2, 1, 9)]
 
 
-CONV_VARIANTS = (1, 2, 4, 6, 12, 13, 14, 15)  # tile shapes with an implicit-conv instantiation
+CONV_VARIANTS = (1, 2, 4, 6, 12, 13, 14, 15, 18, 19, 20, 21, 22)  # with implicit-conv instances
 
 
 @pytest.mark.parametrize("pad", [0, 1])
-@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6, 12, 13, 14, 15, 16])
+@pytest.mark.parametrize("variant", [-1, 0, 1, 2, 3, 4, 5, 6, 12, 13, 14, 15, 16, 18, 19, 20, 21,
+                                     22])
 def test_conv_implicit_variants_bit_exact(hip, torch_cuda, ora, variant, pad):
     """Every tile shape with an implicit-conv instantiation (others report
     UNSUPPORTED), both gather forms (padded copy / bounds-checked)."""
