@@ -24,6 +24,27 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 constexpr int NT = 1024;
 constexpr int NWAVES = NT / 64;
+constexpr int KC = 128;  // largest k-chunk of the LDS-staged forward gemm
+
+// Diagnostic build only (-DTNS_MLP_STAMPS, scripts/mlp_stamps.py): thread 0
+// records s_memtime at stage boundaries into 64 uint32 pairs after the packed
+// buffer (the caller allocates them).  Compiled out of the product.
+#ifdef TNS_MLP_STAMPS
+#define MLP_STAMP(i)                                                              \
+  do {                                                                            \
+    __syncthreads();                                                              \
+    if (threadIdx.x == 0) {                                                       \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                 \
+      unsigned* st_ = reinterpret_cast<unsigned*>(a.buf + a.stamp_off) + 2 * (i); \
+      st_[0] = (unsigned)t_;                                                      \
+      st_[1] = (unsigned)(t_ >> 32);                                              \
+    }                                                                             \
+  } while (0)
+#else
+#define MLP_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
 __device__ constexpr float SEPS = 0.000001f;
 
 // Per-layer views into the packed buffer.  The element offsets are computed
@@ -67,12 +88,11 @@ template <int U = 8>
 __device__ __forceinline__ void mfma_chain(floatx16& acc, int steps, const float* pa, int64_t sa,
                                            bool va, const float* pb, int64_t sb, bool vb,
                                            int64_t k0, int64_t kstep, int64_t K) {
-  int s = 0;
-  for (; s + U <= steps; s += U) {
+  for (int s = 0; s < steps; s += U) {
     float av[U], bv[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool ok = k0 + (int64_t)(s + u) * kstep < K;
+    for (int u = 0; u < U; ++u) {  // the last batch may be partial: loads stay together
+      const bool ok = (s + u < steps) && k0 + (int64_t)(s + u) * kstep < K;
       const int64_t ia = ok ? (int64_t)(s + u) * sa : 0, ib = ok ? (int64_t)(s + u) * sb : 0;
       const float x = pa[ia], y = pb[ib];
       av[u] = (ok && va) ? x : 0.0f;
@@ -80,13 +100,7 @@ __device__ __forceinline__ void mfma_chain(floatx16& acc, int steps, const float
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
-  }
-  for (; s < steps; ++s) {
-    const bool ok = k0 + (int64_t)s * kstep < K;
-    const float x = pa[ok ? (int64_t)s * sa : 0], y = pb[ok ? (int64_t)s * sb : 0];
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32((ok && va) ? x : 0.0f, (ok && vb) ? y : 0.0f,
-                                               acc, 0, 0, 0);
+      if (s + u < steps) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
   }
 }
 
@@ -107,8 +121,61 @@ __device__ __forceinline__ float vssum8(const float* a, int64_t n) {
   return r;
 }
 
+// Forward gemm of one layer, out[B][O] partials per residue class r = k mod 8
+// into lds[(r*B + m)*O + n], with wave w = (tile, r) and both operands staged
+// through LDS in k-chunks of KCH by coalesced loads; each chain continues
+// across chunks in ascending k (bit-identical to the direct chain).  The
+// chunks alias the partial-sum region: every wave has passed the barrier
+// after the last chunk before any partial is written.
+template <int KCH>
+__device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const float* W, int64_t B,
+                                             int64_t O, int64_t I, int tm, int tn) {
+  constexpr int KP = KCH + 1;  // LDS row: an odd stride for the lanes' row reads
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  float* Xs = lds;
+  float* Ws = Xs + tm * 32 * KP;
+  const int rowsX = tm * 32, rows = (tm + tn) * 32;
+  const bool active = wid < tm * tn * 8;
+  const int r = wid & 7, tile = wid >> 3;
+  const int m0 = (tile / tn) * 32, n0 = (tile % tn) * 32;
+  const int l31 = lane & 31, h = lane >> 5;
+  floatx16 acc;
+  for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+  for (int64_t kc0 = 0; kc0 < I; kc0 += KCH) {
+#pragma unroll 4
+    for (int i = tid; i < rows * KCH; i += NT) {
+      const int row = i / KCH, kk = i % KCH;
+      const int64_t k = kc0 + kk;
+      const bool isx = row < rowsX;
+      const int64_t rr = isx ? row : row - rowsX;
+      const bool ok = k < I && rr < (isx ? B : O);
+      const float* src = isx ? in : W;
+      const float v = src[ok ? rr * I + k : 0];
+      lds[row * KP + kk] = ok ? v : 0.0f;
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int st = 0; st < KCH / 16; ++st) {  // k = kc0 + r + 8*(2*st + h)
+        const int kk = r + 8 * (2 * st + h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Xs[(m0 + l31) * KP + kk],
+                                                   Ws[(n0 + l31) * KP + kk], acc, 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  if (active)
+    for (int e = 0; e < 16; ++e) {
+      const int64_t m = m0 + acc_row(e), n = n0 + l31;
+      if (m < B && n < O) lds[(r * B + m) * O + n] = acc[e];
+    }
+}
+
 __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
-  extern __shared__ float lds[];  // 8 * B * O_max partial sums of the forward gemm
+  // 8 * B * O_max floats: partial sums of the forward gemm; between gemms,
+  // up to three [B][O] blocks staged for the per-channel (column) passes, so
+  // their sequential sums read LDS instead of waiting on memory per row
+  extern __shared__ float lds[];
   const int tid = threadIdx.x;
   const int wid = tid >> 6;
   const int lane = tid & 63;
@@ -121,6 +188,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   float* sm_loss = smx + 2 * B * C;
 
   // ---- forward ------------------------------------------------------------
+  MLP_STAMP(0);
   const float* in = a.X;
   for (int l = 0; l < L; ++l) {
     const Layer lay(a, l);
@@ -132,6 +200,15 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     const int tm = (int)((B + 31) / 32), tn = (int)((O + 31) / 32);
     const int64_t kr = (I + 7) / 8;            // k values per residue class
     const int steps = (int)((kr + 1) / 2);
+    if (tm * tn * 8 <= NWAVES && a.lds_chunks) {
+      // One (tile, residue) task per wave; both operands are k-contiguous
+      // rows (an MFMA lane per row), so they are staged through LDS in
+      // k-chunks by coalesced loads (gemm_chunked)
+      if (I > 64)
+        gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn);
+      else
+        gemm_chunked<64>(lds, in, lay.W(), B, O, I, tm, tn);
+    } else
     for (int w = wid; w < tm * tn * 8; w += NWAVES) {
       const int r = w & 7, tile = w >> 3;
       const int64_t m0 = (int64_t)(tile / tn) * 32, n0 = (int64_t)(tile % tn) * 32;
@@ -156,20 +233,23 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       const float s0 = p[0] + p[4], s1 = p[1] + p[5], s2 = p[2] + p[6], s3 = p[3] + p[7];
       const float dot = (s0 + s1) + (s2 + s3);
       const float c0 = 0.0f * lay.out()[e];  // beta = 0 => 0*C (mulvs)
-      lay.out()[e] = c0 + 1.0f * dot;        // C := C + ALPHA*sdot
+      const float y = c0 + 1.0f * dot;       // C := C + ALPHA*sdot
+      lay.out()[e] = y;
+      lds[e] = y;  // (this thread's own partial slot, already read)
     }
     __syncthreads();
     if (a.bn) {
       // per channel: MeansAndVars, rolling stats, x, normalize, x_norm, scale
+      const float* col = lds;  // the layer output, [B][O]
       for (int64_t o = tid; o < O; o += NT) {
         float m = 0.0f;
 #pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) m = m + lay.out()[b * O + o];
+        for (int64_t b = 0; b < B; ++b) m = m + col[b * O + o];
         m = m / (float)B;
         float v = 0.0f;
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float t = lay.out()[b * O + o] - m;
+          const float t = col[b * O + o] - m;
           v = v + t * t;
         }
         v = v / (float)(B - 1);
@@ -179,13 +259,14 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         lay.rmean()[o] = fmaf(mom, m, lay.rmean()[o] * (1.0f - mom));
         lay.rvar()[o] = fmaf(mom, v, lay.rvar()[o] * (1.0f - mom));
         const float sd = sqrtf(v > SEPS ? v : SEPS);
+        const float sc = lay.scales()[o];
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float xv = lay.out()[b * O + o];
+          const float xv = col[b * O + o];
           lay.x()[b * O + o] = xv;
           const float xn = (xv - m) / sd;
           lay.xnorm()[b * O + o] = xn;
-          lay.out()[b * O + o] = xn * lay.scales()[o];
+          lay.out()[b * O + o] = xn * sc;
         }
       }
       __syncthreads();
@@ -196,6 +277,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     }
     __syncthreads();
     in = lay.out();
+    MLP_STAMP(1 + l);
   }
 
   // ---- softmax + cross-entropy (groups 1, temperature 1) ----------------------
@@ -221,6 +303,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   }
   __syncthreads();
   if (tid == 0) *a.cost = vssum8(sm_loss, B * C);
+  MLP_STAMP(20);
 
   // ---- backward ---------------------------------------------------------------
   for (int l = L - 1; l >= 0; --l) {
@@ -233,33 +316,43 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       lin = prev.out();
       prev_delta = prev.delta();  // state.delta = nil for layer 0 (nnet.pas:332-335)
     }
-    // softmax backward: prev.delta() += delta; then clamp + activation gradient
+    // softmax backward: prev.delta() += delta; then clamp + activation gradient.
+    // Stage delta (and x, x_norm for batch norm) in LDS for the column passes.
+    float* sdel = lds;
+    float* sx = lds + BO;
+    float* sxn = lds + 2 * BO;
     for (int64_t e = tid; e < BO; e += NT) {
       float d = lay.delta()[e];
       if (l == L - 1) d = d + sm_delta[e];
       d = d < -1.0f ? -1.0f : (d > 1.0f ? 1.0f : d);  // delta.Clamp(-1, 1)
-      lay.delta()[e] = d * grad_apply(lay.out()[e], lay.act);
+      d = d * grad_apply(lay.out()[e], lay.act);
+      lay.delta()[e] = d;
+      sdel[e] = d;
+      if (a.bn) {
+        sx[e] = lay.x()[e];
+        sxn[e] = lay.xnorm()[e];
+      }
     }
     __syncthreads();
     // per channel: bias_updates.addSums, then the BN backward chain
     for (int64_t o = tid; o < O; o += NT) {
       float r = 0.0f;
 #pragma unroll 8
-      for (int64_t b = 0; b < B; ++b) r = r + lay.delta()[b * O + o];
+      for (int64_t b = 0; b < B; ++b) r = r + sdel[b * O + o];
       lay.db()[o] = lay.db()[o] + r;
       if (a.bn) {
         float dd = 0.0f;  // addDots (strided sdot: mul then add)
 #pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) dd = dd + lay.xnorm()[b * O + o] * lay.delta()[b * O + o];
+        for (int64_t b = 0; b < B; ++b) dd = dd + sxn[b * O + o] * sdel[b * O + o];
         lay.dscales()[o] = lay.dscales()[o] + dd;
         const float sc = lay.scales()[o], mu = lay.mean()[o];
         float m = 0.0f, v = 0.0f;
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float d = lay.delta()[b * O + o] * sc;  // forwardScale
-          lay.delta()[b * O + o] = d;
+          const float d = sdel[b * O + o] * sc;  // forwardScale
+          sdel[b * O + o] = d;                   // (own column only)
           m = m + d;
-          v = v + (lay.x()[b * O + o] - mu) * d;
+          v = v + (sx[b * O + o] - mu) * d;
         }
         const float ve = lay.var()[o] > SEPS ? lay.var()[o] : SEPS;
         const float md = m * (-1.0f / sqrtf(ve));
@@ -269,8 +362,8 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         const float mdb = md / (float)B, vdb = 2.0f * vd / (float)B, sd = sqrtf(ve);
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
-          const float q = lay.delta()[b * O + o] / sd;
-          const float t = (lay.x()[b * O + o] - mu) * vdb + mdb;
+          const float q = sdel[b * O + o] / sd;
+          const float t = (sx[b * O + o] - mu) * vdb + mdb;
           lay.delta()[b * O + o] = q + t;
         }
       }
@@ -308,6 +401,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       }
     }
     __syncthreads();
+    MLP_STAMP(21 + l);
   }
 
   // ---- update (TConnectedLayer.update, constant learning rate) ----------------
@@ -324,12 +418,30 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         lay.dscales()[o] = a.momentum * lay.dscales()[o];
       }
     }
-    for (int64_t e = tid; e < IO; e += NT) {
-      float dw = fmaf(wdec, lay.W()[e], lay.dW()[e]);  // weight_updates.axpy(-decay*batch, W)
-      const float w = fmaf(lrb, dw, lay.W()[e]);     // weights.axpy(lr/batch, dW)
-      lay.W()[e] = w;
-      lay.dW()[e] = a.momentum * dw;                  // weight_updates.Multiply(momentum)
+    // UB elements per thread per round, their loads issued together (W and dW
+    // live in one buffer: the compiler cannot move a load past a store)
+    constexpr int UB = 8;
+    float* W = lay.W();
+    float* dW = lay.dW();
+    for (int64_t e0 = tid; e0 < IO; e0 += (int64_t)NT * UB) {
+      float w[UB], g[UB];
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int64_t e = e0 + (int64_t)u * NT;
+        w[u] = W[e < IO ? e : e0];
+        g[u] = dW[e < IO ? e : e0];
+      }
+#pragma unroll
+      for (int u = 0; u < UB; ++u) {
+        const int64_t e = e0 + (int64_t)u * NT;
+        if (e < IO) {
+          const float dw = fmaf(wdec, w[u], g[u]);  // weight_updates.axpy(-decay*batch, W)
+          W[e] = fmaf(lrb, dw, w[u]);               // weights.axpy(lr/batch, dW)
+          dW[e] = a.momentum * dw;                  // weight_updates.Multiply(momentum)
+        }
+      }
     }
+    MLP_STAMP(40 + l);
   }
 }
 
@@ -376,10 +488,24 @@ hipError_t launch_mlp_train_step(const MlpArgs& args, hipStream_t s) {
     }
   }
   a.softmax_off = p;
+  a.stamp_off = p + 3 * B * a.widths[a.nlayers];
   int64_t omax = 0;
   for (int l = 0; l < a.nlayers; ++l) omax = a.widths[l + 1] > omax ? a.widths[l + 1] : omax;
-  const size_t lds = (size_t)(8 * a.batch * omax) * sizeof(float);
+  // partial sums (>= 3 [B][O] blocks); the forward gemm's k-chunks of both
+  // operands reuse the same space when one (tile, residue) task per wave
+  // covers every layer
+  const int64_t tmx = (a.batch + 31) / 32, tnx = (omax + 31) / 32;
+  size_t lds = (size_t)(8 * a.batch * omax) * sizeof(float);
+  const size_t lds_chunks = (size_t)((tmx + tnx) * 32 * (KC + 1)) * sizeof(float);
+  a.lds_chunks = tmx * tnx * 8 <= NWAVES && lds_chunks <= 160 * 1024;
+  if (a.lds_chunks && lds_chunks > lds) lds = lds_chunks;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(mlp_train_kernel, dim3(1), dim3(NT), lds, s, a);
   return hipGetLastError();
 }
