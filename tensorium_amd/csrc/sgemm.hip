@@ -19,6 +19,8 @@ const VariantInfo kVariants[] = {TNS_SHAPES(TNS_ROW)};
 #undef TNS_ROW
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
+unsigned* g_stamps = nullptr;  // block timeline buffer (diagnostic builds only)
+
 enum {
   V_128x128 = 0, V_128x64 = 1, V_64x128 = 2, V_64x256 = 3, V_32x256 = 4, V_256x256w8 = 5,
   V_64x64 = 6, V_64x64m16 = 12, V_32x32m16 = 13, V_64x32m16 = 14, V_32x64m16 = 15,
@@ -68,7 +70,9 @@ int pick_conv_variant(const GemmArgs& a) {
 
 }  // namespace
 
-hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s) {
+hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a_in, hipStream_t s) {
+  GemmArgs a = a_in;
+  a.stamps = g_stamps;
   if (a.M <= 0 || a.N <= 0 || a.batch <= 0) return hipSuccess;
   if (!a.conv || !a.ktab) return hipErrorInvalidValue;
   const bool av = vec4_ok(a.A, a.lda, a.strideA, a.batch, a.K);
@@ -98,8 +102,10 @@ hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s) {
 int sgemm_variant_count() { return kNumVariants; }
 const char* sgemm_variant_name(int v) { return (v >= 0 && v < kNumVariants) ? kVariants[v].name : ""; }
 
-hipError_t launch_sgemm_variant(int variant, const GemmArgs& a, bool transA, bool transB,
+hipError_t launch_sgemm_variant(int variant, const GemmArgs& a_in, bool transA, bool transB,
                                 hipStream_t s) {
+  GemmArgs a = a_in;
+  a.stamps = g_stamps;
   if (a.M <= 0 || a.N <= 0 || a.batch <= 0) return hipSuccess;
   // A is k-contiguous unless transposed; B is n-contiguous unless transposed
   const bool av = vec4_ok(a.A, a.lda, a.strideA, a.batch, transA ? a.M : a.K);
@@ -112,5 +118,15 @@ hipError_t launch_sgemm_variant(int variant, const GemmArgs& a, bool transA, boo
 hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s) {
   return launch_sgemm_variant(-1, a, transA, transB, s);
 }
+
+#ifdef TNS_GEMM_STAMPS
+// diagnostic build only (not in include/tns.h): every following launch
+// records {start, end, HW_ID, XCC_ID} per block into dev_buf (8 words per
+// block), or nothing when dev_buf is NULL
+extern "C" int tns_debug_gemm_stamps(unsigned* dev_buf) {
+  g_stamps = dev_buf;
+  return 0;
+}
+#endif
 
 }  // namespace tns

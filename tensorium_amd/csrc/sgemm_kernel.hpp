@@ -272,36 +272,13 @@ struct Acc<16> {
 // MFMA steps [S0, S1) of one k-tile: step s consumes k = KS*s + lane/MF
 // (lane half for 32x32x2, lane quarter for 16x16x4) — ascending k per
 // accumulator (the MFMA chains its k in lane-group order).
-// TNS_PREREAD: issue every fragment read of the half-tile before its first
-// MFMA (the waits then drain progressively instead of one full LDS latency
-// per step pair).
-#ifndef TNS_PREREAD
-#define TNS_PREREAD 0
-#endif
+// (Issuing all of a half-tile's fragment reads ahead of its MFMAs measured
+// slower on the YOLOv3 layers; the compiler's interleaving is kept.)
 template <int MF, int TM, int TN, int LDA_S, int LDB_S, int S0, int S1>
 __device__ __forceinline__ void mma_steps(typename Acc<MF>::type (&acc)[TM][TN], const float* ap,
                                           const float* bp) {
   constexpr int KS = 64 / MF;
-  // small wave tiles: all reads first (registers are plentiful there)
-  constexpr bool PRE = TNS_PREREAD && (TM + TN) * (S1 - S0) <= 24;
-  if constexpr (PRE) {
-    float a[S1 - S0][TM], b[S1 - S0][TN];
-#pragma unroll
-    for (int s = S0; s < S1; ++s) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) a[s - S0][i] = ap[KS * s * LDA_S + MF * i];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) b[s - S0][j] = bp[KS * s * LDB_S + MF * j];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = S0; s < S1; ++s)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = Acc<MF>::mma(a[s - S0][i], b[s - S0][j], acc[i][j]);
-  } else {
+  {
 #pragma unroll
     for (int s = S0; s < S1; ++s) {
       float a[TM], b[TN];
@@ -336,6 +313,10 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
   const int tid = threadIdx.x;
+#ifdef TNS_GEMM_STAMPS
+  // diagnostic build only: block start time and placement (scripts/gemm_timeline.py)
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
   const int lane = tid & 63;
   const int lc = lane % MF;  // accumulator column / operand row of this lane
   const int h = lane / MF;   // k within an MFMA step; 4h = first output row
@@ -487,6 +468,18 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
   }
 
   // ---- epilogue ----------------------------------------------------------
+#ifdef TNS_GEMM_STAMPS
+  if (tid == 0 && p.stamps != nullptr && blockIdx.x < (1u << 16) && blockIdx.y == 0) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memtime();
+    unsigned* st = p.stamps + 8 * blockIdx.x;
+    st[0] = (unsigned)t_start;
+    st[1] = (unsigned)(t_start >> 32);
+    st[2] = (unsigned)t_end;
+    st[3] = (unsigned)(t_end >> 32);
+    st[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    st[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
+#endif
   const bool fuse = p.epi == EPI_BIAS_ACT;
   const int act = p.act;
 #pragma unroll

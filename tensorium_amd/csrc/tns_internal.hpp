@@ -66,6 +66,8 @@ struct GemmArgs {
   int ktab_n;
   int conv_H, conv_W, conv_ow, conv_ohw, conv_sY, conv_sX, conv_pH, conv_pW;
   int conv_bytes;
+  // diagnostic builds (-DTNS_GEMM_STAMPS) only: per-block timeline records
+  unsigned* stamps;
 };
 
 hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s);
