@@ -237,9 +237,45 @@ def cpu_baseline(n, target_s):
     else:
         rows_t, secs = rows, dt
     gflops = 2.0 * rows_t * n * n / secs / 1e9
-    return {"value": round(gflops, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
-            "sample": f"{rows_t} of {n} rows of the {n}^3 NN product "
-                      f"(restated sgemm_nn/saxpy_avx2 FMA chain, {secs:.1f} s)"}
+    out = {"value": round(gflops, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
+           "sample": f"{rows_t} of {n} rows of the {n}^3 NN product "
+                     f"(restated sgemm_nn/saxpy_avx2 FMA chain, {secs:.1f} s)"}
+    out.update(cpu_yolo_mnist())
+    return out
+
+
+def cpu_yolo_mnist():
+    """The oracle's restated conv-layer forward (im2col + sgemm_nn + bias +
+    activation, same thread count) over all 75 YOLOv3 conv layers for one
+    image, and the restated MNIST train step."""
+    from oracle import oracle as ora
+    from tensorium_amd.yolo import yolov3_conv_table
+    table = yolov3_conv_table()
+    flop_img = sum(s.flops for s in table)
+    t_flop, t_sec = 0.0, 0.0
+    for idx, s in enumerate(table):
+        x = ora.uniform(s.c * s.h * s.h, 3, idx, 0.0, 1.0).reshape(1, s.c, s.h, s.h)
+        sc = float(np.sqrt(2.0 / (s.size * s.size * s.c)))
+        w = ora.uniform(s.filters * s.K, 4, idx, -sc, sc)
+        b = ora.uniform(s.filters, 5, idx, -0.1, 0.1)
+        t0 = time.perf_counter()
+        ora.conv_forward(x, w, b, s.filters, s.size, s.stride, s.pad, s.activation)
+        t_sec += time.perf_counter() - t0
+        t_flop += s.flops
+    widths, acts, B = [784, 64, 64, 64, 64, 32, 10], [1, 1, 1, 1, 1, 4], 32
+    buf = ora.mlp_init(widths, 1, B)
+    X, T = ora.mnist_batch(B)
+    ora.mlp_train_step(widths, acts, 1, B, X, T, 1e-3, 0.9, 1e-4, buf)
+    steps, t0 = 0, time.perf_counter()
+    while steps < 50 and time.perf_counter() - t0 < 2.0:
+        ora.mlp_train_step(widths, acts, 1, B, X, T, 1e-3, 0.9, 1e-4, buf)
+        steps += 1
+    mnist_s = (time.perf_counter() - t0) / steps
+    return {"yolo_images_per_s": round(t_flop / t_sec / flop_img, 4),
+            "yolo_sample": f"one image through all 75 conv layers ({t_flop / 1e9:.2f} GFLOP "
+                           f"in {t_sec:.2f} s)",
+            "mnist_steps_per_s": round(1.0 / mnist_s, 2),
+            "mnist_sample": f"{steps} restated train steps (batch 32, BN)"}
 
 
 def traffic_from_profiles(n):

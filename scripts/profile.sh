@@ -9,7 +9,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--steps 10 --warmup 3 --no-cpu ${EXTRA:-}"
+ARGS="${PROF_ARGS:---no-cpu}"
 run() { local name=$1; shift; timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 $R/bench.py $ARGS > $OUT/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; return $rc; }
 run trace --kernel-trace --stats || exit $?
 [ "${PMC:-1}" = "1" ] || exit 0

@@ -23,9 +23,10 @@ _warned = set()
 
 def time_variant(hip, v, prob, reps):
     M, N, K, batch, A, B, C = prob
+    sA = M * K if A.dim() == 3 else 0  # batched: own A per GEMM; yolo: shared weights
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     try:
-        hip.gemmVariant(v, False, False, M, N, K, 1.0, A, 0, K, 0 if batch > 1 else 0, B, 0, N,
+        hip.gemmVariant(v, False, False, M, N, K, 1.0, A, 0, K, sA, B, 0, N,
                         K * N, 0.0, C, 0, N, M * N, batch)
     except Exception as e:
         if v not in _warned:
@@ -35,7 +36,7 @@ def time_variant(hip, v, prob, reps):
     torch.cuda.synchronize()
     ev0.record()
     for _ in range(reps):
-        hip.gemmVariant(v, False, False, M, N, K, 1.0, A, 0, K, 0, B, 0, N, K * N, 0.0, C, 0, N,
+        hip.gemmVariant(v, False, False, M, N, K, 1.0, A, 0, K, sA, B, 0, N, K * N, 0.0, C, 0, N,
                         M * N, batch)
     ev1.record()
     torch.cuda.synchronize()
@@ -48,6 +49,7 @@ def main():
     ap.add_argument("--yolo", action="store_true")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="")
+    ap.add_argument("--batched", default="", help="n:batch strided-batched n^3 GEMMs")
     args = ap.parse_args()
     hip = TNNHip(0)
     names = TNNHip.gemmVariants()
@@ -58,6 +60,12 @@ def main():
         B = torch.rand(n, n, device="cuda") * 2 - 1
         C = torch.zeros(n, n, device="cuda")
         probs[f"sq{n}"] = (n, n, n, 1, A, B, C)
+    if args.batched:
+        n, nb = (int(v) for v in args.batched.split(":"))
+        A = torch.rand(nb, n, n, device="cuda") * 2 - 1
+        B = torch.rand(nb, n, n, device="cuda") * 2 - 1
+        C = torch.zeros(nb, n, n, device="cuda")
+        probs[f"batched{n}x{nb}"] = (n, n, n, nb, A, B, C)
     if args.yolo:
         seen = set()
         for s in yolov3_conv_table():
