@@ -299,7 +299,7 @@ def main():
     ctx = tdist.init("nccl")
     rank, world, local = ctx.rank, ctx.world, ctx.local
     from tensorium_amd.nnhip import TNNHip
-    hip = TNNHip(local)
+    hip = TNNHip(ctx.gpu)
     n = args.size
 
     wall, kern_ms, kern_min = bench_sgemm(torch, hip, ctx, rank, n, args.steps, args.warmup)

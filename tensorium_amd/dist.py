@@ -18,6 +18,7 @@ class DistCtx:
     world: int
     local: int
     device: str
+    gpu: int = 0  # HIP device of this rank
 
     def barrier(self):
         if self.dist is not None:
@@ -60,20 +61,24 @@ def init(backend: str | None = None) -> DistCtx:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    # TNS_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
+    # devices round-robin; RCCL needs one device per rank)
+    backend = os.environ.get("TNS_DIST_BACKEND") or backend
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     device = "cpu"
-    if backend == "nccl":
-        torch.cuda.set_device(local)
-        device = f"cuda:{local}"
-    elif torch.cuda.is_available():
-        torch.cuda.set_device(local)
+    gpu = 0
+    if torch.cuda.is_available():
+        gpu = local % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(gpu)
+        if backend == "nccl":
+            device = f"cuda:{gpu}"
     if world <= 1:
-        return DistCtx(None, 0, 1, local, device)
+        return DistCtx(None, 0, 1, local, device, gpu)
     import torch.distributed as dist
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     kw = {}
     if backend == "nccl":
-        kw["device_id"] = torch.device("cuda", local)
+        kw["device_id"] = torch.device("cuda", gpu)
     dist.init_process_group(backend, rank=rank, world_size=world, **kw)
-    return DistCtx(dist, rank, world, local, device)
+    return DistCtx(dist, rank, world, local, device, gpu)
