@@ -21,6 +21,8 @@ Extra fields on the single JSON line:
                  0 at N=1 only, on a bounded sample of rows of the same product.
   yolo         — YOLOv3-416 conv forward, batch 8 per GPU, 75 conv layers
                  (BASELINE configs[2]); images/s over all ranks.
+  yolo_network — the whole YOLOv3-416 network (convolutions chained through
+                 shortcut / route / upsample / yolo layers), batch 8 per GPU.
 """
 from __future__ import annotations
 
@@ -138,6 +140,27 @@ def bench_yolo(torch, hip, ctx, rank, steps, warmup=1):
         "gemm_tflops": gflop / gemm_ms if gemm_ms > 0 else None,
         "im2col_gbs": (col_bytes + in_bytes) / (i2c_ms * 1e6) if i2c_ms > 0 else None,
     }
+
+
+def bench_yolo_network(torch, hip, ctx, steps):
+    """The whole YOLOv3-416 network (yolov3.cfg plan: 75 convolutions chained
+    through shortcut / route / upsample / yolo, darknet.HipDarknet), batch 8
+    per GPU, BN-folded synthetic parameters."""
+    from tensorium_amd import darknet as dn
+    net = dn.Network(dn.parse_cfg(dn.yolov3_cfg(416)), 8)
+    model = dn.HipDarknet(hip, net, dn.random_params(net, seed=3), torch)
+    x = synthetic(torch, (8, 3, 416, 416), 3 * 100000 + ctx.rank, 0.0, 1.0)
+    model.forward(x)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        model.forward(x)
+    torch.cuda.synchronize()
+    ctx.barrier()
+    ms = ctx.max((time.perf_counter() - t0) / steps * 1e3)
+    return {"layers": len(net.layers), "batch_per_gpu": 8, "ms_per_batch": round(ms, 4),
+            "images_per_s": round(ctx.world * 8 / (ms / 1e3), 2)}
 
 
 def bench_batched(torch, hip, ctx, n_gemm=1024, n=1024, steps=3):
@@ -318,6 +341,9 @@ def main():
         y["images_per_s"] = world * y["batch_per_gpu"] / (ms / 1e3)
         yolo = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in y.items()}
 
+    yolo_net = None
+    if not args.no_yolo and args.yolo_steps > 0:
+        yolo_net = bench_yolo_network(torch, hip, ctx, args.yolo_steps)
     batched = None if args.no_batched else bench_batched(torch, hip, ctx)
     mnist = None if args.no_mnist else bench_mnist(torch, hip, ctx)
 
@@ -354,6 +380,7 @@ def main():
                          "algorithmic_flop_per_launch": flop},
             "cpu_baseline": cpu,
             "yolo": yolo,
+            "yolo_network": yolo_net,
             "batched_gemm": batched,
             "mnist_train": mnist,
         }

@@ -222,6 +222,22 @@ int tns_hip_copy(tns_ctx* ctx, int64_t N, const float* src, int64_t srcOffset, i
 int tns_hip_clamp(tns_ctx* ctx, int64_t N, float alpha, const float* src, float* dst,
                   int64_t stride, int64_t offset);
 
+/* ---- non-convolutional YOLOv3 layers (forward) ------------------------- */
+/* TAddLayer.forward (naddlayer.pas:667-720), single input of equal size:
+ * out = activate(a + b) (addvv, then the layer's activation). */
+int tns_hip_shortcut(tns_ctx* ctx, int64_t N, const float* a, int64_t aOffset, const float* b,
+                     int64_t bOffset, float* out, int64_t outOffset, int32_t activation);
+/* upsample() forward (nupsamplelayer.pas:83-113): planes = batch*channels,
+ * out[(p*H*s + y)*W*s + x] = scale * in[(p*H + y div s)*W + x div s]. */
+int tns_hip_upsample(tns_ctx* ctx, int64_t planes, int64_t H, int64_t W, int64_t stride,
+                     float scale, const float* in, float* out);
+/* TYoloLayer.forward inference part (nyololayer.pas:786-825): out = in with
+ * the logistic applied to entries 0, 1 and 4 .. 4+classes of every anchor;
+ * data [batch][anchors][classes+5][hw].  (Route/concat = tns_hip_copy of
+ * whole tensors, TTensor.concat ntensors.pas:12045-12061.) */
+int tns_hip_yolo_forward(tns_ctx* ctx, int64_t batch, int64_t anchors, int64_t classes,
+                         int64_t hw, const float* in, float* out);
+
 /* ---- batch norm / softmax (TNNCuda twins, nncuda.pas:1056-1510; CPU
  * semantics ntensors.pas:7687-7830, 8693-8951, 9102-9177,
  * nsoftmaxlayer.pas:83-137).  Data is [groups][channels][blockSize]. ---- */

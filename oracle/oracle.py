@@ -35,6 +35,9 @@ _PROTO = {
     "ora_add_bias": (None, [i64, fp, i64, fp, i64, i64]),
     "ora_backward_bias": (None, [i64, fp, i64, i64, fp]),
     "ora_activate": (C.c_int, [fp, i64, i32]),
+    "ora_shortcut": (C.c_int, [i64, fp, fp, fp, i32]),
+    "ora_upsample": (None, [i64, i64, i64, i64, f32, fp, fp]),
+    "ora_yolo_forward": (None, [i64, i64, i64, i64, fp, fp]),
     "ora_gradient": (C.c_int, [fp, i64, i32, fp]),
     "ora_conv2d": (None, [i64, i64, i64, i64, fp, fp, i64, i64, i64, i64, i64, i64, i64, i64, i64,
                           fp, fp]),
@@ -125,6 +128,30 @@ def col2im(C_, H, W, kH, kW, pH, pW, sY, sX, dY, dX, col: np.ndarray, im: np.nda
 def add_bias(x: np.ndarray, bias: np.ndarray, filters: int, block: int, batch: int):
     lib().ora_add_bias(filters, _p(x), block, _p(bias), 1, batch)
     return x
+
+
+def shortcut(a: np.ndarray, b: np.ndarray, act: int) -> np.ndarray:
+    out = np.empty_like(a)
+    rc = lib().ora_shortcut(a.size, _p(a), _p(b), _p(out), act)
+    assert rc == 0, act
+    return out
+
+
+def upsample(x: np.ndarray, planes: int, h: int, w: int, stride: int, scale: float = 1.0):
+    out = np.empty(planes * h * stride * w * stride, np.float32)
+    lib().ora_upsample(planes, h, w, stride, scale, _p(x), _p(out))
+    return out
+
+
+def yolo_forward(x: np.ndarray, batch: int, anchors: int, classes: int, hw: int) -> np.ndarray:
+    out = np.empty_like(x)
+    lib().ora_yolo_forward(batch, anchors, classes, hw, _p(x), _p(out))
+    return out
+
+
+def concat(tensors) -> np.ndarray:
+    """TTensor.concat (ntensors.pas:12045-12061): whole tensors, in order."""
+    return np.concatenate([np.ascontiguousarray(t).ravel() for t in tensors])
 
 
 def activate(x: np.ndarray, act: int) -> np.ndarray:
@@ -302,3 +329,40 @@ def mnist_batch(batch, seed=5, classes=10, inputs=784):
     T = np.zeros((batch, classes), np.float32)
     T[np.arange(batch), lab] = 1.0
     return X, T.ravel()
+
+
+def darknet_forward(net, params, x):
+    """TNNet.forward restated over a tensorium_amd.darknet.Network: every
+    layer's output (float32, flat), convolutions with BN folded first
+    (ora_fuse_batchnorm = fuseBatchNorm, nConvolutionLayer.pas:102-126)."""
+    B = net.batch
+    outs = []
+    prev = np.ascontiguousarray(x, np.float32).ravel()
+    ci = 0
+    for l in net.layers:
+        if l.kind == "convolutional":
+            p = params[ci]
+            ci += 1
+            w = np.ascontiguousarray(p.weights, np.float32).ravel().copy()
+            b = np.ascontiguousarray(p.biases, np.float32).copy()
+            if l.bn:
+                sc, rm, rv = (np.ascontiguousarray(t, np.float32) for t in
+                              (p.scales, p.rolling_mean, p.rolling_var))
+                lib().ora_fuse_batchnorm(l.filters, l.c * l.size * l.size, _p(w), _p(b), _p(sc),
+                                         _p(rm), _p(rv))
+            y = conv_forward(prev.reshape(B, l.c, l.h, l.w), w, b, l.filters, l.size, l.stride,
+                             l.pad, l.activation).ravel()
+        elif l.kind == "shortcut":
+            y = shortcut(prev, outs[l.inputs[0]], l.activation)
+        elif l.kind == "route":
+            y = concat([outs[s] for s in l.inputs])
+        elif l.kind == "upsample":
+            y = upsample(prev, B * l.c, l.h, l.w, l.stride, 1.0)
+        elif l.kind == "yolo":
+            y = yolo_forward(prev, B, l.anchors, l.classes, l.h * l.w)
+        else:
+            raise ValueError(l.kind)
+        outs.append(y)
+        prev = y
+    return outs
+

@@ -573,3 +573,40 @@ void ora_fill_uniform(float* x, int64_t n, uint64_t seed, uint64_t stream, float
     x[i] = fmaf(range, u, lo);
   }
 }
+
+/* ---- non-convolutional YOLOv3 layers (forward) -------------------------- */
+
+/* TAddLayer.forward (naddlayer.pas:667-720), one input of equal size:
+ * TSingleTensor.addvv(input, from.output) -> output, then the activation. */
+int ora_shortcut(int64_t n, const float* a, const float* b, float* out, int32_t act) {
+  for (int64_t i = 0; i < n; i++) out[i] = a[i] + b[i];
+  return ora_activate(out, n, act);
+}
+
+/* upsample(..., isForward = true, ...) (nupsamplelayer.pas:83-113) */
+void ora_upsample(int64_t planes, int64_t h, int64_t w, int64_t stride, float scale,
+                  const float* in, float* out) {
+  for (int64_t c = 0; c < planes; c++)
+    for (int64_t y = 0; y < h * stride; y++)
+      for (int64_t x = 0; x < w * stride; x++) {
+        const int64_t in_index = (c * h + y / stride) * w + x / stride;
+        const int64_t out_index = (c * h * stride + y) * stride * w + x;
+        out[out_index] = scale * in[in_index];
+      }
+}
+
+/* TYoloLayer.forward, inference part (nyololayer.pas:786-825, newCoords
+ * false, scaleXY 1): input copied, logistic over entries 0..1 and 4..4+classes
+ * of every (image, anchor); data [batch][anchors][classes+5][hw]. */
+void ora_yolo_forward(int64_t batch, int64_t anchors, int64_t classes, int64_t hw,
+                      const float* in, float* out) {
+  const int64_t entries = classes + 5;
+  memcpy(out, in, (size_t)(batch * anchors * entries * hw) * sizeof(float));
+  for (int64_t b = 0; b < batch; b++)
+    for (int64_t a = 0; a < anchors; a++) {
+      float* base = out + (b * anchors + a) * entries * hw;
+      ora_activate(base, 2 * hw, 0);
+      ora_activate(base + 4 * hw, (1 + classes) * hw, 0);
+    }
+}
+

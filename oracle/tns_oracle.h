@@ -142,6 +142,15 @@ float   ora_mlp_train_step(int32_t nlayers, const int64_t* widths, const int32_t
                            float momentum, float decay, float* buf);
 int64_t ora_mlp_buffer_floats(int32_t nlayers, const int64_t* widths, int32_t bn, int64_t B);
 
+/* non-convolutional YOLOv3 layers (forward): shortcut = addvv + activation
+ * (naddlayer.pas:667-720), upsample (nupsamplelayer.pas:83-113), yolo
+ * (nyololayer.pas:786-825) */
+int     ora_shortcut(int64_t n, const float* a, const float* b, float* out, int32_t act);
+void    ora_upsample(int64_t planes, int64_t h, int64_t w, int64_t stride, float scale,
+                     const float* in, float* out);
+void    ora_yolo_forward(int64_t batch, int64_t anchors, int64_t classes, int64_t hw,
+                         const float* in, float* out);
+
 /* counter-based synthetic data (splitmix64 -> u in [lo,hi)), keyed by
  * (seed, stream, index) so CPU and GPU regenerate identical tensors. */
 void    ora_fill_uniform(float* x, int64_t n, uint64_t seed, uint64_t stream,

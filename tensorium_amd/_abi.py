@@ -141,6 +141,9 @@ def check(rc: int) -> None:
 
 
 PROTOTYPES.update({
+    "tns_hip_shortcut": (C.c_int, [vp, i64, fptr, i64, fptr, i64, fptr, i64, i32]),
+    "tns_hip_upsample": (C.c_int, [vp, i64, i64, i64, i64, f32, fptr, fptr]),
+    "tns_hip_yolo_forward": (C.c_int, [vp, i64, i64, i64, i64, fptr, fptr]),
     "tns_hip_means_and_vars": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, fptr]),
     "tns_hip_normalize": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, i64, fptr, i64]),
     "tns_hip_forward_scale": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64]),

@@ -475,6 +475,36 @@ int tns_hip_copy(tns_ctx* c, int64_t N, const float* src, int64_t srcOffset, int
                     "copy");
 }
 
+int tns_hip_shortcut(tns_ctx* c, int64_t N, const float* a, int64_t aOffset, const float* b,
+                     int64_t bOffset, float* out, int64_t outOffset, int32_t activation) {
+  if (int r = check_ctx(c)) return r;
+  if (N < 0 || (N > 0 && (!a || !b || !out))) return set_error(TNS_ERR_ARG, "shortcut: bad args");
+  if (!act_supported(activation))
+    return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
+  return hip_status(launch_shortcut(N, a + aOffset, b + bOffset, out + outOffset, activation,
+                                    c->stream),
+                    "shortcut");
+}
+
+int tns_hip_upsample(tns_ctx* c, int64_t planes, int64_t H, int64_t W, int64_t stride, float scale,
+                     const float* in, float* out) {
+  if (int r = check_ctx(c)) return r;
+  if (planes < 0 || H < 0 || W < 0 || stride < 1 || H * stride > 0x7fffffff ||
+      W * stride > 0x7fffffff || (planes * H * W > 0 && (!in || !out)))
+    return set_error(TNS_ERR_ARG, "upsample: bad args");
+  return hip_status(launch_upsample(planes, (int)H, (int)W, (int)stride, scale, in, out, c->stream),
+                    "upsample");
+}
+
+int tns_hip_yolo_forward(tns_ctx* c, int64_t batch, int64_t anchors, int64_t classes, int64_t hw,
+                         const float* in, float* out) {
+  if (int r = check_ctx(c)) return r;
+  if (batch < 0 || anchors < 0 || classes < 0 || hw < 0 ||
+      (batch * anchors * hw > 0 && (!in || !out)))
+    return set_error(TNS_ERR_ARG, "yolo: bad args");
+  return hip_status(launch_yolo(batch, (int)anchors, (int)classes, hw, in, out, c->stream), "yolo");
+}
+
 int tns_hip_clamp(tns_ctx* c, int64_t N, float alpha, const float* src, float* dst,
                   int64_t stride, int64_t offset) {
   if (int r = check_ctx(c)) return r;

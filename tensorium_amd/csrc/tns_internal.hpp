@@ -106,6 +106,13 @@ hipError_t launch_forward_bias(float* dst, int64_t nFilters, int64_t blockSize,
 hipError_t launch_backward_bias(float* dst, int64_t nDst, const float* src, int64_t blockSize,
                                 int64_t batch, int64_t incb, hipStream_t s);
 hipError_t launch_activate(float* x, int64_t n, int act, hipStream_t s);
+// darknet_layers.hip: shortcut / upsample / yolo forward
+hipError_t launch_shortcut(int64_t n, const float* a, const float* b, float* out, int act,
+                           hipStream_t s);
+hipError_t launch_upsample(int64_t planes, int H, int W, int stride, float scale, const float* in,
+                           float* out, hipStream_t s);
+hipError_t launch_yolo(int64_t batch, int anchors, int classes, int64_t hw, const float* in,
+                       float* out, hipStream_t s);
 hipError_t launch_bias_activate(float* dst, int64_t nFilters, int64_t blockSize,
                                 const float* bias, int64_t batch, int act, hipStream_t s);
 hipError_t launch_derive(const float* x, int64_t n, int act, float* delta, hipStream_t s);

@@ -171,6 +171,20 @@ class TNNHip:
         check(self.lib.tns_hip_clamp(self.ctx, N, float(alpha), _ptr(src), _ptr(dst), stride,
                                      offset))
 
+    # -- non-convolutional YOLOv3 layers ----------------------------------------
+    def shortcut(self, N, a, aOffset, b, bOffset, out, outOffset=0, activation=4):
+        """TAddLayer.forward: out = activate(a + b)."""
+        check(self.lib.tns_hip_shortcut(self.ctx, N, _ptr(a), aOffset, _ptr(b), bOffset, _ptr(out),
+                                        outOffset, int(activation)))
+
+    def upsample(self, planes, H, W, stride, scale, inp, out):
+        check(self.lib.tns_hip_upsample(self.ctx, planes, H, W, stride, float(scale), _ptr(inp),
+                                        _ptr(out)))
+
+    def yoloForward(self, batch, anchors, classes, hw, inp, out):
+        check(self.lib.tns_hip_yolo_forward(self.ctx, batch, anchors, classes, hw, _ptr(inp),
+                                            _ptr(out)))
+
     # -- layer drivers ------------------------------------------------------------
     def conv2d(self, batch, C_, H, W, input, weights, filters, kH, kW, wPadding, hPadding,
                xStride, yStride, xDilation, yDilation, workspace, out):
