@@ -36,8 +36,12 @@ names.update({1 + l: f"fwd{l}" for l in range(6)})
 names[20] = "softmax"
 names.update({21 + l: f"bwd{l}" for l in range(6)})
 names.update({40 + l: f"upd{l}" for l in range(6)})
-order = [0] + [1 + l for l in range(6)] + [20] + [21 + l for l in reversed(range(6))] + \
-    [40 + l for l in range(6)]
+names.update({50 + 2 * l: f"bwd{l}.stage" for l in range(6)})
+names.update({51 + 2 * l: f"bwd{l}.chan" for l in range(6)})
+order = [0] + [1 + l for l in range(6)] + [20]
+for l in reversed(range(6)):
+    order += [50 + 2 * l, 51 + 2 * l, 21 + l]  # stage, column pass, gemms
+order += [40 + l for l in range(6)]
 prev = None
 for i in order:
     if prev is not None:

@@ -242,6 +242,9 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       // per channel: MeansAndVars, rolling stats, x, normalize, x_norm, scale
       const float* col = lds;  // the layer output, [B][O]
       for (int64_t o = tid; o < O; o += NT) {
+        // this channel's parameters, all loaded before any store: one memory
+        // round trip instead of one per use
+        const float rm0 = lay.rmean()[o], rv0 = lay.rvar()[o], sc = lay.scales()[o];
         float m = 0.0f;
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) m = m + col[b * O + o];
@@ -256,10 +259,9 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         lay.mean()[o] = m;
         lay.var()[o] = v;
         const float mom = 0.05f;  // bnMomentum, nconnectedlayer.pas:67
-        lay.rmean()[o] = fmaf(mom, m, lay.rmean()[o] * (1.0f - mom));
-        lay.rvar()[o] = fmaf(mom, v, lay.rvar()[o] * (1.0f - mom));
+        lay.rmean()[o] = fmaf(mom, m, rm0 * (1.0f - mom));
+        lay.rvar()[o] = fmaf(mom, v, rv0 * (1.0f - mom));
         const float sd = sqrtf(v > SEPS ? v : SEPS);
-        const float sc = lay.scales()[o];
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
           const float xv = col[b * O + o];
@@ -334,18 +336,28 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       }
     }
     __syncthreads();
+    MLP_STAMP(50 + 2 * l);
     // per channel: bias_updates.addSums, then the BN backward chain
     for (int64_t o = tid; o < O; o += NT) {
+      // this channel's parameters, all loaded before any store (one memory
+      // round trip instead of one per use)
+      const float db0 = lay.db()[o];
+      float ds0 = 0.0f, sc = 0.0f, mu = 0.0f, var = 0.0f;
+      if (a.bn) {
+        ds0 = lay.dscales()[o];
+        sc = lay.scales()[o];
+        mu = lay.mean()[o];
+        var = lay.var()[o];
+      }
       float r = 0.0f;
 #pragma unroll 8
       for (int64_t b = 0; b < B; ++b) r = r + sdel[b * O + o];
-      lay.db()[o] = lay.db()[o] + r;
+      lay.db()[o] = db0 + r;
       if (a.bn) {
         float dd = 0.0f;  // addDots (strided sdot: mul then add)
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) dd = dd + sxn[b * O + o] * sdel[b * O + o];
-        lay.dscales()[o] = lay.dscales()[o] + dd;
-        const float sc = lay.scales()[o], mu = lay.mean()[o];
+        lay.dscales()[o] = ds0 + dd;
         float m = 0.0f, v = 0.0f;
 #pragma unroll 8
         for (int64_t b = 0; b < B; ++b) {
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
           m = m + d;
           v = v + (sx[b * O + o] - mu) * d;
         }
-        const float ve = lay.var()[o] > SEPS ? lay.var()[o] : SEPS;
+        const float ve = var > SEPS ? var : SEPS;
         const float md = m * (-1.0f / sqrtf(ve));
         const float vd = (float)((double)v * -0.5 * pow((double)ve, -1.5));
         lay.mdelta()[o] = md;
@@ -369,6 +381,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       }
     }
     __syncthreads();
+    MLP_STAMP(51 + 2 * l);
     // dW += delta^T . in   (TN: M=O, N=I, K=B, beta 1)   and
     // prev_delta += delta . W (NN: M=B, N=I, K=O, beta 1), both ascending chains
     const int tmo = (int)((O + 31) / 32), tni = (int)((I + 31) / 32), tmb = (int)((B + 31) / 32);
