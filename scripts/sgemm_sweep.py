@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", default="")
     ap.add_argument("--batched", default="", help="n:batch strided-batched n^3 GEMMs")
+    ap.add_argument("--shapes", default="", help="M,N,K[;M,N,K...] plain NN GEMMs")
     args = ap.parse_args()
     hip = TNNHip(0)
     names = TNNHip.gemmVariants()
@@ -60,6 +61,12 @@ def main():
         B = torch.rand(n, n, device="cuda") * 2 - 1
         C = torch.zeros(n, n, device="cuda")
         probs[f"sq{n}"] = (n, n, n, 1, A, B, C)
+    for shp in [x for x in args.shapes.split(";") if x]:
+        M, N, K = (int(v) for v in shp.split(","))
+        A = torch.rand(M, K, device="cuda") * 2 - 1
+        B = torch.rand(K, N, device="cuda") * 2 - 1
+        C = torch.zeros(M, N, device="cuda")
+        probs[f"g{M}x{N}x{K}"] = (M, N, K, 1, A, B, C)
     if args.batched:
         n, nb = (int(v) for v in args.batched.split(":"))
         A = torch.rand(nb, n, n, device="cuda") * 2 - 1
