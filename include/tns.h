@@ -216,6 +216,18 @@ int tns_hip_derive_array(tns_ctx* ctx, int64_t N, const float* x, int64_t offset
 int tns_hip_axpy(tns_ctx* ctx, int64_t N, float a, const float* x, int64_t xOffset, int64_t incx,
                  float* y, int64_t yOffset, int64_t incy);
 int tns_hip_scale(tns_ctx* ctx, int64_t N, float a, float* x, int64_t stride);
+/* TConnectedLayer.update (nconnectedlayer.pas:324-359) /
+ * TConvolutionalLayer.update (nConvolutionLayer.pas:673-705) in one pass:
+ * biases += lrOverBatch*bias_updates, bias_updates *= momentum, the same for
+ * scales (NULL pair when the layer has no batch norm), weight_updates +=
+ * negDecayTimesBatch*weights, weights += lrOverBatch*weight_updates,
+ * weight_updates *= momentum (each axpy one FMA, each scale one multiply).
+ * The caller computes lrOverBatch = learning_rate / batch and
+ * negDecayTimesBatch = -decay * batch in single precision as the reference. */
+int tns_hip_sgd_update(tns_ctx* ctx, int64_t nWeights, float* weights, float* weight_updates,
+                       int64_t n, float* biases, float* bias_updates, float* scales,
+                       float* scale_updates, float lrOverBatch, float negDecayTimesBatch,
+                       float momentum);
 int tns_hip_fill(tns_ctx* ctx, int64_t N, float* x, int64_t offset, float val, int64_t stride);
 int tns_hip_copy(tns_ctx* ctx, int64_t N, const float* src, int64_t srcOffset, int64_t inca,
                  float* dst, int64_t dstOffset, int64_t incb);
@@ -361,8 +373,12 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * TNS_OPT_CONV_VARIANT (default -1 = heuristic): forces the tile shape of the
  * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name).
  * TNS_OPT_CONV_PAD (default -1 = by cost): 1 gathers from a zero-padded copy
- * of the images, 0 bounds-checks the window inside the GEMM. */
-enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2 };
+ * of the images, 0 bounds-checks the window inside the GEMM.
+ * TNS_OPT_NT_SDOT (default 1): gemm(NoTrans, Trans) sums in the reference's
+ * sdot_avx2 order (8 residue chains, ntensors.pas:1233-1306, 1957-2005), bit
+ * for bit; 0 = one ascending-k chain per element (faster, within 1e-4). */
+enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
+       TNS_OPT_NT_SDOT = 3 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

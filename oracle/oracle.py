@@ -203,6 +203,7 @@ def conv_backward(x, w, filters, k, stride, pad, act, output, delta, bias_update
 
 _PROTO2 = {
     "ora_vssum": (f32, [i64, fp]),
+    "ora_sgd_update": (None, [i64, fp, fp, i64, fp, fp, fp, fp, f32, f32, f32]),
     "ora_means_and_vars": (None, [fp, i64, i64, i64, fp, fp]),
     "ora_normalize": (None, [fp, i64, i64, i64, fp, fp]),
     "ora_forward_scale": (None, [fp, i64, i64, i64, fp]),
@@ -259,6 +260,14 @@ def add_dots(dst, a, b, groups, N, bs):
 def add_sums(dst, src, groups, N, bs):
     _lib2().ora_add_sums(_p(dst), _p(src), groups, N, bs)
     return dst
+
+
+def sgd_update(W, dW, b, db, scales, dscales, lrb, ndb, momentum):
+    """TConnectedLayer/TConvolutionalLayer.update in place (ora_sgd_update)."""
+    _lib2().ora_sgd_update(W.size, _p(W), _p(dW), b.size, _p(b), _p(db),
+                           _p(scales) if scales is not None else None,
+                           _p(dscales) if dscales is not None else None,
+                           lrb, ndb, momentum)
 
 
 def mean_var_delta(delta, x, mean, var, groups, N, bs):

@@ -397,15 +397,13 @@ void ora_add_bias(int64_t N, float* a, int64_t blockSize, const float* b, int64_
 void ora_backward_bias(int64_t nDst, float* dst, int64_t groups, int64_t blockSize,
                        const float* src) {
   /* addSums (7729-7781), generic (non-blockSize=1) branch order:
-   * _sum := sum_j sumv(blockSize, ...) ; sumv sequential (vsSumI). */
+   * _sum := _sum + sumv(blockSize, block_j, 1) for j ascending; sumv =
+   * vsSumI (3624-3635), which with stride 1 on an AVX2 x86-64 host is
+   * vssum_avx2 (3592-3620): 8 lanes, fold, sequential tail. */
   for (int64_t i = 0; i < nDst; i++) {
     float sum = 0.0f;
-    for (int64_t j = 0; j < groups; j++) {
-      const float* s = src + (j * nDst + i) * blockSize;
-      float part = 0.0f;
-      for (int64_t t = 0; t < blockSize; t++) part = part + s[t];
-      sum = sum + part;
-    }
+    for (int64_t j = 0; j < groups; j++)
+      sum = sum + ora_vssum(blockSize, src + (j * nDst + i) * blockSize);
     dst[i] = dst[i] + sum;
   }
 }

@@ -119,6 +119,8 @@ void    ora_fuse_batchnorm(int64_t filters, int64_t filterSize, float* weights,
 /* ---- batch-norm / softmax / SGD / connected-layer train step -------------
  * (tns_oracle_train.c; tolerance oracle: exp/ln/Power evaluated in double) */
 float   ora_vssum(int64_t n, const float* a);
+void    ora_sgd_update(int64_t nw, float* W, float* dW, int64_t n, float* b, float* db,
+                       float* scales, float* dscales, float lrb, float ndb, float momentum);
 void    ora_means_and_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
                            float* vars);
 void    ora_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,

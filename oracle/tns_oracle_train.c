@@ -116,9 +116,11 @@ void ora_add_dots(float* dst, const float* a, const float* b, int64_t groups, in
 }
 
 /* addSums blockSize == 1 branch: dst[i] += sumv(groups, src+i, stride N)
- * (strided -> scalar vsSumI loop). */
+ * (strided -> scalar vsSumI loop; stride 1, i.e. N == 1 -> vssum_avx2). */
 void ora_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs) {
-  if (bs == 1) {
+  if (bs == 1 && N == 1) {
+    dst[0] = dst[0] + ora_vssum(groups, src);
+  } else if (bs == 1) {
     for (int64_t i = 0; i < N; i++) {
       float r = 0.0f;
       for (int64_t g = 0; g < groups; g++) r = r + src[i + g * N];
@@ -264,17 +266,29 @@ static void scal_(int64_t n, float a, float* x) {
   for (int64_t i = 0; i < n; i++) x[i] = a * x[i]; /* sscal vmulps */
 }
 
-static void fc_update(ora_fc* L, float lr, float momentum, float decay, int64_t batch) {
-  const float lrb = lr / (float)batch;
-  axpy_(L->O, lrb, L->db, L->b);
-  scal_(L->O, momentum, L->db);
-  if (L->bn) {
-    axpy_(L->O, lrb, L->dscales, L->scales);
-    scal_(L->O, momentum, L->dscales);
+/* TConnectedLayer.update (nconnectedlayer.pas:324-359) and
+ * TConvolutionalLayer.update (nConvolutionLayer.pas:673-705), with
+ * lrb = learning_rate / batch and ndb = -decay * batch computed by the caller:
+ *   biases.axpy(lrb, bias_updates); bias_updates *= momentum;
+ *   scales.axpy(lrb, scale_updates); scale_updates *= momentum  (if scales);
+ *   weight_updates.axpy(ndb, weights); weights.axpy(lrb, weight_updates);
+ *   weight_updates *= momentum. */
+void ora_sgd_update(int64_t nw, float* W, float* dW, int64_t n, float* b, float* db,
+                    float* scales, float* dscales, float lrb, float ndb, float momentum) {
+  axpy_(n, lrb, db, b);
+  scal_(n, momentum, db);
+  if (scales) {
+    axpy_(n, lrb, dscales, scales);
+    scal_(n, momentum, dscales);
   }
-  axpy_(L->O * L->I, -decay * (float)batch, L->W, L->dW);
-  axpy_(L->O * L->I, lrb, L->dW, L->W);
-  scal_(L->O * L->I, momentum, L->dW);
+  axpy_(nw, ndb, W, dW);
+  axpy_(nw, lrb, dW, W);
+  scal_(nw, momentum, dW);
+}
+
+static void fc_update(ora_fc* L, float lr, float momentum, float decay, int64_t batch) {
+  ora_sgd_update(L->O * L->I, L->W, L->dW, L->O, L->b, L->db, L->bn ? L->scales : NULL,
+                 L->bn ? L->dscales : NULL, lr / (float)batch, -decay * (float)batch, momentum);
 }
 
 /* One TNNet.Propagate + update over a stack of connected layers followed by

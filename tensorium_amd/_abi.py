@@ -28,6 +28,7 @@ ACT = dict(LOGISTIC=0, RELU=1, RELU6=2, RELIE=3, LINEAR=4, RAMP=5, TANH=6, PLSE=
 TNS_OK = 0
 TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM, TNS_OP_BIAS, TNS_OP_ACTIVATE = range(5)
 TNS_OPT_STRICT_BETA0 = 0
+TNS_OPT_CONV_VARIANT, TNS_OPT_CONV_PAD, TNS_OPT_NT_SDOT = 1, 2, 3
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 
@@ -73,6 +74,8 @@ PROTOTYPES: dict[str, tuple] = {
     "tns_hip_activate_array": (C.c_int, [vp, i64, fptr, i64, i32]),
     "tns_hip_derive_array": (C.c_int, [vp, i64, fptr, i64, i32, fptr]),
     "tns_hip_axpy": (C.c_int, [vp, i64, f32, fptr, i64, i64, fptr, i64, i64]),
+    "tns_hip_sgd_update": (C.c_int, [vp, i64, fptr, fptr, i64, fptr, fptr, fptr, fptr, f32, f32,
+                                     f32]),
     "tns_hip_scale": (C.c_int, [vp, i64, f32, fptr, i64]),
     "tns_hip_fill": (C.c_int, [vp, i64, fptr, i64, f32, i64]),
     "tns_hip_copy": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64]),

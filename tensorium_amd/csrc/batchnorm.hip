@@ -307,6 +307,8 @@ hipError_t launch_add_dots(float* dst, const float* a, const float* b, int64_t g
 hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs,
                            hipStream_t s) {
   if (N <= 0) return hipSuccess;
+  if (bs == 1 && N == 1)  // stride 1: sumv is vssum_avx2 over the groups
+    return launch_backward_bias(dst, 1, src, groups, 1, 1, s);
   if (bs == 1) {
     hipLaunchKernelGGL(add_sums_seq, dim3(nblk(N)), dim3(TPB), 0, s, dst, src, groups, N);
     return hipGetLastError();

@@ -5,9 +5,8 @@
 //   activate        activate_array (nactivation.pas:508-621)
 //   bias_activate   the two above in one pass (conv forward, unfused GEMM path)
 //   derive          gradient_array (nactivation.pas:624-717)
-//   backward_bias   addSums (ntensors.pas:7729-7781) — one workgroup per
-//                   output, fixed-order tree reduction (deterministic; not
-//                   the reference's sequential order)
+//   backward_bias   addSums (ntensors.pas:7729-7781) in the reference's
+//                   order (vssum_avx2 per block, blocks in sequence)
 //   axpy/scale/fill/copy/clamp  TNNCuda BLAS-1 helpers
 // Contiguous kernels move 16 B per lane (float4) when alignment allows.
 #include "tns_act.hpp"
@@ -87,26 +86,185 @@ __global__ __launch_bounds__(TPB) void derive_kernel(const float* __restrict__ x
     delta[i] = delta[i] * grad_apply(x[i], act);
 }
 
-// one workgroup per output element; tree reduction in a fixed order.
+// addSums (ntensors.pas:7729-7781) in the reference's order: for output i,
+// _sum := _sum + sumv(bs, block_j) over groups j ascending, then
+// dst[i] := dst[i] + _sum; sumv = vssum_avx2 (3592-3620) on contiguous
+// blocks: 8 lanes of sequential adds over the full 8-blocks, lane pairs
+// (l, l+4) then ((s0+s1)+(s2+s3)), then the tail added in order.  One
+// workgroup per output; 8 consecutive lanes own one block (lane l = the
+// vssum lane), block totals meet in LDS and one thread adds them in j order.
+constexpr int BB_SLOTS = TPB / 8;
+constexpr int BB_CHUNK = 1024;
 __global__ __launch_bounds__(TPB) void backward_bias_kernel(float* __restrict__ dst, int64_t nDst,
                                                             const float* __restrict__ src,
-                                                            int64_t bs, int64_t batch,
+                                                            int64_t bs, int64_t groups,
                                                             int64_t incb) {
+  __shared__ float tot[BB_CHUNK];
   const int64_t i = blockIdx.x;
-  float s = 0.0f;
-  const int64_t per = batch * bs;
-  for (int64_t t = threadIdx.x; t < per; t += TPB) {
-    const int64_t b = t / bs, j = t - b * bs;
-    s += src[(b * nDst + i) * bs + j];
+  const int l = threadIdx.x & 7, q = threadIdx.x >> 3;
+  const int64_t nb = bs >> 3;
+  float sum = 0.0f;
+  for (int64_t j0 = 0; j0 < groups; j0 += BB_CHUNK) {
+    const int64_t jn = groups - j0 < BB_CHUNK ? groups - j0 : BB_CHUNK;
+    for (int64_t jj = q; jj < ((jn + BB_SLOTS - 1) / BB_SLOTS) * BB_SLOTS; jj += BB_SLOTS) {
+      const bool on = jj < jn;  // whole 8-lane groups are on or off
+      const float* blk = src + ((j0 + (on ? jj : 0)) * nDst + i) * bs;
+      float acc = 0.0f;
+      if (on) {
+        const float* p = blk + l;
+        int64_t t = 0;
+        for (; t + 8 <= nb; t += 8) {  // loads issued ahead of the dependent adds
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = p[8 * (t + u)];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc = acc + v[u];
+        }
+        for (; t < nb; ++t) acc = acc + p[8 * t];
+      }
+      const float s = acc + __shfl_down(acc, 4, 8);  // s_l = lane_l + lane_{l+4}
+      const float h = s + __shfl_down(s, 1, 8);      // s0+s1 (l=0), s2+s3 (l=2)
+      float r = h + __shfl_down(h, 2, 8);            // (s0+s1)+(s2+s3)
+      if (on && l == 0) {
+        for (int64_t u = nb * 8; u < bs; ++u) r = r + blk[u];
+        tot[jj] = r;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int64_t jj = 0; jj < jn; ++jj) sum = sum + tot[jj];
+    __syncthreads();
   }
-  // wave reduce (64 lanes) then across the 4 waves
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
-  __shared__ float part[TPB / 64];
-  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float tot = (part[0] + part[1]) + (part[2] + part[3]);
-    dst[i * incb] = dst[i * incb] + tot;
+  if (threadIdx.x == 0) dst[i * incb] = dst[i * incb] + sum;
+}
+
+// Same order for long blocks (conv layers at high resolution): 8 blocks at a
+// time, staged through LDS in tiles of BB_T elements per block by all 256
+// threads (coalesced, double-buffered), while wave 0's 64 lanes (8 per block,
+// the vssum lanes) run the sequential chains out of LDS.  The chains are
+// inherently serial; with one workgroup per output the tile loads' latency
+// bounds the widest layers (32 x 173056 x 8: 0.35 ms, 0.5 TB/s).
+constexpr int BB_T = 1024;
+constexpr int BB_LD = BB_T + 8;  // row stride: the 8 blocks' lanes hit distinct banks
+constexpr int BB_E = 8 * BB_T / TPB;
+__global__ __launch_bounds__(TPB) void backward_bias_tiled_kernel(float* __restrict__ dst,
+                                                                  int64_t nDst,
+                                                                  const float* __restrict__ src,
+                                                                  int64_t bs, int64_t groups,
+                                                                  int64_t incb) {
+  __shared__ float buf[2][8 * BB_LD];
+  __shared__ float tot[8];
+  const int64_t i = blockIdx.x;
+  const int tid = threadIdx.x, jj = (tid & 63) >> 3, l = tid & 7;
+  const bool chain = tid < 64;
+  const int64_t nb8 = (bs >> 3) << 3;  // elements in full 8-blocks
+  const int ntile = (int)((nb8 + BB_T - 1) / BB_T);
+  float sum = 0.0f;
+  for (int64_t j0 = 0; j0 < groups; j0 += 8) {
+    const int jn = groups - j0 < 8 ? (int)(groups - j0) : 8;
+    float r[BB_E];
+    auto load = [&](int t) {
+#pragma unroll
+      for (int u = 0; u < BB_E; ++u) {
+        const int e = tid + TPB * u, b = e / BB_T, x = e % BB_T;
+        const int64_t k = (int64_t)t * BB_T + x;
+        r[u] = (b < jn && k < nb8) ? src[((j0 + b) * nDst + i) * bs + k] : 0.0f;
+      }
+    };
+    auto store = [&](float* d) {
+#pragma unroll
+      for (int u = 0; u < BB_E; ++u) {
+        const int e = tid + TPB * u;
+        d[(e / BB_T) * BB_LD + e % BB_T] = r[u];
+      }
+    };
+    float acc = 0.0f;
+    if (ntile > 0) {
+      load(0);
+      store(buf[0]);
+      __syncthreads();
+    }
+    for (int t = 0; t < ntile; ++t) {
+      if (t + 1 < ntile) load(t + 1);
+      if (chain && jj < jn) {
+        const float* row = buf[t & 1] + jj * BB_LD + l;
+        const int64_t rem = nb8 - (int64_t)t * BB_T;
+        const int cnt = (int)((rem < BB_T ? rem : BB_T) >> 3);
+        int u = 0;
+        for (; u + 16 <= cnt; u += 16) {
+          float v[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) v[q] = row[8 * (u + q)];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc = acc + v[q];
+        }
+        for (; u < cnt; ++u) acc = acc + row[8 * u];
+      }
+      if (t + 1 < ntile) store(buf[(t + 1) & 1]);
+      __syncthreads();
+    }
+    {
+      const float s = acc + __shfl_down(acc, 4, 8);
+      const float h = s + __shfl_down(s, 1, 8);
+      float q = h + __shfl_down(h, 2, 8);
+      if (chain && l == 0 && jj < jn) {
+        const float* blk = src + ((j0 + jj) * nDst + i) * bs;
+        for (int64_t u = nb8; u < bs; ++u) q = q + blk[u];
+        tot[jj] = q;
+      }
+    }
+    __syncthreads();
+    if (tid == 0)
+      for (int b = 0; b < jn; ++b) sum = sum + tot[b];
+    __syncthreads();
+  }
+  if (tid == 0) dst[i * incb] = dst[i * incb] + sum;
+}
+
+// TConnectedLayer.update / TConvolutionalLayer.update (nconnectedlayer.pas:
+// 324-359, nConvolutionLayer.pas:673-705) in one pass: per weight
+//   u = fma(ndb, w, dw)       weight_updates.axpy(-decay*batch, weights)
+//   w = fma(lrb, u, w)        weights.axpy(lr/batch, weight_updates)
+//   dw = momentum * u         weight_updates.Multiply(momentum)
+// and per output the biases / scales axpy + momentum scale.  16 B of HBM per
+// weight instead of the 32 B of the three separate passes.
+template <int V>
+__global__ __launch_bounds__(TPB) void sgd_update_kernel(int64_t nw, float* __restrict__ w,
+                                                         float* __restrict__ dw, int64_t n,
+                                                         float* __restrict__ b,
+                                                         float* __restrict__ db,
+                                                         float* __restrict__ sc,
+                                                         float* __restrict__ dsc, float lrb,
+                                                         float ndb, float mom) {
+  const int64_t stride = (int64_t)gridDim.x * TPB;
+  const int64_t t0 = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if constexpr (V == 4) {
+    float4* w4 = reinterpret_cast<float4*>(w);
+    float4* d4 = reinterpret_cast<float4*>(dw);
+    for (int64_t i = t0; i < nw / 4; i += stride) {
+      const float4 x = w4[i], g = d4[i];
+      float4 u, y;
+      u.x = fmaf(ndb, x.x, g.x); u.y = fmaf(ndb, x.y, g.y);
+      u.z = fmaf(ndb, x.z, g.z); u.w = fmaf(ndb, x.w, g.w);
+      y.x = fmaf(lrb, u.x, x.x); y.y = fmaf(lrb, u.y, x.y);
+      y.z = fmaf(lrb, u.z, x.z); y.w = fmaf(lrb, u.w, x.w);
+      w4[i] = y;
+      d4[i] = make_float4(mom * u.x, mom * u.y, mom * u.z, mom * u.w);
+    }
+  }
+  for (int64_t i = (V == 4 ? nw / 4 * 4 : 0) + t0; i < nw; i += stride) {
+    const float x = w[i];
+    const float u = fmaf(ndb, x, dw[i]);
+    w[i] = fmaf(lrb, u, x);
+    dw[i] = mom * u;
+  }
+  for (int64_t i = t0; i < n; i += stride) {
+    b[i] = fmaf(lrb, db[i], b[i]);
+    db[i] = mom * db[i];
+    if (sc) {
+      sc[i] = fmaf(lrb, dsc[i], sc[i]);
+      dsc[i] = mom * dsc[i];
+    }
   }
 }
 
@@ -212,8 +370,27 @@ hipError_t launch_derive(const float* x, int64_t n, int act, float* delta, hipSt
 hipError_t launch_backward_bias(float* dst, int64_t nDst, const float* src, int64_t bs,
                                 int64_t batch, int64_t incb, hipStream_t s) {
   if (nDst <= 0) return hipSuccess;
-  hipLaunchKernelGGL(backward_bias_kernel, dim3((unsigned)nDst), dim3(TPB), 0, s, dst, nDst, src,
-                     bs, batch, incb);
+  if (bs >= 2048)
+    hipLaunchKernelGGL(backward_bias_tiled_kernel, dim3((unsigned)nDst), dim3(TPB), 0, s, dst,
+                       nDst, src, bs, batch, incb);
+  else
+    hipLaunchKernelGGL(backward_bias_kernel, dim3((unsigned)nDst), dim3(TPB), 0, s, dst, nDst,
+                       src, bs, batch, incb);
+  return hipGetLastError();
+}
+
+hipError_t launch_sgd_update(int64_t nw, float* w, float* dw, int64_t n, float* b, float* db,
+                             float* sc, float* dsc, float lrb, float ndb, float mom,
+                             hipStream_t s) {
+  if (nw <= 0 && n <= 0) return hipSuccess;
+  const bool v4 = ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dw)) & 15) == 0;
+  const unsigned g = grid_for((v4 ? nw / 4 : nw) > n ? (v4 ? nw / 4 : nw) : n);
+  if (v4)
+    hipLaunchKernelGGL(sgd_update_kernel<4>, dim3(g), dim3(TPB), 0, s, nw, w, dw, n, b, db, sc,
+                       dsc, lrb, ndb, mom);
+  else
+    hipLaunchKernelGGL(sgd_update_kernel<1>, dim3(g), dim3(TPB), 0, s, nw, w, dw, n, b, db, sc,
+                       dsc, lrb, ndb, mom);
   return hipGetLastError();
 }
 

@@ -1,0 +1,186 @@
+// sgemm_sdot.hip — gemm(NoTrans, Trans) in the reference's sdot order.
+//
+// Replaces sgemm_nt / s_nt (ntensors.pas:1957-2005) over sdot_avx2
+// (1233-1306): C[i,j] := C[i,j] + ALPHA * sdot(K, A[i,:], B[j,:]) after the
+// cblas_sgemm beta pre-scale (2231-2286).  sdot_avx2 keeps 8 FMA lanes, lane l
+// an ascending fma chain over k = l (mod 8) started at +0 (the masked tail is
+// the same chain's last element, or fma(0, 0, x) = x), then sums
+// s_l = lane_l + lane_{l+4} and returns (s0 + s1) + (s2 + s3).
+//
+// Here each residue class is an ascending f32-MFMA chain (v_mfma_f32_32x32x2
+// is a bit-exact k-ordered fmaf chain, profiles/r01_mfma_order_probe.txt):
+// a block owns a 32 x 32*TN output tile and its 8 waves are the 8 residue
+// classes; MFMA step s of wave r consumes k = r + 16s + 8h (lane half h).
+// Both operands are k-contiguous rows, staged global -> registers -> LDS
+// ([row][k], odd row stride) in k-tiles of 64, double-buffered with one
+// barrier per tile.  Zero-filled k >= K adds fma(0, 0, x) = x (a chain that
+// starts at +0 never holds -0).  The epilogue meets the 8 partial tiles in LDS
+// and applies the reference's pairwise sum, alpha product and C add, each
+// rounded separately (built with -ffp-contract=off).
+#include "tns_internal.hpp"
+
+namespace tns {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int SD_NT = 512;       // 8 waves = 8 residue classes
+constexpr int SD_BK = 64;        // k per tile: 8 per residue class = 4 MFMA steps
+constexpr int SD_KP = SD_BK + 1;  // LDS row stride
+
+__device__ __attribute__((aligned(16))) static float4 g_sd_zero;
+
+template <int TN, int VEC>
+__global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
+  constexpr int BM = 32, BN = 32 * TN, ROWS = BM + BN;
+  constexpr int KV = SD_BK / VEC;               // staging units per row
+  constexpr int U = ROWS * KV / SD_NT;          // staging units per thread
+  static_assert(ROWS * KV % SD_NT == 0, "staging split");
+  constexpr int STAGE = ROWS * SD_KP;
+  constexpr int PART = 8 * BM * BN;
+  constexpr int LDS = 2 * STAGE > PART ? 2 * STAGE : PART;
+  __shared__ float lds[LDS];
+
+  const int tid = threadIdx.x, r = tid >> 6, lane = tid & 63;
+  const int l31 = lane & 31, h = lane >> 5;
+  const int tiles_m = (int)((p.M + BM - 1) / BM);
+  const int64_t m0 = (int64_t)(blockIdx.x % tiles_m) * BM;
+  const int64_t n0 = (int64_t)(blockIdx.x / tiles_m) * BN;
+  const int64_t bz = blockIdx.y;
+  const float* __restrict__ A = p.A + bz * p.strideA;
+  const float* __restrict__ B = p.B + bz * p.strideB;
+  float* __restrict__ C = p.C + bz * p.strideC;
+  const int64_t M = p.M, N = p.N, K = p.K;
+
+  float st[U * VEC];
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = tid + SD_NT * u;
+      const int row = idx / KV;
+      const int64_t k = k0 + VEC * (idx % KV);
+      const bool isa = row < BM;
+      const int64_t g = isa ? m0 + row : n0 + row - BM;
+      // VEC = 4 only when K % 4 == 0: a float4 is wholly inside or outside
+      const bool ok = (g < (isa ? M : N)) & (k < K);
+      const float* src = ok ? (isa ? A + g * p.lda : B + g * p.ldb) + k
+                            : reinterpret_cast<const float*>(&g_sd_zero);
+      if constexpr (VEC == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(src);
+        st[4 * u + 0] = v.x;
+        st[4 * u + 1] = v.y;
+        st[4 * u + 2] = v.z;
+        st[4 * u + 3] = v.w;
+      } else {
+        st[u] = *src;
+      }
+    }
+  };
+  auto store = [&](float* buf) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = tid + SD_NT * u;
+      const int row = idx / KV, k = VEC * (idx % KV);
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) buf[row * SD_KP + k + c] = st[VEC * u + c];
+    }
+  };
+
+  floatx16 acc[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
+
+  const int nt = (int)((K + SD_BK - 1) / SD_BK);
+  if (nt > 0) {
+    load(0);
+    store(lds);
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const float* cur = lds + (t & 1) * STAGE;
+      if (t + 1 < nt) load((int64_t)(t + 1) * SD_BK);
+#pragma unroll
+      for (int s = 0; s < SD_BK / 16; ++s) {
+        const int kk = r + 16 * s + 8 * h;  // residue class r, ascending
+        const float a = cur[l31 * SD_KP + kk];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, cur[(BM + 32 * j + l31) * SD_KP + kk],
+                                                        acc[j], 0, 0, 0);
+      }
+      if (t + 1 < nt) store(lds + ((t + 1) & 1) * STAGE);
+      __syncthreads();
+    }
+  }
+
+  // partial tile of residue class r -> lds[r][row][col] (every wave has
+  // passed the last barrier, so the operand buffers are free)
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+      lds[(r * BM + row) * BN + 32 * j + l31] = acc[j][e];
+    }
+  __syncthreads();
+  const float alpha = p.alpha, beta = p.beta;
+  for (int o = tid; o < BM * BN; o += SD_NT) {
+    const int64_t m = m0 + o / BN, n = n0 + o % BN;
+    if (m >= M || n >= N) continue;
+    float q[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) q[c] = lds[c * BM * BN + o];
+    const float s0 = q[0] + q[4], s1 = q[1] + q[5], s2 = q[2] + q[6], s3 = q[3] + q[7];
+    const float dot = (s0 + s1) + (s2 + s3);
+    const float sum = alpha * dot;  // sum := ALPHA * sdot(...)
+    float* cp = C + m * p.ldc + n;
+    float c0;
+    if (p.beta_mode == BETA_ZERO)
+      c0 = 0.0f;
+    else if (p.beta_mode == BETA_SCALE)
+      c0 = beta * *cp;  // cblas_sgemm's mulvs pre-scale
+    else
+      c0 = *cp;
+    *cp = c0 + sum;  // C[i,j] := C[i,j] + sum
+  }
+}
+
+template <int TN, int VEC>
+hipError_t launch_tn(const GemmArgs& a, hipStream_t s) {
+  const int64_t tiles = ((a.M + 31) / 32) * ((a.N + 32 * TN - 1) / (32 * TN));
+  if (tiles > 0x7fffffff) return hipErrorInvalidValue;
+  for (int64_t b0 = 0; b0 < a.batch; b0 += 65535) {
+    GemmArgs sub = a;
+    const int64_t nb = a.batch - b0 < 65535 ? a.batch - b0 : 65535;
+    sub.A = a.A + b0 * a.strideA;
+    sub.B = a.B + b0 * a.strideB;
+    sub.C = a.C + b0 * a.strideC;
+    sub.batch = nb;
+    hipLaunchKernelGGL((sgemm_nt_sdot_kernel<TN, VEC>), dim3((unsigned)tiles, (unsigned)nb),
+                       dim3(SD_NT), 0, s, sub);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+bool k_vec4(const float* p, int64_t ld, int64_t stride, int64_t batch, int64_t K) {
+  if ((reinterpret_cast<uintptr_t>(p) & 15) != 0) return false;
+  if (ld % 4 != 0 || K % 4 != 0) return false;
+  return batch <= 1 || stride % 4 == 0;
+}
+
+}  // namespace
+
+// 32x64 tiles when they still give >= 4 blocks per CU, else 32x32
+hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0 || a.batch <= 0) return hipSuccess;
+  const bool v = k_vec4(a.A, a.lda, a.strideA, a.batch, a.K) &&
+                 k_vec4(a.B, a.ldb, a.strideB, a.batch, a.K);
+  const int64_t b64 = ((a.M + 31) / 32) * ((a.N + 63) / 64) * a.batch;
+  if (b64 >= 1024) return v ? launch_tn<2, 4>(a, s) : launch_tn<2, 1>(a, s);
+  return v ? launch_tn<1, 4>(a, s) : launch_tn<1, 1>(a, s);
+}
+
+}  // namespace tns

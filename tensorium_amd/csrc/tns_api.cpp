@@ -27,6 +27,7 @@ namespace tns {
 static thread_local std::string g_err;
 static tns_error_hook_t g_hook = nullptr;
 static int64_t g_strict_beta0 = 1;
+static int64_t g_nt_sdot = 1;
 static int64_t g_conv_variant = -1;
 static int64_t g_conv_pad = -1;
 
@@ -142,6 +143,8 @@ int do_gemm(tns_ctx* c, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float
   a.C = C; a.ldc = ldc; a.strideC = sC;
   a.batch = batch; a.epi = epi; a.bias = bias; a.act = act;
   OpTimer t(c, TNS_OP_GEMM);
+  if (!ta && tb && g_nt_sdot && variant < 0 && epi == EPI_NONE)
+    return hip_status(launch_sgemm_nt_sdot(a, c->stream), "sgemm_nt launch");
   hipError_t e = launch_sgemm_variant(variant, a, ta, tb, c->stream);
   if (e == hipErrorInvalidValue && variant >= 0)
     return set_error(TNS_ERR_UNSUPPORTED, "gemm variant %d (%s) does not support this problem",
@@ -236,6 +239,9 @@ int tns_set_option(int32_t opt, int64_t value) {
       return TNS_OK;
     case TNS_OPT_CONV_PAD:
       g_conv_pad = value < 0 ? -1 : (value ? 1 : 0);
+      return TNS_OK;
+    case TNS_OPT_NT_SDOT:
+      g_nt_sdot = value ? 1 : 0;
       return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
@@ -456,6 +462,20 @@ int tns_hip_axpy(tns_ctx* c, int64_t N, float a, const float* x, int64_t xOffset
                  float* y, int64_t yOffset, int64_t incy) {
   if (int r = check_ctx(c)) return r;
   return hip_status(launch_axpy(N, a, x + xOffset, incx, y + yOffset, incy, c->stream), "axpy");
+}
+
+int tns_hip_sgd_update(tns_ctx* c, int64_t nWeights, float* weights, float* weight_updates,
+                       int64_t n, float* biases, float* bias_updates, float* scales,
+                       float* scale_updates, float lrOverBatch, float negDecayTimesBatch,
+                       float momentum) {
+  if (int r = check_ctx(c)) return r;
+  if (nWeights < 0 || n < 0 || (nWeights > 0 && (!weights || !weight_updates)) ||
+      (n > 0 && (!biases || !bias_updates)) || (!scales != !scale_updates))
+    return set_error(TNS_ERR_ARG, "sgd_update: bad arguments");
+  return hip_status(launch_sgd_update(nWeights, weights, weight_updates, n, biases, bias_updates,
+                                      n > 0 ? scales : nullptr, scale_updates, lrOverBatch,
+                                      negDecayTimesBatch, momentum, c->stream),
+                    "sgd_update");
 }
 
 int tns_hip_scale(tns_ctx* c, int64_t N, float a, float* x, int64_t stride) {

@@ -71,6 +71,9 @@ struct GemmArgs {
 };
 
 hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s);
+// gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
+// plain epilogue only
+hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
 // implicit-GEMM convolution: NN, B generated from the image (a.conv must be set)
 hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s);
 hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s);
@@ -116,6 +119,10 @@ hipError_t launch_yolo(int64_t batch, int anchors, int classes, int64_t hw, cons
 hipError_t launch_bias_activate(float* dst, int64_t nFilters, int64_t blockSize,
                                 const float* bias, int64_t batch, int act, hipStream_t s);
 hipError_t launch_derive(const float* x, int64_t n, int act, float* delta, hipStream_t s);
+// TConnectedLayer/TConvolutionalLayer.update fused (elementwise.hip)
+hipError_t launch_sgd_update(int64_t nw, float* w, float* dw, int64_t n, float* b, float* db,
+                             float* sc, float* dsc, float lrb, float ndb, float mom,
+                             hipStream_t s);
 hipError_t launch_axpy(int64_t n, float a, const float* x, int64_t incx, float* y, int64_t incy,
                        hipStream_t s);
 hipError_t launch_scale(int64_t n, float a, float* x, int64_t stride, hipStream_t s);

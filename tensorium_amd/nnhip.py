@@ -12,6 +12,8 @@ from __future__ import annotations
 
 import ctypes as C
 
+import numpy as np
+
 from ._abi import TnsError, check, load
 
 try:  # torch is optional plumbing
@@ -157,6 +159,18 @@ class TNNHip:
         check(self.lib.tns_hip_axpy(self.ctx, N, float(a), _ptr(x), xOffset, incx, _ptr(y),
                                     yOffset, incy))
 
+    def sgdUpdate(self, weights, weight_updates, biases, bias_updates, learningRate, batch,
+                  decay, momentum, scales=None, scale_updates=None):
+        """TConnectedLayer.update / TConvolutionalLayer.update (learningRate
+        already multiplied by learningRateScale for conv layers), fused."""
+        f32 = np.float32
+        lrb = f32(f32(learningRate) / f32(batch))
+        ndb = f32(-f32(decay) * f32(batch))
+        check(self.lib.tns_hip_sgd_update(
+            self.ctx, weights.numel(), _ptr(weights), _ptr(weight_updates), biases.numel(),
+            _ptr(biases), _ptr(bias_updates), _ptr(scales), _ptr(scale_updates), float(lrb),
+            float(ndb), float(momentum)))
+
     def scale(self, N, a, x, stride):
         check(self.lib.tns_hip_scale(self.ctx, N, float(a), _ptr(x), stride))
 
@@ -218,6 +232,11 @@ class TNNHip:
     def setConvPad(self, mode: int = -1):
         """Implicit-GEMM gather: 1 padded copy, 0 bounds-checked, -1 by cost."""
         check(self.lib.tns_set_option(2, int(mode)))
+
+    def setNtSdot(self, on: bool = True):
+        """gemm(NoTrans, Trans) in the reference's sdot order (default) or as
+        one ascending-k chain per element; process-wide."""
+        check(self.lib.tns_set_option(3, 1 if on else 0))
 
     # -- batch norm / softmax (TNNCuda.meansAndVars ... crossEntropySoftmax) ----
     def meansAndVars(self, srcSize, dstSize, groups, src, offset, means, vars_):

@@ -128,9 +128,8 @@ def test_yolov3_layers_batch8_implicit(hip, torch_cuda, ora, idx):
     (2, 3, 17, 8, 3, 1, 1, 9), (3, 5, 12, 7, 3, 2, 1, 9), (2, 16, 9, 5, 1, 1, 0, 4),
     (2, 6, 13, 33, 3, 1, 1, 1), (1, 32, 26, 64, 3, 2, 1, 9)])
 def test_conv_backward_matches_oracle(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act):
-    """delta (derived) and state_delta (TN + col2im) bit-exact; weight_updates
-    (NT, reference sdot order) within the componentwise GEMM bound; bias
-    sums within 1e-5 relative."""
+    """delta (derived), state_delta (TN + col2im), weight_updates (NT in the
+    reference's sdot order) and bias_updates (addSums order) bit-exact."""
     rng = np.random.default_rng(batch * 1000 + C * 10 + H)
     oh = (H + 2 * p - k) // s + 1
     x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
@@ -148,14 +147,8 @@ def test_conv_backward_matches_oracle(hip, torch_cuda, ora, batch, C, H, F, k, s
     hip.finish()
     assert np.array_equal(dd.cpu().numpy(), rd)
     assert np.array_equal(dsd.cpu().numpy(), rsd)
-    # weight_updates bound: |A||B| over the batch-concatenated NT product
-    i_k = oh * oh
-    cols = ora.im2col(C, H, H, k, k, p, p, s, s, 1, 1, x, batch)
-    bnd = sum(np.abs(rd[b].reshape(F, -1)).astype(np.float64) @ np.abs(cols[b]).T
-              for b in range(batch)) + np.abs(wu0.reshape(F, -1))
-    err = np.abs(dwu.cpu().numpy().reshape(F, -1).astype(np.float64) - rwu.reshape(F, -1))
-    assert np.all(err <= 1e-4 * bnd + 1e-30)
-    assert np.allclose(dbu.cpu().numpy(), rbu, rtol=1e-5, atol=1e-5)
+    assert np.array_equal(dwu.cpu().numpy(), rwu)
+    assert np.array_equal(dbu.cpu().numpy(), rbu)
 
 
 def test_conv_backward_rejects_dilation(hip, torch_cuda):

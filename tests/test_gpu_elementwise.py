@@ -54,16 +54,22 @@ def test_forward_bias(hip, torch_cuda, ora, F, bs, batch):
     assert np.array_equal(dx.cpu().numpy(), ref)
 
 
-def test_backward_bias_close(hip, torch_cuda, ora):
-    F, bs, batch = 16, 333, 4
+@pytest.mark.parametrize("F,bs,batch", [(16, 333, 4), (3, 8, 2), (5, 7, 3), (1, 1000, 40),
+                                         (4, 64, 1100), (2, 43264, 8), (3, 2053, 11),
+                                         (2, 4096, 3)])
+def test_backward_bias_addsums_order(hip, torch_cuda, ora, F, bs, batch):
+    """addSums (ntensors.pas:7729-7781): vssum_avx2 per contiguous block,
+    blocks summed in order — bit-exact; also more groups than one LDS chunk."""
     src = ora.uniform(batch * F * bs, 13, 0)
     dst = ora.uniform(F, 14, 0)
-    ref = dst.astype(np.float64) + src.reshape(batch, F, bs).astype(np.float64).sum(axis=(0, 2))
+    ref = ora.add_sums(dst.copy(), src, batch, F, bs)
     dsrc, ddst = torch_cuda.from_numpy(src).cuda(), torch_cuda.from_numpy(dst.copy()).cuda()
     hip.backwardBias(F, ddst, src.size, dsrc, 0, 1, batch)
     hip.finish()
+    assert np.array_equal(ddst.cpu().numpy(), ref)
     scale = np.abs(src.reshape(batch, F, bs)).sum(axis=(0, 2)) + np.abs(dst)
-    assert np.all(np.abs(ddst.cpu().numpy() - ref) <= 1e-5 * scale)
+    f64 = dst.astype(np.float64) + src.reshape(batch, F, bs).astype(np.float64).sum(axis=(0, 2))
+    assert np.all(np.abs(ref - f64) <= 1e-5 * scale)
 
 
 def test_blas1(hip, torch_cuda, ora):

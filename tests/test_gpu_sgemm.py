@@ -4,8 +4,11 @@ against the oracle (restated cblas_sgemm, ntensors.pas:2231-2304).
 Bar:
   * NN and TN: bit-identical to the reference's ascending-k FMA chain
     (gfx950 f32 MFMA is an exact k-ordered fmaf chain).
-  * NT and TT: componentwise |C - C_ref| <= 1e-4 * (|alpha||A||B| + |beta||C0|)_ij
-    (the reference sums NT in 8 sdot lanes and TT with unfused mul+add).
+  * NT: bit-identical to the reference's sdot_avx2 order (8 residue chains
+    k mod 8, pairwise lane sum, alpha product, C add; sgemm_sdot.hip);
+    with TNS_OPT_NT_SDOT = 0, within the componentwise bound below.
+  * TT: componentwise |C - C_ref| <= 1e-4 * (|alpha||A||B| + |beta||C0|)_ij
+    (the reference's scalar TT rounds mul and add separately).
 """
 import numpy as np
 import pytest
@@ -74,6 +77,54 @@ def test_all_transposes_within_bound(hip, torch_cuda, ora, M, N, K, ta, tb):
         bnd = bound(ta, tb, A, B, alpha, beta, C0)
         err = np.abs(got.astype(np.float64) - ref)
         assert np.all(err <= TOL * bnd + 1e-30), float((err / (bnd + 1e-30)).max())
+
+
+NT_SHAPES = SHAPES + [(32, 4096, 4096), (32, 64, 784), (10, 32, 32), (3, 5, 8), (3, 5, 9),
+                     (33, 65, 15), (64, 1152, 2704), (70, 90, 2304)]
+
+
+@pytest.mark.parametrize("M,N,K", NT_SHAPES)
+def test_nt_sdot_bit_exact(hip, torch_cuda, ora, M, N, K):
+    """gemm(NoTrans, Trans) = s_nt over sdot_avx2 (ntensors.pas:1957-2005,
+    1233-1306): every K mod 8 tail, float4 and scalar staging, skinny FC
+    shapes (batch 32) and conv dW shapes."""
+    rng = np.random.default_rng(M * 7 + N * 3 + K + 11)
+    A, B, C0 = operands(rng, 0, 1, M, N, K)
+    for alpha, beta in [(1.0, 0.0), (0.5, 2.0), (1.0, 1.0), (-1.5, 0.25)]:
+        got = run_dev(hip, torch_cuda, 0, 1, A, B, C0, alpha, beta)
+        ref = run_ref(ora, 0, 1, A, B, C0, alpha, beta)
+        assert np.array_equal(got, ref), (M, N, K, alpha, beta,
+                                          float(np.abs(got - ref).max()))
+        if M * N * K > 1e8:
+            break
+
+
+def test_nt_sdot_batched_offsets_and_plain_order(hip, torch_cuda, ora):
+    """Strided-batched NT with element offsets and padded leading dims; then
+    the plain-order option (one ascending chain per element) within bound."""
+    rng = np.random.default_rng(12)
+    batch, M, N, K, lda, ldb, off = 3, 45, 70, 37, 41, 39, 5
+    A = rng.uniform(-1, 1, off + batch * M * lda).astype(np.float32)
+    B = rng.uniform(-1, 1, off + batch * N * ldb).astype(np.float32)
+    C = rng.uniform(-1, 1, off + batch * M * N).astype(np.float32)
+    dA, dB, dC = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B, C))
+    hip.gemmStridedBatched(False, True, M, N, K, 0.5, dA, off, lda, M * lda, dB, off, ldb,
+                           N * ldb, 1.0, dC, off, N, M * N, batch)
+    hip.finish()
+    ref = C.copy()
+    ora.sgemm_batch_strided(False, True, M, N, K, 0.5, A[off:], lda, M * lda, B[off:], ldb,
+                            N * ldb, 1.0, ref[off:], N, M * N, batch)
+    assert np.array_equal(dC.cpu().numpy(), ref)
+    Mq, Nq, Kq = 129, 130, 67
+    A2, B2, C2 = operands(rng, 0, 1, Mq, Nq, Kq)
+    hip.setNtSdot(False)
+    try:
+        got = run_dev(hip, torch_cuda, 0, 1, A2, B2, C2, 1.0, 0.0)
+    finally:
+        hip.setNtSdot(True)
+    ref = run_ref(ora, 0, 1, A2, B2, C2, 1.0, 0.0)
+    bnd = bound(0, 1, A2, B2, 1.0, 0.0, C2)
+    assert np.all(np.abs(got.astype(np.float64) - ref) <= TOL * bnd + 1e-30)
 
 
 def test_unaligned_leading_dims_and_offsets(hip, torch_cuda, ora):
@@ -154,7 +205,7 @@ def test_host_api_all_transposes(hiplib, torch_cuda, ora, ta, tb):
              A.shape[1], B.ctypes.data, B.shape[1], 2.0, C.ctypes.data, N)
     assert hiplib.tns_last_error() == b""
     ref = run_ref(ora, ta, tb, A, B, C0, 0.5, 2.0)
-    if (ta, tb) in [(0, 0), (1, 0)]:
+    if (ta, tb) in [(0, 0), (1, 0), (0, 1)]:
         assert np.array_equal(C, ref)
     else:
         bnd = bound(ta, tb, A, B, 0.5, 2.0, C0)

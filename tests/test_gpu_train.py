@@ -88,8 +88,9 @@ def test_softmax_xent_sum(hip, torch_cuda, ora):
     assert abs(float(out.item()) - ora.vssum(e)) <= 1e-5 * abs(ora.vssum(e))
 
 
-def test_backward_bias_fc_sequential(hip, torch_cuda, ora):
-    B, O = 32, 64
+@pytest.mark.parametrize("O", [64, 1])
+def test_backward_bias_fc_sequential(hip, torch_cuda, ora, O):
+    B = 32
     src = ora.uniform(B * O, 51, 0)
     dst = ora.uniform(O, 52, 0)
     ref = ora.add_sums(dst.copy(), src, B, O, 1)
@@ -147,3 +148,27 @@ def test_fused_mlp_no_bn_is_bit_exact_one_step(hip, torch_cuda, ora):
     got = dbuf.cpu().numpy()
     frac = float(np.mean(got == buf))
     assert frac == 1.0, f"{(1 - frac) * 100:.4f}% of buffer elements differ"
+
+
+@pytest.mark.parametrize("nw,n,bn,offset", [(784 * 64, 64, True, 0), (4096 * 4097, 4097, False, 0),
+                                            (1001, 7, True, 1), (0, 5, False, 0)])
+def test_sgd_update_fused(hip, torch_cuda, ora, nw, n, bn, offset):
+    """TConnectedLayer.update (nconnectedlayer.pas:324-359) fused into one
+    pass: bit-exact against the restated axpy/scale sequence (float4 and
+    scalar paths, with and without batch-norm scales)."""
+    rng = np.random.default_rng(nw + n)
+    mk = lambda k: rng.uniform(-1, 1, k + offset).astype(np.float32)  # noqa: E731
+    W, dW, b, db = mk(nw), mk(nw), mk(n), mk(n)
+    sc, dsc = (mk(n), mk(n)) if bn else (None, None)
+    lr, batch, decay, mom = 1e-3, 32, 1e-4, 0.9
+    lrb = np.float32(np.float32(lr) / np.float32(batch))
+    ndb = np.float32(-np.float32(decay) * np.float32(batch))
+    t = lambda a: None if a is None else torch_cuda.from_numpy(a.copy()).cuda()[offset:]  # noqa
+    g = [t(a) for a in (W, dW, b, db, sc, dsc)]
+    ref = [None if a is None else a[offset:].copy() for a in (W, dW, b, db, sc, dsc)]
+    ora.sgd_update(*ref, float(lrb), float(ndb), mom)
+    hip.sgdUpdate(g[0], g[1], g[2], g[3], lr, batch, decay, mom, g[4], g[5])
+    hip.finish()
+    for x, r in zip(g, ref):
+        if r is not None:
+            assert np.array_equal(x.cpu().numpy(), r)
