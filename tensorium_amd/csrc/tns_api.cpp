@@ -166,9 +166,10 @@ int check_geom(const ConvGeom& g) {
   if (g.C < 0 || g.H < 0 || g.W < 0 || g.kH <= 0 || g.kW <= 0 || g.sY <= 0 || g.sX <= 0 ||
       g.dY <= 0 || g.dX <= 0 || g.padH < 0 || g.padW < 0)
     return set_error(TNS_ERR_ARG, "im2col: invalid geometry");
-  // kernel indexing is 32-bit inside one image
-  if (g.C * g.kH * g.kW * (g.oh > 0 ? g.oh : 1) * (g.ow > 0 ? g.ow : 1) > 0x7fffffffLL ||
-      g.C * g.H * g.W > 0x7fffffffLL)
+  // kernel indexing is 32-bit inside one plane (image plane, col row) and
+  // over the col rows; offsets of planes and rows are 64-bit
+  if (g.C * g.kH * g.kW > 0x7fffffffLL || (g.oh > 0 ? g.oh : 1) * (g.ow > 0 ? g.ow : 1) >
+      0x7fffffffLL || g.H * g.W > 0x7fffffffLL)
     return set_error(TNS_ERR_ARG, "im2col: image too large for 32-bit indexing");
   return TNS_OK;
 }
@@ -760,7 +761,14 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
   // (a padded 1x1/s1 convolution is left to the reference's direct path,
   // which ignores the padding — ntensors.pas:8286)
   const bool direct_ok = needs_col || padding == 0;
-  const bool implicit = direct_ok && (fused == TNS_CONV_IMPLICIT || fused == TNS_CONV_FUSED);
+  // implicit-GEMM limits (32-bit buffer offsets within one image, k-table
+  // entries, 16-bit window offsets); the library choice falls back to the
+  // im2col schedule past them
+  const int64_t img_max = C * (H + 2 * padding) * (W + 2 * padding);
+  const bool fits = !(k > 0x0fffffffLL - KTAB_PAD || img_max * 4 > 0x7fffffffLL ||
+                      (kSize - 1) * dilation >= 0x8000);
+  const bool implicit =
+      direct_ok && (fused == TNS_CONV_IMPLICIT || (fused == TNS_CONV_FUSED && fits));
   if (implicit) {
     // implicit GEMM: batch folded into N, B gathered from zero-padded images
     if (!input || !weights || !out || !biases)
