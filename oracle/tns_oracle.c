@@ -422,7 +422,12 @@ int ora_activate(float* x, int64_t N, int32_t act) {
     case 4: /* acLINEAR: no-op */
       return 0;
     case 6: /* acTANH */
-      for (int64_t i = 0; i < N; i++) x[i] = (float)tanh((double)x[i]);
+      /* tanh_activate (351-357): px := exp(x); nx := exp(-x) as singles,
+       * then (px - nx)/(px + nx) in single (NaN once exp overflows) */
+      for (int64_t i = 0; i < N; i++) {
+        const float px = (float)exp((double)x[i]), nx = (float)exp(-(double)x[i]);
+        x[i] = (px - nx) / (px + nx);
+      }
       return 0;
     case 8:
     case 9: /* acREVLEAKY, acLEAKY: leaky_array (234-267): if 0 > x then x*0.1f */

@@ -494,7 +494,8 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
         const int64_t col = col_base + j * MF;
         if (col >= N) continue;
         float v = acc[i][j][e];
-        if (fuse) v = act_apply(v + bias, act);  // forwardBias then activate
+        // forwardBias then activate (logistic/tanh: a separate pass, host side)
+        if (fuse) v = act_apply_cheap(v + bias, act);
         C[c_at(row, col)] = v;
       }
     }

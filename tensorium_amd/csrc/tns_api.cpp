@@ -810,7 +810,8 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
       a.A = weights; a.lda = k; a.strideA = 0;
       a.B = src + b0 * img; a.ldb = outImg; a.strideB = img;
       a.C = out + b0 * outImg * filters; a.ldc = outImg; a.strideC = outImg * filters;
-      a.batch = 1; a.epi = EPI_BIAS_ACT; a.bias = biases; a.act = activation;
+      a.batch = 1; a.epi = EPI_BIAS_ACT; a.bias = biases;
+      a.act = act_transcendental(activation) ? 4 : activation;
       a.conv = padded ? 1 : 2; a.ktab = kt; a.ktab_n = (int)(k + KTAB_PAD);
       a.conv_H = (int)Hs; a.conv_W = (int)Ws; a.conv_ow = (int)ow; a.conv_ohw = (int)outImg;
       a.conv_sY = (int)stride; a.conv_sX = (int)stride;
@@ -822,6 +823,11 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
         return set_error(TNS_ERR_UNSUPPORTED, "conv variant %lld unsupported",
                          (long long)g_conv_variant);
       if (int r = hip_status(e, "implicit conv launch")) return r;
+    }
+    if (act_transcendental(activation)) {
+      OpTimer t(c, TNS_OP_ACTIVATE);
+      return hip_status(launch_activate(out, batch * filters * outImg, activation, c->stream),
+                        "activate launch");
     }
     return TNS_OK;
   }
@@ -844,9 +850,16 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
     Bp = input;
   }
   // conv GEMM with forwardBias + activate fused into the epilogue
-  return do_gemm(c, false, false, filters, outImg, k, 1.0f, weights, k, 0, Bp, outImg, strideB,
-                 0.0f, out, outImg, outImg * filters, batch, EPI_BIAS_ACT, biases, activation,
-                 true);
+  // (logistic / tanh: bias in the epilogue, activation in its own pass)
+  const bool transc = act_transcendental(activation);
+  if (int r = do_gemm(c, false, false, filters, outImg, k, 1.0f, weights, k, 0, Bp, outImg,
+                      strideB, 0.0f, out, outImg, outImg * filters, batch, EPI_BIAS_ACT, biases,
+                      transc ? 4 : activation, true))
+    return r;
+  if (!transc) return TNS_OK;
+  OpTimer t(c, TNS_OP_ACTIVATE);
+  return hip_status(launch_activate(out, batch * filters * outImg, activation, c->stream),
+                    "activate launch");
 }
 
 int tns_hip_conv_backward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,

@@ -24,6 +24,9 @@ const char* hip_err_str(hipError_t e);
 //   EPI_NONE          C = acc
 //   EPI_BIAS_ACT      C = act(acc + bias[row])   (forwardBias + activate)
 enum EpiKind { EPI_NONE = 0, EPI_BIAS_ACT = 1 };
+// logistic / tanh (exp in double) are applied after the GEMM, not in its
+// epilogue (tns_act.hpp)
+constexpr bool act_transcendental(int act) { return act == 0 || act == 6; }
 
 // beta handling, decided on the host:
 //   BETA_ZERO   acc starts at 0 (C not read)       — BLAS convention

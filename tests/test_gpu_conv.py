@@ -30,10 +30,7 @@ def conv_case(hip, torch, ora, batch, C, H, F, k, s, p, act, fused, seed=0, dil=
     (1, 4, 20, 33, 3, 2, 1, 1), (2, 3, 13, 6, 5, 1, 2, 0)])
 def test_conv_forward_small(hip, torch_cuda, ora, fused, batch, C, H, F, k, s, p, act):
     got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, fused)
-    if act == 0:
-        assert np.allclose(got, ref, rtol=1e-5, atol=1e-6)
-    else:
-        assert np.array_equal(got, ref)
+    assert np.array_equal(got, ref)
 
 
 def test_conv2d_driver_matches_oracle(hip, torch_cuda, ora):

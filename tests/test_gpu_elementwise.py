@@ -1,6 +1,9 @@
 """Bias / activation / BLAS-1 kernels vs the oracle.
-Bar: bias add, relu, leaky (x*0.1f), linear, hardtan: bit-exact;
-logistic / tanh (libm differences): |d| <= 1e-4*max(|ref|,1e-6) + 4 ulp."""
+Bar: bit-exact for every supported activation.  logistic / tanh follow the
+scalar Pascal forms with exp's real result rounded where the Pascal stores it
+(tanh: two single exps, NaN once exp overflows); the device and the oracle
+share that form, so only a last-ulp difference between the two libms' double
+exp could separate them (not seen)."""
 import numpy as np
 import pytest
 
@@ -10,24 +13,19 @@ EXACT = [1, 4, 8, 9, 13]
 TRANSC = [0, 6]
 
 
-def close_transc(got, ref):
-    ulp = np.spacing(np.abs(ref).astype(np.float32))
-    return np.all(np.abs(got - ref) <= 1e-4 * np.maximum(np.abs(ref), 1e-6) + 4 * ulp)
-
-
 @pytest.mark.parametrize("act", EXACT + TRANSC)
 @pytest.mark.parametrize("n", [1, 7, 1024, 100003])
 def test_activate(hip, torch_cuda, ora, act, n):
     x = ora.uniform(n, 8, act, -6.0, 6.0)
+    if n > 100:  # overflow / underflow / signed zero edges
+        x[:8] = np.array([-100, 100, 0.0, -0.0, 88.8, -88.8, 1e-8, -1e-30], np.float32)
     ref = ora.activate(x.copy(), act)
     dx = torch_cuda.from_numpy(x).cuda()
     hip.ActivateArray(n, dx, 0, act)
     hip.finish()
     got = dx.cpu().numpy()
-    if act in EXACT:
-        assert np.array_equal(got, ref)
-    else:
-        assert close_transc(got, ref)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)) or \
+        np.array_equal(got, ref, equal_nan=True), (act, np.abs(got - ref).max())
 
 
 @pytest.mark.parametrize("act", EXACT + TRANSC)
