@@ -205,6 +205,7 @@ _PROTO2 = {
     "ora_vssum": (f32, [i64, fp]),
     "ora_sgd_update": (None, [i64, fp, fp, i64, fp, fp, fp, fp, f32, f32, f32]),
     "ora_means_and_vars": (None, [fp, i64, i64, i64, fp, fp]),
+    "ora_means_and_vars_q": (None, [fp, i64, i64, i64, fp, fp, i32]),
     "ora_normalize": (None, [fp, i64, i64, i64, fp, fp]),
     "ora_forward_scale": (None, [fp, i64, i64, i64, fp]),
     "ora_add_dots": (None, [fp, fp, fp, i64, i64, i64]),
@@ -235,10 +236,10 @@ def vssum(a):
     return float(_lib2().ora_vssum(a.size, _p(a)))
 
 
-def means_and_vars(x, groups, N, bs):
+def means_and_vars(x, groups, N, bs, quirk=0):
     m = np.zeros(N, np.float32)
     v = np.zeros(N, np.float32)
-    _lib2().ora_means_and_vars(_p(x), groups, N, bs, _p(m), _p(v))
+    _lib2().ora_means_and_vars_q(_p(x), groups, N, bs, _p(m), _p(v), int(quirk))
     return m, v
 
 

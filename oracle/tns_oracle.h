@@ -123,6 +123,9 @@ void    ora_sgd_update(int64_t nw, float* W, float* dW, int64_t n, float* b, flo
                        float* scales, float* dscales, float lrb, float ndb, float momentum);
 void    ora_means_and_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
                            float* vars);
+void    ora_means_and_vars_q(const float* x, int64_t groups, int64_t N, int64_t bs,
+                             float* means, float* vars, int quirk);
+float   ora_srss(int64_t n, float mean, const float* a, int quirk);
 void    ora_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
                       const float* vars);
 void    ora_forward_scale(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales);

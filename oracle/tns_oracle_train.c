@@ -42,31 +42,54 @@ float ora_vssum(int64_t n, const float* a) {
 
 /* MeansAndVars: per channel i, m = sum_b sumv(bs, x_{b,i}) / (G*bs);
  * v = sum_b rss(bs, m, x_{b,i}) / (G*bs - 1)  (unbiased).  Scalar sums. */
-void ora_means_and_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
-                        float* vars) {
+/* srss (ntensors.pas:1493-1523), the stride-1 rssv of an AVX2 host
+ * (vsRSS 3646-3658): 8 lanes of (mean - a)^2 sums over the full 8-blocks;
+ * when a tail exists, lanes l and l+4 are folded and the tail added to lane
+ * 0 in order; then ((x0 + x1) + (x2 + x3)).  With no tail (N % 8 == 0) the
+ * reference skips the fold and drops lanes 4..7 — reproduced only when
+ * quirk != 0 (TNS_OPT_SRSS_QUIRK); otherwise the lanes are folded as with a
+ * tail (reference quirk 6). */
+float ora_srss(int64_t n, float mean, const float* a, int quirk) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t blocks = n >> 3;
+  for (int64_t t = 0; t < blocks; t++)
+    for (int l = 0; l < 8; l++) {
+      const float d = mean - a[8 * t + l];
+      acc[l] = acc[l] + d * d;
+    }
+  float x[4];
+  if ((n & 7) == 0 && quirk) {
+    for (int l = 0; l < 4; l++) x[l] = acc[l];
+  } else {
+    for (int l = 0; l < 4; l++) x[l] = acc[l] + acc[l + 4];
+    for (int64_t i = blocks * 8; i < n; i++) {
+      const float d = mean - a[i];
+      x[0] = x[0] + d * d;
+    }
+  }
+  return (x[0] + x[1]) + (x[2] + x[3]);
+}
+
+/* MeansAndVars (ntensors.pas:9102-9177): per channel, m := m + sumv(block)
+ * over the groups in order (sumv = vsSumI -> vssum_avx2 for stride 1),
+ * m / S; then v := v + rssv(block, m) (srss), v / S2. */
+void ora_means_and_vars_q(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
+                          float* vars, int quirk) {
   const float S = (float)(groups * bs), S2 = (float)(groups * bs - 1);
   for (int64_t i = 0; i < N; i++) {
     float m = 0.0f;
-    for (int64_t b = 0; b < groups; b++) {
-      const float* d = x + (i + b * N) * bs;
-      float s = 0.0f;
-      for (int64_t j = 0; j < bs; j++) s = s + d[j];
-      m = m + s;
-    }
+    for (int64_t b = 0; b < groups; b++) m = m + ora_vssum(bs, x + (i + b * N) * bs);
     m = m / S;
     means[i] = m;
     float v = 0.0f;
-    for (int64_t b = 0; b < groups; b++) {
-      const float* d = x + (i + b * N) * bs;
-      float r = 0.0f;
-      for (int64_t j = 0; j < bs; j++) {
-        float t = d[j] - m;
-        r = r + t * t;
-      }
-      v = v + r;
-    }
+    for (int64_t b = 0; b < groups; b++) v = v + ora_srss(bs, m, x + (i + b * N) * bs, quirk);
     vars[i] = v / S2;
   }
+}
+
+void ora_means_and_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
+                        float* vars) {
+  ora_means_and_vars_q(x, groups, N, bs, means, vars, 0);
 }
 
 /* blockNormalize: bs == 1 -> _snormvv: (x-m)/sqrt(max(v,eps));

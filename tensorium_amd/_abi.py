@@ -28,7 +28,7 @@ ACT = dict(LOGISTIC=0, RELU=1, RELU6=2, RELIE=3, LINEAR=4, RAMP=5, TANH=6, PLSE=
 TNS_OK = 0
 TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM, TNS_OP_BIAS, TNS_OP_ACTIVATE = range(5)
 TNS_OPT_STRICT_BETA0 = 0
-TNS_OPT_CONV_VARIANT, TNS_OPT_CONV_PAD, TNS_OPT_NT_SDOT = 1, 2, 3
+TNS_OPT_CONV_VARIANT, TNS_OPT_CONV_PAD, TNS_OPT_NT_SDOT, TNS_OPT_SRSS_QUIRK = 1, 2, 3, 4
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 

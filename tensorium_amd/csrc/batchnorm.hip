@@ -7,11 +7,10 @@
 // ntensors.pas:7687-7830, 8693-8718, 8821-8951, 9102-9177 and
 // nsoftmaxlayer.pas:83-137 (see oracle/tns_oracle_train.c).
 //
-// Reductions over one channel run as ONE thread walking the reference's
-// sequential order when the channel has <= kSeqMax elements (the FC layers:
-// blockSize 1, groups = batch), so sums are bit-identical; larger channels
-// (conv BN) use a fixed-order workgroup tree reduction (deterministic, within
-// the 1e-4 relative bar).  Transcendentals (exp, ln, pow) are evaluated in
+// Reductions over one channel follow the reference's order exactly: ONE
+// thread per channel when it has <= kSeqMax elements (the FC layers:
+// blockSize 1, groups = batch); larger channels (conv BN) give each block's
+// 8 AVX2 lanes to 8 GPU lanes and add the block results in order.  Transcendentals (exp, ln, pow) are evaluated in
 // double and rounded once, as the oracle does.
 #include "tns_internal.hpp"
 
@@ -27,73 +26,145 @@ inline unsigned nblk(int64_t n) {
   return (unsigned)(g < 1 ? 1 : (g > 65535 * 4 ? 65535 * 4 : g));
 }
 
-// fixed-order block reduction of one float per thread (TPB threads)
-__device__ __forceinline__ float block_sum(float v, float* sh) {
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  float r = 0.0f;
-  if (threadIdx.x == 0) r = (sh[0] + sh[1]) + (sh[2] + sh[3]);
-  __syncthreads();
-  return r;
+// ---- MeansAndVars --------------------------------------------------------
+// MeansAndVars (ntensors.pas:9102-9177) per channel: m := m + sumv(block)
+// over the groups in order, m / S; v := v + rssv(block, m), v / S2.  With
+// stride-1 blocks on an AVX2 host sumv is vssum_avx2 (3592-3620) and rssv is
+// srss (1493-1523): 8 lanes, then (for srss, when a tail exists) lanes l and
+// l+4 folded and the tail added to lane 0, then ((x0+x1)+(x2+x3)).  srss
+// without a tail drops lanes 4..7 in the reference; reproduced only under
+// TNS_OPT_SRSS_QUIRK (quirk != 0), otherwise folded as with a tail.
+__device__ __forceinline__ float vssum8(const float* a, int64_t n);  // below
+
+__device__ __forceinline__ float srss_fold(const float (&acc)[8], bool notail_quirk) {
+  float x0, x1, x2, x3;
+  if (notail_quirk) {
+    x0 = acc[0]; x1 = acc[1]; x2 = acc[2]; x3 = acc[3];
+  } else {
+    x0 = acc[0] + acc[4]; x1 = acc[1] + acc[5]; x2 = acc[2] + acc[6]; x3 = acc[3] + acc[7];
+  }
+  return (x0 + x1) + (x2 + x3);
 }
 
-// ---- MeansAndVars --------------------------------------------------------
+__device__ __forceinline__ float srss8(const float* a, int64_t n, float mean, int quirk) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t blocks = n >> 3;
+  for (int64_t t = 0; t < blocks; ++t)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const float d = mean - a[8 * t + l];
+      acc[l] = acc[l] + d * d;
+    }
+  if ((n & 7) == 0) return srss_fold(acc, quirk != 0);
+  float x0 = acc[0] + acc[4];
+  for (int64_t i = blocks * 8; i < n; ++i) {
+    const float d = mean - a[i];
+    x0 = x0 + d * d;
+  }
+  return (x0 + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7]));
+}
+
+// one thread per channel (FC layers: blockSize 1, groups = batch)
 __global__ void means_vars_seq(const float* __restrict__ x, int64_t groups, int64_t N, int64_t bs,
-                               float* __restrict__ means, float* __restrict__ vars) {
+                               float* __restrict__ means, float* __restrict__ vars, int quirk) {
   const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= N) return;
   const float S = (float)(groups * bs), S2 = (float)(groups * bs - 1);
   float m = 0.0f;
-  for (int64_t b = 0; b < groups; ++b) {
-    const float* d = x + (i + b * N) * bs;
-    float s = 0.0f;
-    for (int64_t j = 0; j < bs; ++j) s = s + d[j];
-    m = m + s;
-  }
+  for (int64_t b = 0; b < groups; ++b) m = m + vssum8(x + (i + b * N) * bs, bs);
   m = m / S;
   means[i] = m;
   float v = 0.0f;
-  for (int64_t b = 0; b < groups; ++b) {
-    const float* d = x + (i + b * N) * bs;
-    float r = 0.0f;
-    for (int64_t j = 0; j < bs; ++j) {
-      const float t = d[j] - m;
-      r = r + t * t;
-    }
-    v = v + r;
-  }
+  for (int64_t b = 0; b < groups; ++b) v = v + srss8(x + (i + b * N) * bs, bs, m, quirk);
   vars[i] = v / S2;
 }
 
-__global__ __launch_bounds__(TPB) void means_vars_blk(const float* __restrict__ x, int64_t groups,
-                                                      int64_t N, int64_t bs,
-                                                      float* __restrict__ means,
-                                                      float* __restrict__ vars) {
-  __shared__ float sh[4];
+// one workgroup per channel (conv layers): 8 consecutive lanes own a block
+// (lane l = the vssum / srss lane), block results meet in LDS and one thread
+// adds them in group order
+constexpr int MV_SLOTS = TPB / 8;
+constexpr int MV_CHUNK = 1024;
+__global__ __launch_bounds__(TPB) void means_vars_lanes(const float* __restrict__ x,
+                                                        int64_t groups, int64_t N, int64_t bs,
+                                                        float* __restrict__ means,
+                                                        float* __restrict__ vars, int quirk) {
+  __shared__ float tot[MV_CHUNK];
   __shared__ float mean_s;
   const int64_t i = blockIdx.x;
-  const int64_t per = groups * bs;
-  float s = 0.0f;
-  for (int64_t t = threadIdx.x; t < per; t += TPB) {
-    const int64_t b = t / bs, j = t - b * bs;
-    s += x[(i + b * N) * bs + j];
+  const int l = threadIdx.x & 7, q = threadIdx.x >> 3;
+  const int64_t nb = bs >> 3;
+  const bool tail = (bs & 7) != 0;
+  float m = 0.0f, v = 0.0f;
+  for (int pass = 0; pass < 2; ++pass) {
+    const float mu = pass ? mean_s : 0.0f;
+    float run = 0.0f;
+    for (int64_t j0 = 0; j0 < groups; j0 += MV_CHUNK) {
+      const int64_t jn = groups - j0 < MV_CHUNK ? groups - j0 : MV_CHUNK;
+      for (int64_t jj = q; jj < ((jn + MV_SLOTS - 1) / MV_SLOTS) * MV_SLOTS; jj += MV_SLOTS) {
+        const bool on = jj < jn;
+        const float* blk = x + ((j0 + (on ? jj : 0)) * N + i) * bs;
+        float acc = 0.0f;
+        if (on) {
+          const float* p = blk + l;
+          int64_t t = 0;
+          for (; t + 8 <= nb; t += 8) {
+            float w[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w[u] = p[8 * (t + u)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              if (pass) {
+                const float d = mu - w[u];
+                acc = acc + d * d;
+              } else {
+                acc = acc + w[u];
+              }
+            }
+          }
+          for (; t < nb; ++t) {
+            if (pass) {
+              const float d = mu - p[8 * t];
+              acc = acc + d * d;
+            } else {
+              acc = acc + p[8 * t];
+            }
+          }
+        }
+        const bool drop = pass && !tail && quirk;          // srss without a tail
+        const float up = __shfl_down(acc, 4, 8);           // lane l+4
+        float x0 = drop ? acc : acc + up;                  // lanes 0..3: x_l
+        if (pass && tail && on && l == 0)                  // srss: tail into lane 0
+          for (int64_t u = nb * 8; u < bs; ++u) {
+            const float d = mu - blk[u];
+            x0 = x0 + d * d;
+          }
+        const float h = x0 + __shfl_down(x0, 1, 8);        // x0+x1 (l=0), x2+x3 (l=2)
+        float r = h + __shfl_down(h, 2, 8);                // (x0+x1)+(x2+x3)
+        if (on && l == 0) {
+          if (!pass)                                       // vssum: tail after the fold
+            for (int64_t u = nb * 8; u < bs; ++u) r = r + blk[u];
+          tot[jj] = r;
+        }
+      }
+      __syncthreads();
+      if (threadIdx.x == 0)
+        for (int64_t jj = 0; jj < jn; ++jj) run = run + tot[jj];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      if (pass) {
+        v = run / (float)(groups * bs - 1);
+      } else {
+        m = run / (float)(groups * bs);
+        mean_s = m;
+      }
+    }
+    __syncthreads();
   }
-  s = block_sum(s, sh);
   if (threadIdx.x == 0) {
-    mean_s = s / (float)per;
-    means[i] = mean_s;
+    means[i] = m;
+    vars[i] = v;
   }
-  __syncthreads();
-  const float m = mean_s;
-  float r = 0.0f;
-  for (int64_t t = threadIdx.x; t < per; t += TPB) {
-    const int64_t b = t / bs, j = t - b * bs;
-    const float d = x[(i + b * N) * bs + j] - m;
-    r += d * d;
-  }
-  r = block_sum(r, sh);
-  if (threadIdx.x == 0) vars[i] = r / (float)(per - 1);
 }
 
 // ---- normalize / scale / bias ----------------------------------------------
@@ -268,14 +339,14 @@ __global__ void vssum_k(int64_t n, const float* __restrict__ a, float* __restric
 }  // namespace
 
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
-                             float* vars, hipStream_t s) {
+                             float* vars, int quirk, hipStream_t s) {
   if (N <= 0) return hipSuccess;
-  if (groups * bs <= kSeqMax)
+  if (bs == 1 || groups * bs <= kSeqMax)
     hipLaunchKernelGGL(means_vars_seq, dim3(nblk(N)), dim3(TPB), 0, s, x, groups, N, bs, means,
-                       vars);
+                       vars, quirk);
   else
-    hipLaunchKernelGGL(means_vars_blk, dim3((unsigned)N), dim3(TPB), 0, s, x, groups, N, bs,
-                       means, vars);
+    hipLaunchKernelGGL(means_vars_lanes, dim3((unsigned)N), dim3(TPB), 0, s, x, groups, N, bs,
+                       means, vars, quirk);
   return hipGetLastError();
 }
 

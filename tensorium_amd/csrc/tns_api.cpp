@@ -28,6 +28,7 @@ static thread_local std::string g_err;
 static tns_error_hook_t g_hook = nullptr;
 static int64_t g_strict_beta0 = 1;
 static int64_t g_nt_sdot = 1;
+static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
 static int64_t g_conv_pad = -1;
 
@@ -243,6 +244,9 @@ int tns_set_option(int32_t opt, int64_t value) {
       return TNS_OK;
     case TNS_OPT_NT_SDOT:
       g_nt_sdot = value ? 1 : 0;
+      return TNS_OK;
+    case TNS_OPT_SRSS_QUIRK:
+      g_srss_quirk = value ? 1 : 0;
       return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
@@ -550,7 +554,8 @@ int tns_hip_means_and_vars(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t
   int64_t bs;
   if (int r = blocks_of(srcSize, dstSize, groups, &bs, "meansAndVars")) return r;
   if (!src || !means || !vars) return set_error(TNS_ERR_ARG, "meansAndVars: null pointer");
-  return hip_status(launch_means_vars(src + offset, groups, dstSize, bs, means, vars, c->stream),
+  return hip_status(launch_means_vars(src + offset, groups, dstSize, bs, means, vars,
+                                      (int)g_srss_quirk, c->stream),
                     "meansAndVars");
 }
 

@@ -137,8 +137,9 @@ hipError_t launch_clamp(int64_t n, float alpha, const float* src, float* dst, in
 
 // ---- batch-norm / softmax (batchnorm.hip) ----------------------------------
 // x laid out [groups][N][bs]; one statistic per channel i in [0, N)
+// quirk != 0: srss drops lanes 4..7 of tail-less blocks, as the reference
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
-                             float* vars, hipStream_t s);
+                             float* vars, int quirk, hipStream_t s);
 hipError_t launch_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
                             int64_t mstride, const float* vars, int64_t vstride, hipStream_t s);
 hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales,

@@ -233,6 +233,11 @@ class TNNHip:
         """Implicit-GEMM gather: 1 padded copy, 0 bounds-checked, -1 by cost."""
         check(self.lib.tns_set_option(2, int(mode)))
 
+    def setSrssQuirk(self, on: bool = False):
+        """Reproduce the reference's srss lane drop in meansAndVars (blocks a
+        multiple of 8 long); process-wide."""
+        check(self.lib.tns_set_option(4, 1 if on else 0))
+
     def setNtSdot(self, on: bool = True):
         """gemm(NoTrans, Trans) in the reference's sdot order (default) or as
         one ascending-k chain per element; process-wide."""
