@@ -379,9 +379,12 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * for bit; 0 = one ascending-k chain per element (faster, within 1e-4).
  * TNS_OPT_SRSS_QUIRK (default 0): 1 reproduces the reference's srss dropping
  * lanes 4..7 of the variance sum when a block is a multiple of 8 long
- * (ntensors.pas:1493-1523, meansAndVars with blockSize % 8 == 0). */
+ * (ntensors.pas:1493-1523, meansAndVars with blockSize % 8 == 0).
+ * TNS_OPT_TT_EXACT (default 1): gemm(Trans, Trans) sums in the reference's
+ * scalar s_tt order (mul, mul, add each rounded; ntensors.pas:2159-2182) on
+ * the VALU, bit for bit; 0 = the fp32 MFMA kernel (faster, within 1e-4). */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
-       TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4 };
+       TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

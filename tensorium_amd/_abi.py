@@ -29,6 +29,7 @@ TNS_OK = 0
 TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM, TNS_OP_BIAS, TNS_OP_ACTIVATE = range(5)
 TNS_OPT_STRICT_BETA0 = 0
 TNS_OPT_CONV_VARIANT, TNS_OPT_CONV_PAD, TNS_OPT_NT_SDOT, TNS_OPT_SRSS_QUIRK = 1, 2, 3, 4
+TNS_OPT_TT_EXACT = 5
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 

@@ -14,7 +14,9 @@
 //   pre-multiplies A by alpha once (the reference's A_PART) and starts the
 //   accumulator at beta*C (the reference's mulvs pre-scale).  No split-K.
 //   NT/TT use a different order in the reference (8-lane sdot / unfused
-//   mul+add) and agree within the componentwise bound documented in DESIGN.md.
+//   mul+add): the default dispatch sends them to sgemm_sdot.hip / sgemm_tt.hip
+//   (bit-exact); through this kernel they agree within the componentwise
+//   bound documented in DESIGN.md.
 //
 // Structure (one template, several tile shapes picked per problem):
 //   block tile BM x BN, k-tile BK, WM x WN waves, each wave owning

@@ -28,6 +28,7 @@ static thread_local std::string g_err;
 static tns_error_hook_t g_hook = nullptr;
 static int64_t g_strict_beta0 = 1;
 static int64_t g_nt_sdot = 1;
+static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
 static int64_t g_conv_pad = -1;
@@ -146,6 +147,8 @@ int do_gemm(tns_ctx* c, bool ta, bool tb, int64_t M, int64_t N, int64_t K, float
   OpTimer t(c, TNS_OP_GEMM);
   if (!ta && tb && g_nt_sdot && variant < 0 && epi == EPI_NONE)
     return hip_status(launch_sgemm_nt_sdot(a, c->stream), "sgemm_nt launch");
+  if (ta && tb && g_tt_exact && variant < 0 && epi == EPI_NONE)
+    return hip_status(launch_sgemm_tt(a, c->stream), "sgemm_tt launch");
   hipError_t e = launch_sgemm_variant(variant, a, ta, tb, c->stream);
   if (e == hipErrorInvalidValue && variant >= 0)
     return set_error(TNS_ERR_UNSUPPORTED, "gemm variant %d (%s) does not support this problem",
@@ -247,6 +250,9 @@ int tns_set_option(int32_t opt, int64_t value) {
       return TNS_OK;
     case TNS_OPT_SRSS_QUIRK:
       g_srss_quirk = value ? 1 : 0;
+      return TNS_OK;
+    case TNS_OPT_TT_EXACT:
+      g_tt_exact = value ? 1 : 0;
       return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);

@@ -77,6 +77,9 @@ hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t
 // gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
 // plain epilogue only
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
+// gemm(Trans, Trans) in the reference's scalar s_tt order (sgemm_tt.hip);
+// plain epilogue only
+hipError_t launch_sgemm_tt(const GemmArgs& a, hipStream_t s);
 // implicit-GEMM convolution: NN, B generated from the image (a.conv must be set)
 hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s);
 hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s);

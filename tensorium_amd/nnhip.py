@@ -243,6 +243,11 @@ class TNNHip:
         one ascending-k chain per element; process-wide."""
         check(self.lib.tns_set_option(3, 1 if on else 0))
 
+    def setTtExact(self, on: bool = True):
+        """gemm(Trans, Trans) in the reference's scalar s_tt order on the VALU
+        (default) or on the fp32 MFMA kernel; process-wide."""
+        check(self.lib.tns_set_option(5, 1 if on else 0))
+
     # -- batch norm / softmax (TNNCuda.meansAndVars ... crossEntropySoftmax) ----
     def meansAndVars(self, srcSize, dstSize, groups, src, offset, means, vars_):
         check(self.lib.tns_hip_means_and_vars(self.ctx, srcSize, dstSize, groups, _ptr(src),

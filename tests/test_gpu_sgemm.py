@@ -7,8 +7,10 @@ Bar:
   * NT: bit-identical to the reference's sdot_avx2 order (8 residue chains
     k mod 8, pairwise lane sum, alpha product, C add; sgemm_sdot.hip);
     with TNS_OPT_NT_SDOT = 0, within the componentwise bound below.
-  * TT: componentwise |C - C_ref| <= 1e-4 * (|alpha||A||B| + |beta||C0|)_ij
-    (the reference's scalar TT rounds mul and add separately).
+  * TT: bit-identical to the reference's scalar s_tt (alpha*A, *B, + sum,
+    each rounded; sgemm_tt.hip on the VALU); with TNS_OPT_TT_EXACT = 0 (the
+    MFMA kernel) componentwise |C - C_ref| <= 1e-4 * (|alpha||A||B| +
+    |beta||C0|)_ij.
 """
 import numpy as np
 import pytest
@@ -127,6 +129,49 @@ def test_nt_sdot_batched_offsets_and_plain_order(hip, torch_cuda, ora):
     assert np.all(np.abs(got.astype(np.float64) - ref) <= TOL * bnd + 1e-30)
 
 
+@pytest.mark.parametrize("M,N,K", SHAPES + [(2945, 2945, 37)])
+def test_tt_bit_exact(hip, torch_cuda, ora, M, N, K):
+    """gemm(Trans, Trans) = s_tt (ntensors.pas:2159-2182): both tile sizes
+    (2945^2 takes the 128x128 tiles), every K mod 16 tail, K = 0."""
+    rng = np.random.default_rng(M * 5 + N * 13 + K + 3)
+    A, B, C0 = operands(rng, 1, 1, M, N, K)
+    for alpha, beta in [(1.0, 0.0), (0.5, 2.0), (1.0, 1.0), (-1.5, 0.25)]:
+        got = run_dev(hip, torch_cuda, 1, 1, A, B, C0, alpha, beta)
+        ref = run_ref(ora, 1, 1, A, B, C0, alpha, beta)
+        assert np.array_equal(got, ref), (M, N, K, alpha, beta,
+                                          float(np.abs(got - ref).max()))
+        if M * N * K > 1e8:
+            break
+
+
+def test_tt_batched_offsets_and_mfma_option(hip, torch_cuda, ora):
+    """Strided-batched TT with element offsets and padded leading dims; then
+    the MFMA kernel (TNS_OPT_TT_EXACT = 0) within bound."""
+    rng = np.random.default_rng(21)
+    batch, M, N, K, lda, ldb, off = 3, 45, 70, 37, 49, 39, 5
+    A = rng.uniform(-1, 1, off + batch * K * lda).astype(np.float32)
+    B = rng.uniform(-1, 1, off + batch * N * ldb).astype(np.float32)
+    C = rng.uniform(-1, 1, off + batch * M * N).astype(np.float32)
+    dA, dB, dC = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B, C))
+    hip.gemmStridedBatched(True, True, M, N, K, 0.5, dA, off, lda, K * lda, dB, off, ldb,
+                           N * ldb, 2.0, dC, off, N, M * N, batch)
+    hip.finish()
+    ref = C.copy()
+    ora.sgemm_batch_strided(True, True, M, N, K, 0.5, A[off:], lda, K * lda, B[off:], ldb,
+                            N * ldb, 2.0, ref[off:], N, M * N, batch)
+    assert np.array_equal(dC.cpu().numpy(), ref)
+    A2, B2, C2 = operands(rng, 1, 1, 129, 130, 67)
+    hip.setTtExact(False)
+    try:
+        got = run_dev(hip, torch_cuda, 1, 1, A2, B2, C2, 1.0, 0.0)
+    finally:
+        hip.setTtExact(True)
+    ref = run_ref(ora, 1, 1, A2, B2, C2, 1.0, 0.0)
+    assert not np.array_equal(got, ref)  # the MFMA kernel fuses: a different rounding
+    bnd = bound(1, 1, A2, B2, 1.0, 0.0, C2)
+    assert np.all(np.abs(got.astype(np.float64) - ref) <= TOL * bnd + 1e-30)
+
+
 def test_unaligned_leading_dims_and_offsets(hip, torch_cuda, ora):
     # lda/ldb/ldc larger than the logical width, element offsets into buffers
     rng = np.random.default_rng(1)
@@ -205,11 +250,7 @@ def test_host_api_all_transposes(hiplib, torch_cuda, ora, ta, tb):
              A.shape[1], B.ctypes.data, B.shape[1], 2.0, C.ctypes.data, N)
     assert hiplib.tns_last_error() == b""
     ref = run_ref(ora, ta, tb, A, B, C0, 0.5, 2.0)
-    if (ta, tb) in [(0, 0), (1, 0), (0, 1)]:
-        assert np.array_equal(C, ref)
-    else:
-        bnd = bound(ta, tb, A, B, 0.5, 2.0, C0)
-        assert np.all(np.abs(C.astype(np.float64) - ref) <= TOL * bnd)
+    assert np.array_equal(C, ref)
 
 
 def test_4096_cubed_sampled_rows_bit_exact(hip, torch_cuda, ora):
