@@ -45,8 +45,10 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=30,
+                    help="untimed steps; the GPU clock ramps over the first ~20 launches "
+                         "(profiles/r01_clock_ramp.json)")
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--yolo-steps", type=int, default=5)
     ap.add_argument("--no-yolo", action="store_true")
