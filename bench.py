@@ -127,20 +127,36 @@ def bench_yolo(torch, hip, ctx, rank, steps, warmup=1):
     torch.cuda.synchronize()
     ctx.barrier()
     wall = (time.perf_counter() - t0) / steps
-    # per-op split with telemetry (synchronous per op, separate pass)
+    # per-op split with telemetry (synchronous per op, separate passes):
+    # the fused schedule (implicit GEMM; its only other op is the zero-border
+    # copy of padded images), then the reference's three stages (im2col,
+    # GEMM, bias+activation) for the elementwise kernels' HBM rates
+    from tensorium_amd._abi import TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_BIAS
     hip.setTelemetry(True)
     step()
-    from tensorium_amd._abi import TNS_OP_GEMM, TNS_OP_IM2COL
-    gemm_ms, i2c_ms = hip.opMs(TNS_OP_GEMM), hip.opMs(TNS_OP_IM2COL)
+    gemm_ms, pad_ms = hip.opMs(TNS_OP_GEMM), hip.opMs(TNS_OP_IM2COL)
+    hip.setTelemetry(False)
+    hip.setTelemetry(True)
+    for s, x, w, b, out in layers:
+        hip.convForward(batch, s.c, s.h, s.h, x, w, b, s.filters, s.size, s.stride, s.pad, 1,
+                        s.activation, ws, out, fused=False)
+    i2c_ms, bias_ms = hip.opMs(TNS_OP_IM2COL), hip.opMs(TNS_OP_BIAS)
     hip.setTelemetry(False)
     gflop = sum(s.flops for s in specs) * batch / 1e9
+    # im2col: writes the col matrix, reads the image (layers that need one)
     col_bytes = sum(s.col_elems for s in specs) * batch * 4
     in_bytes = sum(s.c * s.h * s.h for s in specs if s.needs_im2col) * batch * 4
+    # bias+activation: reads and writes every output element
+    out_bytes = sum(2 * s.filters * s.out_h * s.out_h for s in specs) * batch * 4
     return {
         "batch_per_gpu": batch, "ms_per_batch": wall * 1e3, "gflop_per_batch": gflop,
-        "gemm_ms": gemm_ms, "im2col_ms": i2c_ms,
+        "gemm_ms": gemm_ms, "pad_copy_ms": pad_ms,
         "gemm_tflops": gflop / gemm_ms if gemm_ms > 0 else None,
+        "unfused_im2col_ms": i2c_ms,
         "im2col_gbs": (col_bytes + in_bytes) / (i2c_ms * 1e6) if i2c_ms > 0 else None,
+        "unfused_bias_act_ms": bias_ms,
+        "bias_act_gbs": out_bytes / (bias_ms * 1e6) if bias_ms > 0 else None,
+        "hbm_peak_gbs": 8000.0,
     }
 
 
@@ -194,6 +210,32 @@ def bench_batched(torch, hip, ctx, n_gemm=1024, n=1024, steps=3):
     return {"gemms_total": n_gemm, "gemm_size": n, "gemms_per_rank_max": -(-n_gemm // ctx.world),
             "ms_per_batch": round(wall * 1e3, 4), "tflops_total": round(flop / wall / 1e12, 3),
             "scaling": "strong (fixed 1024 GEMMs split over ranks)"}
+
+
+def bench_host_api(n, steps=3):
+    """Boundary A (host pointers, the reference's `gemm` op-table slot):
+    tns_cblas_sgemm on pageable numpy arrays, i.e. H2D of A and B, the kernel
+    and D2H of C inside each call (beta = 0 skips the C upload).  Reported as
+    the PCIe-inclusive rate beside `value`, never as `value`."""
+    from tensorium_amd.ntensors import bind_hip_op_table
+    ops = bind_hip_op_table()
+    rng = np.random.default_rng(6)
+    A = rng.uniform(-1, 1, (n, n)).astype(np.float32)
+    B = rng.uniform(-1, 1, (n, n)).astype(np.float32)
+    C = np.zeros((n, n), np.float32)
+
+    def call():
+        ops.gemm(101, 111, 111, n, n, n, 1.0, A.ctypes.data, n, B.ctypes.data, n, 0.0,
+                 C.ctypes.data, n)
+
+    call()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        call()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    return {"entry": "tns_cblas_sgemm (host pointers, pageable)", "ms_per_call": round(ms, 3),
+            "gflops_pcie_inclusive": round(2.0 * n ** 3 / ms / 1e6, 1),
+            "bytes_moved_per_call": 3 * n * n * 4}
 
 
 def bench_mnist(torch, hip, ctx, steps=200):
@@ -348,6 +390,7 @@ def main():
         yolo_net = bench_yolo_network(torch, hip, ctx, args.yolo_steps)
     batched = None if args.no_batched else bench_batched(torch, hip, ctx)
     mnist = None if args.no_mnist else bench_mnist(torch, hip, ctx)
+    host_api = bench_host_api(n) if rank == 0 and world == 1 and not args.no_cpu else None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -385,6 +428,7 @@ def main():
             "yolo_network": yolo_net,
             "batched_gemm": batched,
             "mnist_train": mnist,
+            "host_api": host_api,
         }
         print(json.dumps(line), flush=True)
     hip.finish()

@@ -3,10 +3,13 @@
 // im2col restates sim2Col (ntensors.pas:11415-11491) and its batched form
 // (11493-11532): col[((c*kH+kr)*kW+kc)*oh*ow + orow*ow + ocol] =
 //   im[c][-padH + kr*dY + orow*sY][-padW + kc*dX + ocol*sX], 0 outside.
-// Pure copies => bit-exact.  Output-stationary: each thread writes 4
-// consecutive col elements with one 16-byte store when oh*ow % 4 == 0
-// (HBM-write bound; the gathered reads hit L2 — each input pixel is read
-// kH*kW times).
+// Pure copies => bit-exact.  Main form (im2col_rows_kernel): a block stages
+// the input rows of one (image, channel, kernel row, chunk of output rows) in
+// LDS and writes the kW col rows of that chunk from there, 16-byte stores
+// contiguous across the wave (nontemporal for col matrices far larger than
+// the caches).  HBM-write bound.  The output-stationary gather kernel (each
+// thread 4 consecutive col elements, scalar gathers through L2) remains for
+// rows too wide for LDS.
 //
 // col2im restates c2i/scol2im (ntensors.pas:11650-11763) as a race-free
 // GATHER: one thread per image pixel sums, in ascending kernel index order
@@ -15,6 +18,8 @@
 // value (the reference accumulates and never zeroes im).  Same float adds in
 // the same order => bit-exact.  The reference's col2im dilation formula,
 // input_row := (kernel_row - pad) * dil  (11693, 11700), is kept.
+#include <algorithm>
+
 #include "tns_internal.hpp"
 
 namespace tns {
@@ -132,6 +137,95 @@ __global__ __launch_bounds__(256) void im2col_kernel(I2CArgs a) {
   }
 }
 
+// Row-staged im2col: a block owns (image, channel c, kernel row kr) and a
+// chunk of R output rows.  It copies the R input rows that chunk reads
+// (ir = -padH + kr*dY + orow*sY), zero-padded to Wp = W + 2*padW columns,
+// into LDS once with coalesced loads, then writes the kW col rows (c, kr, kc)
+// of the chunk — each a contiguous run of R*ow elements — from LDS.  Every
+// input element is fetched from memory once per kernel row instead of once
+// per (kr, kc) by scattered scalar loads.  Same values as the plain kernel.
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct I2CRowArgs {
+  I2CArgs g;
+  int R;       // output rows per block
+  int chunks;  // ceil(oh / R)
+  int Wp;      // staged row length (covers every window column)
+};
+
+template <int VEC, bool NT>
+__global__ __launch_bounds__(256) void im2col_rows_kernel(I2CRowArgs ra) {
+  extern __shared__ float rows[];
+  const I2CArgs& a = ra.g;
+  const int chunk = blockIdx.x % ra.chunks;
+  const int64_t t = blockIdx.x / ra.chunks;  // (image, c, kr)
+  const int kr = (int)(t % a.kH);
+  const int64_t t2 = t / a.kH;
+  const int c = (int)(t2 % a.C);
+  const int64_t img = t2 / a.C;
+  const int orow0 = chunk * ra.R;
+  const int nr = min(ra.R, a.oh - orow0);
+  const float* __restrict__ im = a.im + img * a.imStride + (int64_t)c * a.H * a.W;
+  const int Wp = ra.Wp;
+  for (int i = threadIdx.x; i < nr * Wp; i += 256) {
+    const int r = i / Wp, x = i - r * Wp;
+    const int ir = -a.padH + kr * a.dY + (orow0 + r) * a.sY, ic = x - a.padW;
+    rows[i] = ((unsigned)ir < (unsigned)a.H && (unsigned)ic < (unsigned)a.W) ? im[ir * a.W + ic]
+                                                                            : 0.0f;
+  }
+  __syncthreads();
+  const int ohw = a.oh * a.ow, n = nr * a.ow;
+  for (int kc = 0; kc < a.kW; ++kc) {
+    const int row = (c * a.kH + kr) * a.kW + kc;
+    float* __restrict__ col = a.col + img * a.colStride + (int64_t)row * ohw + orow0 * a.ow;
+    const int cx = kc * a.dX;
+    if constexpr (VEC == 4) {
+      // quads 256 apart per thread (each store instruction of a wave writes
+      // 1 KB contiguous), four per pass: all LDS reads, then four stores
+      constexpr int IT = 4;
+      const int nq = n >> 2;
+      const int dr = 1024 / a.ow, dc = 1024 - dr * a.ow;  // advance by 256 quads
+      for (int q0 = threadIdx.x; q0 < nq; q0 += 256 * IT) {
+        int r = (4 * q0) / a.ow;
+        int oc0 = 4 * q0 - r * a.ow;
+        floatx4 v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+          int rr = r, oc = oc0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[it][e] = (q0 + 256 * it < nq) ? rows[rr * Wp + cx + oc * a.sX] : 0.0f;
+            if (++oc == a.ow) {
+              oc = 0;
+              ++rr;
+            }
+          }
+          r += dr;
+          oc0 += dc;
+          if (oc0 >= a.ow) {
+            oc0 -= a.ow;
+            ++r;
+          }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+          if (q0 + 256 * it < nq) {
+            floatx4* dst = reinterpret_cast<floatx4*>(col + 4 * (q0 + 256 * it));
+            if constexpr (NT)
+              __builtin_nontemporal_store(v[it], dst);
+            else
+              *dst = v[it];
+          }
+      }
+    } else {
+      for (int p0 = threadIdx.x; p0 < n; p0 += 256) {
+        const int r = p0 / a.ow, oc = p0 - r * a.ow;
+        col[p0] = rows[r * Wp + cx + oc * a.sX];
+      }
+    }
+  }
+}
+
 struct C2IArgs {
   int C, H, W, kH, kW, padH, padW, sY, sX, dY, dX, oh, ow;
   const float* col;
@@ -186,6 +280,43 @@ hipError_t launch_im2col(const ConvGeom& g, const float* im, int64_t imStride, f
                    (colStride % 4 == 0 || batch == 1);
   const int VEC = vec ? 4 : 1;
   a.quads = (int)((ohw + VEC - 1) / VEC);
+  // row-staged form: ~4096 (float4 form) or ~2048 col elements per kernel
+  // column per block, chunks
+  // of a multiple of 4 rows (aligned float4 runs) or the whole plane
+  {
+    // staged row: every window column (kc*dX + ocol*sX, zero outside the
+    // image) — W + 2*padW, or more when out_dim's truncation toward zero
+    // admits a window that overhangs the padded row
+    const int64_t Wp = std::max<int64_t>(g.W + 2 * g.padW,
+                                         (g.kW - 1) * g.dX + (g.ow - 1) * g.sX + 1);
+    int64_t R = std::max<int64_t>(1, (vec ? 4096 : 2048) / g.ow);
+    if (R >= g.oh)
+      R = g.oh;
+    else if (vec)
+      R = std::max<int64_t>(4, R & ~int64_t(3));
+    const int64_t chunks = (g.oh + R - 1) / R;
+    const int64_t blocks = batch * g.C * g.kH * chunks;
+    // the staged rows must fit LDS
+    if (R * Wp * 4 <= 64 * 1024 && blocks <= 0x7fffffffLL) {
+      I2CRowArgs ra;
+      ra.g = a;
+      ra.R = (int)R;
+      ra.chunks = (int)chunks;
+      ra.Wp = (int)Wp;
+      const size_t lds = (size_t)(R * Wp * 4);
+      // col matrices far larger than the caches stream past them
+      // (nontemporal stores: 4.7-5.3 TB/s against 3.6-4.9 TB/s on the
+      // large YOLOv3 layers); smaller ones stay cacheable for the GEMM
+      const bool nt = batch * (int64_t)a.rows * ohw * 4 >= (int64_t)128 << 20;
+      if (vec && nt)
+        hipLaunchKernelGGL((im2col_rows_kernel<4, true>), dim3((unsigned)blocks), dim3(256), lds, s, ra);
+      else if (vec)
+        hipLaunchKernelGGL((im2col_rows_kernel<4, false>), dim3((unsigned)blocks), dim3(256), lds, s, ra);
+      else
+        hipLaunchKernelGGL((im2col_rows_kernel<1, false>), dim3((unsigned)blocks), dim3(256), lds, s, ra);
+      return hipGetLastError();
+    }
+  }
   const int64_t ylim = 65535;
   const int64_t rows_total = (int64_t)a.rows * batch;
   // y = image*rows + row; split the batch so y fits the grid limit
