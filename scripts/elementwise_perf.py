@@ -25,7 +25,8 @@ def main():
     batch = 8
     specs = yolov3_conv_table()
     rows = []
-    tot = {"im2col": [0.0, 0.0], "bias": [0.0, 0.0], "leaky": [0.0, 0.0]}
+    tot = {"im2col": [0.0, 0.0], "col2im": [0.0, 0.0], "bias": [0.0, 0.0],
+           "leaky": [0.0, 0.0]}
     col = torch.empty(max(s.col_elems for s in specs) * batch, device="cuda")
     for s in specs:
         x = torch.rand(batch * s.c * s.h * s.h, device="cuda")
@@ -40,6 +41,14 @@ def main():
             row["im2col_gbs"] = round(by / ms / 1e6, 1)
             tot["im2col"][0] += by
             tot["im2col"][1] += ms
+            # col2im: reads the col matrix, reads and writes the image
+            ms = timed(lambda: hip.col2imStridedBatched(
+                s.c, s.h, s.h, s.size, s.size, s.pad, s.pad, s.stride, s.stride, 1, 1, col,
+                s.col_elems, 0, x, s.c * s.h * s.h, 0, batch), 10)
+            by = (s.col_elems + 2 * s.c * s.h * s.h) * batch * 4
+            row["col2im_gbs"] = round(by / ms / 1e6, 1)
+            tot["col2im"][0] += by
+            tot["col2im"][1] += ms
         by = 2 * out.numel() * 4
         ms = timed(lambda: hip.forwardBias(out.numel(), out, 0, s.filters, b, 1, batch), 10)
         row["bias_gbs"] = round(by / ms / 1e6, 1)
