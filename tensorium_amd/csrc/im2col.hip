@@ -239,13 +239,29 @@ __global__ __launch_bounds__(256) void col2im_kernel(C2IArgs a) {
   const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (pix >= a.pixels) return;
   const int64_t img = blockIdx.y;
-  const int x = (int)(pix % a.W);
+  // within an image row, lanes take the columns of one residue class
+  // x = k (mod sX) together (k-major order): the same kernel columns hit
+  // them all and their col reads are consecutive, instead of sX-1 of sX lanes
+  // idling per tap.  Per pixel nothing changes.
+  const int q = (int)(pix % a.W);
+  int x = q;
+  if (a.sX > 1) {
+    int k = 0, base = 0;
+    while (k < a.sX - 1) {
+      const int wk = (a.W - k + a.sX - 1) / a.sX;
+      if (q < base + wk) break;
+      base += wk;
+      ++k;
+    }
+    x = k + (q - base) * a.sX;
+  }
   const int y = (int)((pix / a.W) % a.H);
   const int c = (int)(pix / ((int64_t)a.W * a.H));
   float* __restrict__ im = a.im + img * a.imStride;
   const float* __restrict__ col = a.col + img * a.colStride;
   const int64_t ohw = (int64_t)a.oh * a.ow;
-  float acc = im[pix];
+  const int64_t at = pix - q + x;
+  float acc = im[at];
   for (int kr = 0; kr < a.kH; ++kr) {
     // rows: y = (kr - padH)*dY + orow*sY
     const int ry = y - (kr - a.padH) * a.dY;
@@ -261,7 +277,53 @@ __global__ __launch_bounds__(256) void col2im_kernel(C2IArgs a) {
       acc = acc + col[i * ohw + (int64_t)orow * a.ow + ocol];
     }
   }
-  im[pix] = acc;
+  im[at] = acc;
+}
+
+// col2im_kernel with 32-bit pixel indexing (C*H*W < 2^31) and the stride
+// as a template constant (S = sY = sX = 1 or 2; 0 = runtime): the per-tap
+// divisibility tests and quotients become masks and shifts instead of
+// integer divisions, which bound the general kernel.  Same adds, same order.
+template <int S>
+__global__ __launch_bounds__(256) void col2im_fast_kernel(C2IArgs a) {
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (int)a.pixels) return;
+  const int64_t img = blockIdx.y;
+  const int sY = S ? S : a.sY, sX = S ? S : a.sX;
+  const int rowi = pix / a.W;  // c*H + y
+  const int q = pix - rowi * a.W;
+  int x = q;
+  if (sX > 1) {  // residue-class order, as col2im_kernel
+    int k = 0, base = 0;
+    while (k < sX - 1) {
+      const int wk = (a.W - k + sX - 1) / sX;
+      if (q < base + wk) break;
+      base += wk;
+      ++k;
+    }
+    x = k + (q - base) * sX;
+  }
+  const int c = rowi / a.H, y = rowi - c * a.H;
+  float* __restrict__ im = a.im + img * a.imStride;
+  const float* __restrict__ col = a.col + img * a.colStride;
+  const int ohw = a.oh * a.ow;
+  const int at = pix - q + x;
+  float acc = im[at];
+  for (int kr = 0; kr < a.kH; ++kr) {
+    const int ry = y - (kr - a.padH) * a.dY;
+    if (ry < 0 || ry % sY != 0) continue;
+    const int orow = ry / sY;
+    if (orow >= a.oh) continue;
+    const float* __restrict__ crow = col + ((int64_t)(c * a.kH + kr) * a.kW) * ohw + orow * a.ow;
+    for (int kc = 0; kc < a.kW; ++kc) {
+      const int rx = x - (kc - a.padW) * a.dX;
+      if (rx < 0 || rx % sX != 0) continue;
+      const int ocol = rx / sX;
+      if (ocol >= a.ow) continue;
+      acc = acc + crow[(int64_t)kc * ohw + ocol];
+    }
+  }
+  im[at] = acc;
 }
 
 }  // namespace
@@ -353,7 +415,16 @@ hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride,
     sub.col = col + b0 * colStride;
     sub.im = im + b0 * imStride;
     dim3 grid((unsigned)((a.pixels + 255) / 256), (unsigned)nb);
-    hipLaunchKernelGGL(col2im_kernel, grid, dim3(256), 0, s, sub);
+    if (a.pixels <= 0x7fffff00LL) {
+      if (g.sY == 1 && g.sX == 1)
+        hipLaunchKernelGGL(col2im_fast_kernel<1>, grid, dim3(256), 0, s, sub);
+      else if (g.sY == 2 && g.sX == 2)
+        hipLaunchKernelGGL(col2im_fast_kernel<2>, grid, dim3(256), 0, s, sub);
+      else
+        hipLaunchKernelGGL(col2im_fast_kernel<0>, grid, dim3(256), 0, s, sub);
+    } else {
+      hipLaunchKernelGGL(col2im_kernel, grid, dim3(256), 0, s, sub);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
