@@ -157,6 +157,9 @@ def bench_yolo(torch, hip, ctx, rank, steps, warmup=1):
         "unfused_bias_act_ms": bias_ms,
         "bias_act_gbs": out_bytes / (bias_ms * 1e6) if bias_ms > 0 else None,
         "hbm_peak_gbs": 8000.0,
+        "rates_note": "unfused rates from per-op synchronous telemetry over all 75 layers "
+                      "(launch/sync gaps included; the 13x13 layers are ~20 us launches); "
+                      "per-kernel rates: scripts/elementwise_perf.py",
     }
 
 

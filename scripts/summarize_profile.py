@@ -37,6 +37,7 @@ def main():
     src = Path(sys.argv[1])
     tag = sys.argv[2]
     size = int(sys.argv[sys.argv.index("--size") + 1]) if "--size" in sys.argv else 4096
+    timed = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 50
     prof = ROOT / "profiles"
     prof.mkdir(exist_ok=True)
     stats = src / "trace" / "trace_kernel_stats.csv"
@@ -68,6 +69,11 @@ def main():
         "tag": tag, "size": size, "kernel": "sgemm_mfma_kernel<Shape<256,256,32,2,4,2>, NN, 4, 4>",
         "launches_traced": len(durs),
         "kernel_ms_mean": round(st.mean(durs), 4), "kernel_ms_min": round(min(durs), 4),
+        # bench.py's timed launches are the last --steps of the warm-up+steps
+        # sequence; the first ones ride the GPU clock ramp
+        "kernel_ms_mean_timed_launches": round(st.mean(durs[-timed:]), 4) if len(durs) > timed
+        else None,
+        "timed_launches": timed,
         "tflops_mean": round(flop / (st.mean(durs) * 1e-3) / 1e12, 2),
         "fetch_size_kb_raw": round(fk, 1), "write_size_kb": round(wk, 1),
         "bytes_per_launch": round(traffic), "algorithmic_bytes": alg,
