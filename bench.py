@@ -163,6 +163,61 @@ def bench_yolo(torch, hip, ctx, rank, steps, warmup=1):
     }
 
 
+def bench_conv_backward(torch, hip, ctx, rank, steps=2):
+    """Row f-2: TConvolutionalLayer.backward over the 75 YOLOv3-416 conv
+    layers at batch 8 (tns_hip_conv_backward: derive, addSums, im2col,
+    per-image NT dW in the sdot order, TN dX + col2im), synthetic delta.
+    Work = dW + dX GEMMs = 2x the forward FLOPs (the first layer's dX is
+    computed too)."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    specs = yolov3_conv_table()
+    batch = 8
+    layers = []
+    max_ws = 0
+    for s in specs:
+        g = 5 * 100000 + rank * 1000 + s.index
+        x = synthetic(torch, (batch, s.c, s.h, s.h), g, 0.0, 1.0)
+        sc = float(np.sqrt(2.0 / (s.size * s.size * s.c)))
+        w = synthetic(torch, (s.filters, s.K), g + 1, -sc, sc)
+        out = synthetic(torch, (batch, s.filters, s.out_h, s.out_h), g + 2, -1.0, 1.0)
+        delta = synthetic(torch, (batch, s.filters, s.out_h, s.out_h), g + 3, -1.0, 1.0)
+        bu = torch.zeros(s.filters, device="cuda")
+        wu = torch.zeros((s.filters, s.K), device="cuda")
+        sd = torch.zeros((batch, s.c, s.h, s.h), device="cuda")
+        layers.append((s, x, w, out, delta, bu, wu, sd))
+        max_ws = max(max_ws, batch * s.K * s.out_h * s.out_h)
+    ws = torch.empty(max(max_ws, 1), device="cuda")
+
+    def step():
+        for s, x, w, out, delta, bu, wu, sd in layers:
+            hip.convBackward(batch, s.c, s.h, s.h, x, w, s.filters, s.size, s.stride, s.pad, 1,
+                             s.activation, out, delta, bu, wu, ws, sd)
+
+    step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    wall = ctx.max((time.perf_counter() - t0) / steps)
+    from tensorium_amd._abi import TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM
+    hip.setTelemetry(True)
+    step()
+    split = {"gemm_ms": round(hip.opMs(TNS_OP_GEMM), 3),
+             "im2col_ms": round(hip.opMs(TNS_OP_IM2COL), 3),
+             "col2im_ms": round(hip.opMs(TNS_OP_COL2IM), 3)}
+    hip.setTelemetry(False)
+    gflop = 2 * sum(s.flops for s in specs) * batch / 1e9
+    del layers, ws
+    torch.cuda.empty_cache()
+    return {"layers": len(specs), "batch_per_gpu": batch, "ms_per_batch": round(wall * 1e3, 3),
+            "gflop_per_batch": round(gflop, 2), "tflops": round(gflop / wall / 1e3, 2),
+            "images_per_s_total": round(ctx.world * batch / wall, 1),
+            "telemetry_split": split}
+
+
 def bench_yolo_network(torch, hip, ctx, steps):
     """The whole YOLOv3-416 network (yolov3.cfg plan: 75 convolutions chained
     through shortcut / route / upsample / yolo, darknet.HipDarknet), batch 8
@@ -391,6 +446,9 @@ def main():
     yolo_net = None
     if not args.no_yolo and args.yolo_steps > 0:
         yolo_net = bench_yolo_network(torch, hip, ctx, args.yolo_steps)
+    conv_bwd = None
+    if not args.no_yolo and args.yolo_steps > 0:
+        conv_bwd = bench_conv_backward(torch, hip, ctx, rank)
     batched = None if args.no_batched else bench_batched(torch, hip, ctx)
     mnist = None if args.no_mnist else bench_mnist(torch, hip, ctx)
     host_api = bench_host_api(n) if rank == 0 and world == 1 and not args.no_cpu else None
@@ -429,6 +487,7 @@ def main():
             "cpu_baseline": cpu,
             "yolo": yolo,
             "yolo_network": yolo_net,
+            "yolo_conv_backward": conv_bwd,
             "batched_gemm": batched,
             "mnist_train": mnist,
             "host_api": host_api,

@@ -407,6 +407,26 @@ hipError_t launch_scale(int64_t n, float a, float* x, int64_t stride, hipStream_
   return hipGetLastError();
 }
 
+namespace {
+__global__ __launch_bounds__(TPB) void add_in_order_kernel(float* __restrict__ C,
+                                                           const float* __restrict__ part,
+                                                           int64_t n, int64_t batch) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * TPB) {
+    float acc = C[i];
+    for (int64_t b = 0; b < batch; ++b) acc = acc + part[b * n + i];
+    C[i] = acc;
+  }
+}
+}  // namespace
+
+hipError_t launch_add_in_order(float* C, const float* part, int64_t n, int64_t batch,
+                               hipStream_t s) {
+  if (n <= 0 || batch <= 0) return hipSuccess;
+  hipLaunchKernelGGL(add_in_order_kernel, dim3(grid_for(n)), dim3(TPB), 0, s, C, part, n, batch);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill(int64_t n, float* x, float v, int64_t stride, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(TPB), 0, s, n, x, v, stride);

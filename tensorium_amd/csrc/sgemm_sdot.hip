@@ -135,6 +135,10 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
     const float dot = (s0 + s1) + (s2 + s3);
     const float sum = alpha * dot;  // sum := ALPHA * sdot(...)
     float* cp = C + m * p.ldc + n;
+    if (p.beta_mode == BETA_STORE) {
+      *cp = sum;
+      continue;
+    }
     float c0;
     if (p.beta_mode == BETA_ZERO)
       c0 = 0.0f;

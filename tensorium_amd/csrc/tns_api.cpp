@@ -55,8 +55,10 @@ struct tns_ctx {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   // device scratch (im2col workspace, host-API staging)
-  float* scratch[4] = {nullptr, nullptr, nullptr, nullptr};
-  size_t scratch_elems[4] = {0, 0, 0, 0};
+  // 0 col workspace, 1 padded images / host staging, 2-3 host staging,
+  // 4 per-image dW partial sums of the conv backward
+  float* scratch[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  size_t scratch_elems[5] = {0, 0, 0, 0, 0};
   // telemetry (TTensorMetrics-style, nopmetrics.pas:25-44)
   bool telemetry = false;
   double op_ms[TNS_OP_COUNT] = {0};
@@ -288,7 +290,7 @@ int tns_hip_destroy(tns_ctx* c) {
   if (!c) return TNS_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 5; ++i)
     if (c->scratch[i]) hipFree(c->scratch[i]);
   for (auto& kv : c->ktabs) hipFree(kv.second);
   if (c->ev0) hipEventDestroy(c->ev0);
@@ -917,12 +919,36 @@ int tns_hip_conv_backward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64
     col = ws;
   }
   // weight_updates += delta_b . col_b^T, one NT GEMM per image (beta = 1),
-  // in image order as the reference loop (nConvolutionLayer.pas:636-640)
-  for (int64_t b = 0; b < batch; ++b)
-    if (int r = do_gemm(c, false, true, i_m, i_n, i_k, 1.0f, delta + b * i_m * i_k, i_k, 0,
-                        col + b * colSize, i_k, 0, 1.0f, weight_updates, i_n, 0, 1, EPI_NONE,
-                        nullptr, 0))
+  // in image order as the reference loop (nConvolutionLayer.pas:636-640):
+  // each image adds sum_b = 1*sdot(...) to C.  The sums of different images
+  // are independent, so they are computed by ONE strided-batched sdot launch
+  // (each stored as is, BETA_STORE), then added to C image by image in the
+  // reference's order — the same roundings, batch-fold more parallelism for
+  // the few-tile, long-k dW shapes.
+  if (g_nt_sdot && batch > 1) {
+    float* part = nullptr;
+    if (int r = ensure_scratch(c, 4, batch * i_m * i_n, &part)) return r;
+    GemmArgs a{};
+    a.M = i_m; a.N = i_n; a.K = i_k;
+    a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_STORE;
+    a.A = delta; a.lda = i_k; a.strideA = i_m * i_k;
+    a.B = col; a.ldb = i_k; a.strideB = colSize;
+    a.C = part; a.ldc = i_n; a.strideC = i_m * i_n;
+    a.batch = batch; a.epi = EPI_NONE;
+    {
+      OpTimer t(c, TNS_OP_GEMM);
+      if (int r = hip_status(launch_sgemm_nt_sdot(a, c->stream), "sgemm_nt launch")) return r;
+    }
+    if (int r = hip_status(launch_add_in_order(weight_updates, part, i_m * i_n, batch,
+                                               c->stream), "dW accumulate launch"))
       return r;
+  } else {
+    for (int64_t b = 0; b < batch; ++b)
+      if (int r = do_gemm(c, false, true, i_m, i_n, i_k, 1.0f, delta + b * i_m * i_k, i_k, 0,
+                          col + b * colSize, i_k, 0, 1.0f, weight_updates, i_n, 0, 1, EPI_NONE,
+                          nullptr, 0))
+        return r;
+  }
   if (!state_delta) return TNS_OK;
   // col_b = W^T . delta_b (TN strided batched, weights shared, beta = 0 into
   // the workspace), then col2im accumulates into state.delta (646-660)

@@ -33,7 +33,9 @@ constexpr bool act_transcendental(int act) { return act == 0 || act == 6; }
 //   BETA_ONE    acc starts at C                     — matMul accumulate
 //   BETA_SCALE  acc starts at beta*C (single mul)   — reference mulvs, incl.
 //               strict beta=0 (0*C keeps NaN/Inf like ntensors.pas:2259)
-enum BetaMode { BETA_ZERO = 0, BETA_ONE = 1, BETA_SCALE = 2 };
+//   BETA_STORE  C := the product term alone (sdot kernel only: per-image
+//               partial sums that a later in-order pass adds to C)
+enum BetaMode { BETA_ZERO = 0, BETA_ONE = 1, BETA_SCALE = 2, BETA_STORE = 3 };
 
 struct GemmArgs {
   int64_t M, N, K;
@@ -80,6 +82,9 @@ hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
 // gemm(Trans, Trans) in the reference's scalar s_tt order (sgemm_tt.hip);
 // plain epilogue only
 hipError_t launch_sgemm_tt(const GemmArgs& a, hipStream_t s);
+// C[e] := (...((C[e] + part[0][e]) + part[1][e]) ...) + part[batch-1][e]
+hipError_t launch_add_in_order(float* C, const float* part, int64_t n, int64_t batch,
+                               hipStream_t s);
 // implicit-GEMM convolution: NN, B generated from the image (a.conv must be set)
 hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s);
 hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s);

@@ -148,6 +148,33 @@ def test_conv_backward_matches_oracle(hip, torch_cuda, ora, batch, C, H, F, k, s
     assert np.array_equal(dbu.cpu().numpy(), rbu)
 
 
+@pytest.mark.parametrize("idx", [11, 74])
+def test_conv_backward_yolov3_batch8(hip, torch_cuda, ora, idx):
+    """YOLOv3 layer shapes at batch 8: the dW partial sums of all images in
+    one batched sdot launch, added to weight_updates in image order — bit-exact
+    against the reference's per-image beta = 1 loop."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    spec = yolov3_conv_table()[idx]
+    batch, C, H, F, k, s, p = 8, spec.c, spec.h, spec.filters, spec.size, spec.stride, spec.pad
+    rng = np.random.default_rng(idx)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.1, 0.1, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    rd, rbu, rwu = d0.copy(), bu0.copy(), wu0.copy()
+    ora.conv_backward(x, w, F, k, s, p, spec.activation, out, rd, rbu, rwu, None)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    dx, dw, dout, dd, dbu, dwu = map(t, (x, w, out, d0, bu0, wu0))
+    hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, spec.activation, dout, dd, dbu, dwu)
+    hip.finish()
+    assert np.array_equal(dd.cpu().numpy(), rd)
+    assert np.array_equal(dwu.cpu().numpy(), rwu)
+    assert np.array_equal(dbu.cpu().numpy(), rbu)
+
+
 def test_conv_backward_rejects_dilation(hip, torch_cuda):
     from tensorium_amd._abi import TnsError
     z = torch_cuda.zeros(4096, device="cuda")
