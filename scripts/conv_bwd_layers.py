@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""Per-layer split of the YOLOv3 batch-8 conv backward (telemetry: GEMM =
+dW sdot batch + dX TN, im2col, col2im).  One JSON line.
+
+  python scripts/conv_bwd_layers.py
+"""
+import json
+import sys
+from pathlib import Path
+
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from tensorium_amd.nnhip import TNNHip  # noqa: E402
+from tensorium_amd.yolo import yolov3_conv_table  # noqa: E402
+from tensorium_amd._abi import TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM  # noqa: E402
+
+
+def main():
+    hip = TNNHip(0)
+    batch = 8
+    out = []
+    for s in yolov3_conv_table():
+        x = torch.rand(batch, s.c, s.h, s.h, device="cuda")
+        w = torch.rand(s.filters, s.K, device="cuda") * 0.1
+        o = torch.rand(batch, s.filters, s.out_h, s.out_h, device="cuda")
+        d = torch.rand_like(o)
+        bu, wu = torch.zeros(s.filters, device="cuda"), torch.zeros(s.filters, s.K, device="cuda")
+        sd = torch.zeros_like(x)
+        run = lambda: hip.convBackward(batch, s.c, s.h, s.h, x, w, s.filters, s.size, s.stride,  # noqa
+                                       s.pad, 1, s.activation, o, d, bu, wu, None, sd)
+        run()
+        hip.setTelemetry(True)
+        run()
+        g, i, c = hip.opMs(TNS_OP_GEMM), hip.opMs(TNS_OP_IM2COL), hip.opMs(TNS_OP_COL2IM)
+        hip.setTelemetry(False)
+        out.append({"layer": s.index, "shape": f"{s.c}x{s.h} k{s.size}s{s.stride}->{s.filters}",
+                    "gemm_ms": round(g, 3), "tf": round(2 * s.flops * batch / g / 1e9, 1),
+                    "im2col_ms": round(i, 3), "col2im_ms": round(c, 3)})
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -25,13 +25,16 @@ namespace {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int SD_NT = 512;       // 8 waves = 8 residue classes
-constexpr int SD_BK = 64;        // k per tile: 8 per residue class = 4 MFMA steps
-constexpr int SD_KP = SD_BK + 1;  // LDS row stride
+// k per tile: BK/8 per residue class = BK/16 MFMA steps.  64 by default;
+// 256 for few output tiles over long k (conv dW: k = oH*oW up to 173056),
+// where the chains are short per tile and the exposed global-load latency of
+// every tile dominated (one block per image at 2.3 TF on YOLOv3 layer 0).
 
 __device__ __attribute__((aligned(16))) static float4 g_sd_zero;
 
-template <int TN, int VEC>
+template <int TN, int VEC, int SD_BK>
 __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
+  constexpr int SD_KP = SD_BK + 1;  // LDS row stride
   constexpr int BM = 32, BN = 32 * TN, ROWS = BM + BN;
   constexpr int KV = SD_BK / VEC;               // staging units per row
   constexpr int U = ROWS * KV / SD_NT;          // staging units per thread
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
   }
 }
 
-template <int TN, int VEC>
+template <int TN, int VEC, int BK = 64>
 hipError_t launch_tn(const GemmArgs& a, hipStream_t s) {
   const int64_t tiles = ((a.M + 31) / 32) * ((a.N + 32 * TN - 1) / (32 * TN));
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
@@ -161,7 +164,7 @@ hipError_t launch_tn(const GemmArgs& a, hipStream_t s) {
     sub.B = a.B + b0 * a.strideB;
     sub.C = a.C + b0 * a.strideC;
     sub.batch = nb;
-    hipLaunchKernelGGL((sgemm_nt_sdot_kernel<TN, VEC>), dim3((unsigned)tiles, (unsigned)nb),
+    hipLaunchKernelGGL((sgemm_nt_sdot_kernel<TN, VEC, BK>), dim3((unsigned)tiles, (unsigned)nb),
                        dim3(SD_NT), 0, s, sub);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -184,6 +187,10 @@ hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s) {
                  k_vec4(a.B, a.ldb, a.strideB, a.batch, a.K);
   const int64_t b64 = ((a.M + 31) / 32) * ((a.N + 63) / 64) * a.batch;
   if (b64 >= 1024) return v ? launch_tn<2, 4>(a, s) : launch_tn<2, 1>(a, s);
+  // few 32x32 tiles over a long k: 256-deep k-tiles (the 64-row LDS stages
+  // take 2 x 65.8 KB of gfx950's 160 KB)
+  if (a.K >= 16384 && ((a.M + 31) / 32) * ((a.N + 31) / 32) * a.batch < 512)
+    return v ? launch_tn<1, 4, 256>(a, s) : launch_tn<1, 1, 256>(a, s);
   return v ? launch_tn<1, 4>(a, s) : launch_tn<1, 1>(a, s);
 }
 

@@ -148,7 +148,7 @@ def test_conv_backward_matches_oracle(hip, torch_cuda, ora, batch, C, H, F, k, s
     assert np.array_equal(dbu.cpu().numpy(), rbu)
 
 
-@pytest.mark.parametrize("idx", [11, 74])
+@pytest.mark.parametrize("idx", [0, 2, 11, 74])
 def test_conv_backward_yolov3_batch8(hip, torch_cuda, ora, idx):
     """YOLOv3 layer shapes at batch 8: the dW partial sums of all images in
     one batched sdot launch, added to weight_updates in image order — bit-exact

@@ -82,7 +82,8 @@ def test_all_transposes_within_bound(hip, torch_cuda, ora, M, N, K, ta, tb):
 
 
 NT_SHAPES = SHAPES + [(32, 4096, 4096), (32, 64, 784), (10, 32, 32), (3, 5, 8), (3, 5, 9),
-                     (33, 65, 15), (64, 1152, 2704), (70, 90, 2304)]
+                     (33, 65, 15), (64, 1152, 2704), (70, 90, 2304), (32, 27, 173056),
+                     (64, 288, 20001)]
 
 
 @pytest.mark.parametrize("M,N,K", NT_SHAPES)
