@@ -56,7 +56,7 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
   const int64_t M = p.M, N = p.N, K = p.K;
 
   float st[U * VEC];
-  auto load = [&](int64_t k0) {
+  auto load_into = [&](float (&st)[U * VEC], int64_t k0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int idx = tid + SD_NT * u;
@@ -79,7 +79,8 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
       }
     }
   };
-  auto store = [&](float* buf) {
+  auto load = [&](int64_t k0) { load_into(st, k0); };
+  auto store_from = [&](const float (&st)[U * VEC], float* buf) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int idx = tid + SD_NT * u;
@@ -88,6 +89,7 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
       for (int c = 0; c < VEC; ++c) buf[row * SD_KP + k + c] = st[VEC * u + c];
     }
   };
+  auto store = [&](float* buf) { store_from(st, buf); };
 
   floatx16 acc[TN];
 #pragma unroll
@@ -96,22 +98,44 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
     for (int e = 0; e < 16; ++e) acc[j][e] = 0.0f;
 
   const int nt = (int)((K + SD_BK - 1) / SD_BK);
-  if (nt > 0) {
+  auto mma_tile = [&](const float* cur) {
+#pragma unroll
+    for (int s = 0; s < SD_BK / 16; ++s) {
+      const int kk = r + 16 * s + 8 * h;  // residue class r, ascending
+      const float a = cur[l31 * SD_KP + kk];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, cur[(BM + 32 * j + l31) * SD_KP + kk],
+                                                      acc[j], 0, 0, 0);
+    }
+  };
+  if constexpr (SD_BK == 256) {
+    // long-k form: global loads run TWO tiles ahead (two register sets), so
+    // a tile's load latency is covered by two tiles of MFMA chains
+    float st2[U * VEC];
+    auto body = [&](float (&ld)[U * VEC], const float (&sv)[U * VEC], int t) {
+      if (t + 2 < nt) load_into(ld, (int64_t)(t + 2) * SD_BK);
+      mma_tile(lds + (t & 1) * STAGE);
+      if (t + 1 < nt) store_from(sv, lds + ((t + 1) & 1) * STAGE);
+      __syncthreads();
+    };
+    if (nt > 0) {
+      load_into(st, 0);
+      store_from(st, lds);
+      if (nt > 1) load_into(st, SD_BK);
+      __syncthreads();
+      for (int t = 0; t < nt; t += 2) {
+        body(st2, st, t);              // tile t+1 from st, tile t+2 into st2
+        if (t + 1 < nt) body(st, st2, t + 1);  // tile t+2 from st2, t+3 into st
+      }
+    }
+  } else if (nt > 0) {
     load(0);
     store(lds);
     __syncthreads();
     for (int t = 0; t < nt; ++t) {
-      const float* cur = lds + (t & 1) * STAGE;
       if (t + 1 < nt) load((int64_t)(t + 1) * SD_BK);
-#pragma unroll
-      for (int s = 0; s < SD_BK / 16; ++s) {
-        const int kk = r + 16 * s + 8 * h;  // residue class r, ascending
-        const float a = cur[l31 * SD_KP + kk];
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, cur[(BM + 32 * j + l31) * SD_KP + kk],
-                                                        acc[j], 0, 0, 0);
-      }
+      mma_tile(lds + (t & 1) * STAGE);
       if (t + 1 < nt) store(lds + ((t + 1) & 1) * STAGE);
       __syncthreads();
     }
