@@ -84,6 +84,7 @@ __global__ void means_vars_seq(const float* __restrict__ x, int64_t groups, int6
 // adds them in group order
 constexpr int MV_SLOTS = TPB / 8;
 constexpr int MV_CHUNK = 1024;
+constexpr int MV_UNR = 64;
 __global__ __launch_bounds__(TPB) void means_vars_lanes(const float* __restrict__ x,
                                                         int64_t groups, int64_t N, int64_t bs,
                                                         float* __restrict__ means,
@@ -107,12 +108,15 @@ __global__ __launch_bounds__(TPB) void means_vars_lanes(const float* __restrict_
         if (on) {
           const float* p = blk + l;
           int64_t t = 0;
-          for (; t + 8 <= nb; t += 8) {
-            float w[8];
+          // MV_UNR loads in flight per lane ahead of its (sequential) adds:
+          // with one wave per channel-group set, memory-level parallelism
+          // per lane is what bounds this pass
+          for (; t + MV_UNR <= nb; t += MV_UNR) {
+            float w[MV_UNR];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) w[u] = p[8 * (t + u)];
+            for (int u = 0; u < MV_UNR; ++u) w[u] = p[8 * (t + u)];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
+            for (int u = 0; u < MV_UNR; ++u) {
               if (pass) {
                 const float d = mu - w[u];
                 acc = acc + d * d;
@@ -341,7 +345,9 @@ __global__ void vssum_k(int64_t n, const float* __restrict__ a, float* __restric
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
                              float* vars, int quirk, hipStream_t s) {
   if (N <= 0) return hipSuccess;
-  if (bs == 1 || groups * bs <= kSeqMax)
+  // one thread per channel for FC shapes (blockSize 1) and short blocks;
+  // blocks of >= 64 use 8 lanes each (their chains are the reference's lanes)
+  if (bs == 1 || (bs < 64 && groups * bs <= kSeqMax))
     hipLaunchKernelGGL(means_vars_seq, dim3(nblk(N)), dim3(TPB), 0, s, x, groups, N, bs, means,
                        vars, quirk);
   else
