@@ -3,7 +3,8 @@
 lane orders, normalize, forwardScaleAdd) on conv-layer BN shapes of YOLOv3
 at batch 8 ([groups=8][channels][H*W]) and the MNIST FC shape.  Algorithmic
 bytes: meansAndVars reads x (twice: mean then variance pass), normalize and
-scale+bias read and write x.  One JSON line.
+scale+bias read and write x; meansAndVarsDelta reads delta twice and x
+once.  One JSON line.
 
   python scripts/bn_perf.py
 """
@@ -35,6 +36,11 @@ def main():
         row["normalize_gbs"] = round(2 * n * 4 / ms / 1e6, 1)
         ms = timed(lambda: hip.forwardScaleAdd(n, x, 0, N, s, b, 1, groups), 10)
         row["scale_add_gbs"] = round(2 * n * 4 / ms / 1e6, 1)
+        d = torch.rand(n, device="cuda")
+        md, vd = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
+        ms = timed(lambda: hip.meansAndVarsDelta(n, N, groups, d, x, 0, m, v, md, vd), 5)
+        row["means_vars_delta_ms"] = round(ms, 4)
+        row["means_vars_delta_gbs"] = round(3 * n * 4 / ms / 1e6, 1)
         out[f"{groups}x{N}x{bs}"] = row
     print(json.dumps(out))
 

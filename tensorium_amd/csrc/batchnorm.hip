@@ -251,7 +251,15 @@ __global__ void add_sums_seq(float* __restrict__ dst, const float* __restrict__ 
 __device__ __forceinline__ float vssum8(const float* a, int64_t n) {  // vssum_avx2 order
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   const int64_t blocks = n >> 3;
-  for (int64_t t = 0; t < blocks; ++t)
+  int64_t t = 0;
+  for (; t + 4 <= blocks; t += 4) {  // 32 loads ahead of the lane adds
+    float w[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) w[u] = a[8 * t + u];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) acc[u & 7] = acc[u & 7] + w[u];
+  }
+  for (; t < blocks; ++t)
 #pragma unroll
     for (int l = 0; l < 8; ++l) acc[l] = acc[l] + a[8 * t + l];
   const float s0 = acc[0] + acc[4], s1 = acc[1] + acc[5], s2 = acc[2] + acc[6],
@@ -281,6 +289,56 @@ __global__ void mean_var_delta_seq(const float* __restrict__ delta, const float*
   const float inv = -1.0f / sqrtf(ve);
   mean_delta[i] = m * inv;
   var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
+}
+
+// conv blocks: one workgroup per channel, one thread per group — each
+// group's block sums (vssum8 of delta, the sequential (x-mu)*delta chain) are
+// independent; thread 0 adds them in group order as mean_var_delta_seq does
+__global__ __launch_bounds__(TPB) void mean_var_delta_blocks(
+    const float* __restrict__ delta, const float* __restrict__ x, const float* __restrict__ mean,
+    const float* __restrict__ var, int64_t groups, int64_t N, int64_t bs,
+    float* __restrict__ mean_delta, float* __restrict__ var_delta) {
+  __shared__ float ms[TPB], vs[TPB];
+  const int64_t i = blockIdx.x;
+  const float mu = mean[i];
+  float m = 0.0f, v = 0.0f;
+  for (int64_t j0 = 0; j0 < groups; j0 += TPB) {
+    const int64_t jn = groups - j0 < TPB ? groups - j0 : TPB;
+    if (threadIdx.x < jn) {
+      const int64_t j = j0 + threadIdx.x;
+      const float* dd = delta + (i + j * N) * bs;
+      const float* xx = x + (i + j * N) * bs;
+      ms[threadIdx.x] = vssum8(dd, bs);
+      // the chain is sequential; its operands are loaded MV_UNR ahead
+      float t = 0.0f;
+      int64_t k = 0;
+      for (; k + MV_UNR <= bs; k += MV_UNR) {
+        float xa[MV_UNR], da[MV_UNR];
+#pragma unroll
+        for (int u = 0; u < MV_UNR; ++u) {
+          xa[u] = xx[k + u];
+          da[u] = dd[k + u];
+        }
+#pragma unroll
+        for (int u = 0; u < MV_UNR; ++u) t = t + (xa[u] - mu) * da[u];
+      }
+      for (; k < bs; ++k) t = t + (xx[k] - mu) * dd[k];
+      vs[threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int64_t jj = 0; jj < jn; ++jj) {
+        m = m + ms[jj];
+        v = v + vs[jj];
+      }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float ve = var[i] > SEPS ? var[i] : SEPS;
+    const float inv = -1.0f / sqrtf(ve);
+    mean_delta[i] = m * inv;
+    var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
+  }
 }
 
 __global__ void normalize_delta_k(const float* __restrict__ x, const float* __restrict__ mean,
@@ -397,8 +455,12 @@ hipError_t launch_mean_var_delta(const float* delta, const float* x, const float
                                  const float* var, int64_t groups, int64_t N, int64_t bs,
                                  float* mean_delta, float* var_delta, hipStream_t s) {
   if (N <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mean_var_delta_seq, dim3(nblk(N)), dim3(TPB), 0, s, delta, x, mean, var,
-                     groups, N, bs, mean_delta, var_delta);
+  if (bs >= 64 && N <= 0x7fffffffLL)
+    hipLaunchKernelGGL(mean_var_delta_blocks, dim3((unsigned)N), dim3(TPB), 0, s, delta, x, mean,
+                       var, groups, N, bs, mean_delta, var_delta);
+  else
+    hipLaunchKernelGGL(mean_var_delta_seq, dim3(nblk(N)), dim3(TPB), 0, s, delta, x, mean, var,
+                       groups, N, bs, mean_delta, var_delta);
   return hipGetLastError();
 }
 

@@ -60,7 +60,8 @@ def test_means_vars_srss_quirk(hip, torch_cuda, ora, groups, N, bs):
         assert np.array_equal(dm.cpu().numpy(), m) and np.array_equal(dv.cpu().numpy(), v)
 
 
-@pytest.mark.parametrize("groups,N,bs", [(32, 64, 1), (4, 8, 9), (8, 16, 2704)])
+@pytest.mark.parametrize("groups,N,bs", [(32, 64, 1), (4, 8, 9), (8, 16, 2704), (300, 3, 65),
+                                         (2, 5, 1029)])
 def test_bn_backward_ops(hip, torch_cuda, ora, groups, N, bs):
     n = groups * N * bs
     x = ora.uniform(n, 31, N, -2.0, 2.0)
