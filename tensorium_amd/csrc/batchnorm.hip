@@ -238,6 +238,61 @@ __global__ void add_dots_seq(float* __restrict__ dst, const float* __restrict__ 
   }
 }
 
+// conv blocks: one workgroup per channel, one thread per group computing its
+// block's sdot_avx2 (same lanes, same fold); thread 0 sums them in group
+// order and adds to dst as add_dots_seq does
+__device__ __forceinline__ float sdot8_block(const float* pa, const float* pb, int64_t bs) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t blocks = bs >> 3;
+  int64_t t = 0;
+  for (; t + 4 <= blocks; t += 4) {  // 32 operand pairs ahead of the FMAs
+    float wa[32], wb[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      wa[u] = pa[8 * t + u];
+      wb[u] = pb[8 * t + u];
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) acc[u & 7] = fmaf(wa[u], wb[u], acc[u & 7]);
+  }
+  for (; t < blocks; ++t)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc[l] = fmaf(pa[8 * t + l], pb[8 * t + l], acc[l]);
+  const int64_t rem = bs & 7;
+  if (rem) {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const float xa = l < rem ? pa[8 * blocks + l] : 0.0f;
+      const float xb = l < rem ? pb[8 * blocks + l] : 0.0f;
+      acc[l] = fmaf(xa, xb, acc[l]);
+    }
+  }
+  const float s0 = acc[0] + acc[4], s1 = acc[1] + acc[5], s2 = acc[2] + acc[6],
+              s3 = acc[3] + acc[7];
+  return (s0 + s1) + (s2 + s3);
+}
+
+__global__ __launch_bounds__(TPB) void add_dots_blocks(float* __restrict__ dst,
+                                                       const float* __restrict__ a,
+                                                       const float* __restrict__ b,
+                                                       int64_t groups, int64_t N, int64_t bs) {
+  __shared__ float part[TPB];
+  const int64_t i = blockIdx.x;
+  float sum = 0.0f;
+  for (int64_t j0 = 0; j0 < groups; j0 += TPB) {
+    const int64_t jn = groups - j0 < TPB ? groups - j0 : TPB;
+    if (threadIdx.x < jn) {
+      const int64_t g = j0 + threadIdx.x;
+      part[threadIdx.x] = sdot8_block(a + (i + g * N) * bs, b + (i + g * N) * bs, bs);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int64_t jj = 0; jj < jn; ++jj) sum = sum + part[jj];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dst[i] = dst[i] + sum;
+}
+
 __global__ void add_sums_seq(float* __restrict__ dst, const float* __restrict__ src,
                              int64_t groups, int64_t N) {
   const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
@@ -435,7 +490,11 @@ hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, con
 hipError_t launch_add_dots(float* dst, const float* a, const float* b, int64_t groups, int64_t N,
                            int64_t bs, hipStream_t s) {
   if (N <= 0) return hipSuccess;
-  hipLaunchKernelGGL(add_dots_seq, dim3(nblk(N)), dim3(TPB), 0, s, dst, a, b, groups, N, bs);
+  if (bs >= 64 && N <= 0x7fffffffLL)
+    hipLaunchKernelGGL(add_dots_blocks, dim3((unsigned)N), dim3(TPB), 0, s, dst, a, b, groups, N,
+                       bs);
+  else
+    hipLaunchKernelGGL(add_dots_seq, dim3(nblk(N)), dim3(TPB), 0, s, dst, a, b, groups, N, bs);
   return hipGetLastError();
 }
 
