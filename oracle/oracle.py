@@ -211,6 +211,9 @@ _PROTO2 = {
     "ora_add_dots": (None, [fp, fp, fp, i64, i64, i64]),
     "ora_add_sums": (None, [fp, fp, i64, i64, i64]),
     "ora_mean_var_delta": (None, [fp, fp, fp, fp, i64, i64, i64, fp, fp]),
+    "ora_mean_var_delta_q": (None, [fp, fp, fp, fp, i64, i64, i64, fp, fp, i32]),
+    "ora_var_delta_avx": (f32, [i64, f32, fp, fp, i32]),
+    "ora_srss": (f32, [i64, f32, fp, i32]),
     "ora_normalize_delta": (None, [fp, fp, fp, fp, fp, fp, i64, i64, i64]),
     "ora_softmax": (None, [i64, fp, f32, i64, fp]),
     "ora_softmax_xent": (None, [i64, fp, fp, fp, fp]),
@@ -271,11 +274,22 @@ def sgd_update(W, dW, b, db, scales, dscales, lrb, ndb, momentum):
                            lrb, ndb, momentum)
 
 
-def mean_var_delta(delta, x, mean, var, groups, N, bs):
+def mean_var_delta(delta, x, mean, var, groups, N, bs, quirk=0):
     md = np.zeros(N, np.float32)
     vd = np.zeros(N, np.float32)
-    _lib2().ora_mean_var_delta(_p(delta), _p(x), _p(mean), _p(var), groups, N, bs, _p(md), _p(vd))
+    _lib2().ora_mean_var_delta_q(_p(delta), _p(x), _p(mean), _p(var), groups, N, bs, _p(md),
+                                 _p(vd), int(quirk))
     return md, vd
+
+
+def var_delta_avx(mean, delta, x, quirk=0):
+    """sVarinceDelta_avx over one block (ntensors.pas:8721-8757)."""
+    return float(_lib2().ora_var_delta_avx(delta.size, mean, _p(delta), _p(x), int(quirk)))
+
+
+def srss(mean, a, quirk=0):
+    """srss over one block (ntensors.pas:1493-1523)."""
+    return float(_lib2().ora_srss(a.size, mean, _p(a), int(quirk)))
 
 
 def normalize_delta(x, mean, var, md, vd, delta, groups, N, bs):

@@ -135,6 +135,12 @@ void    ora_add_sums(float* dst, const float* src, int64_t groups, int64_t N, in
 void    ora_mean_var_delta(const float* delta, const float* x, const float* mean,
                            const float* var, int64_t groups, int64_t N, int64_t bs,
                            float* mean_delta, float* var_delta);
+void    ora_mean_var_delta_q(const float* delta, const float* x, const float* mean,
+                             const float* var, int64_t groups, int64_t N, int64_t bs,
+                             float* mean_delta, float* var_delta, int quirk);
+/* sVarinceDelta_avx (ntensors.pas:8721-8757): one block's sum of
+ * (x - mean) * delta in the reference's 8-lane order (quirk: see .c) */
+float   ora_var_delta_avx(int64_t n, float mean, const float* delta, const float* x, int quirk);
 void    ora_normalize_delta(const float* x, const float* mean, const float* var,
                             const float* mean_delta, const float* var_delta, float* delta,
                             int64_t groups, int64_t N, int64_t bs);

@@ -154,26 +154,69 @@ void ora_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64
   }
 }
 
-/* sMeanAndVarianceDelta with the AVX2 sVarinceDelta_avx / vssum_avx2 forms
- * (for bs == 1 both reduce to one rounded term per group). */
-void ora_mean_var_delta(const float* delta, const float* x, const float* mean,
-                        const float* var, int64_t groups, int64_t N, int64_t bs,
-                        float* mean_delta, float* var_delta) {
+/* sVarinceDelta_avx (ntensors.pas:8721-8757), the per-block routine the
+ * configured USE_AVX2 build calls from sMeanAndVarianceDelta (8856-8859):
+ *   8 lanes over the full 8-blocks, acc_l := acc_l + (x - mean) * delta
+ *   (vsubps, vmulps, vaddps: each rounded; 8729-8736);
+ *   with a tail (N % 8 != 0): x_l := acc_l + acc_{l+4} (vextractf128 + addps,
+ *   8742-8744), then every tail element added into lane 0 in order
+ *   (vsubss, vmulss, vaddss, 8746-8753);
+ *   then haddps twice: (x0 + x1) + (x2 + x3) (8755-8756).
+ * Without a tail the fold is skipped and lanes 4..7 are dropped (the jz at
+ * 8741 jumps straight to the haddps) — reproduced only when quirk != 0
+ * (TNS_OPT_SRSS_QUIRK, reference quirk 6); otherwise the lanes are folded as
+ * with a tail.  For N < 8 all lanes are +0 and the result is the tail's
+ * sequential sum. */
+float ora_var_delta_avx(int64_t n, float mean, const float* delta, const float* x, int quirk) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t blocks = n >> 3;
+  for (int64_t t = 0; t < blocks; t++)
+    for (int l = 0; l < 8; l++) {
+      const float d = x[8 * t + l] - mean;
+      const float p = d * delta[8 * t + l];
+      acc[l] = acc[l] + p;
+    }
+  float r[4];
+  if ((n & 7) == 0 && quirk) {
+    for (int l = 0; l < 4; l++) r[l] = acc[l];
+  } else {
+    for (int l = 0; l < 4; l++) r[l] = acc[l] + acc[l + 4];
+    for (int64_t i = blocks * 8; i < n; i++) {
+      const float d = x[i] - mean;
+      const float p = d * delta[i];
+      r[0] = r[0] + p;
+    }
+  }
+  return (r[0] + r[1]) + (r[2] + r[3]);
+}
+
+/* sMeanAndVarianceDelta (ntensors.pas:8831-8899) with the USE_AVX2 forms:
+ * per channel i, over the groups j in order, m := m + vsSumI(block)
+ * (vssum_avx2) and v := v + sVarinceDelta_avx(block) (8853, 8856-8859);
+ * then mean_delta = m * (-1/sqrt(max(var, eps))) and
+ * variance_delta = v * -0.5 * Power(max(var, eps), -3/2) (8869-8870). */
+void ora_mean_var_delta_q(const float* delta, const float* x, const float* mean,
+                          const float* var, int64_t groups, int64_t N, int64_t bs,
+                          float* mean_delta, float* var_delta, int quirk) {
   for (int64_t i = 0; i < N; i++) {
     float m = 0.0f, v = 0.0f;
     for (int64_t j = 0; j < groups; j++) {
       const float* dd = delta + (i + j * N) * bs;
       const float* xx = x + (i + j * N) * bs;
       m = m + ora_vssum(bs, dd);
-      float t = 0.0f;
-      for (int64_t k = 0; k < bs; k++) t = t + (xx[k] - mean[i]) * dd[k];
-      v = v + t;
+      v = v + ora_var_delta_avx(bs, mean[i], dd, xx, quirk);
     }
     float ve = var[i] > SEPS ? var[i] : SEPS;
     float inv = -1.0f / sqrtf(ve);
     mean_delta[i] = m * inv;
     var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
   }
+}
+
+void ora_mean_var_delta(const float* delta, const float* x, const float* mean,
+                        const float* var, int64_t groups, int64_t N, int64_t bs,
+                        float* mean_delta, float* var_delta) {
+  ora_mean_var_delta_q(delta, x, mean, var, groups, N, bs, mean_delta, var_delta, 0);
 }
 
 /* sNormalizeDelta (AVX2 sNormalizeDelta_avx order):

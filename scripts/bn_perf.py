@@ -3,8 +3,9 @@
 lane orders, normalize, forwardScaleAdd) on conv-layer BN shapes of YOLOv3
 at batch 8 ([groups=8][channels][H*W]) and the MNIST FC shape.  Algorithmic
 bytes: meansAndVars reads x (twice: mean then variance pass), normalize and
-scale+bias read and write x; meansAndVarsDelta reads delta twice and x
-once.  One JSON line.
+scale+bias read and write x; meansAndVarsDelta reads delta and x once
+(both lane chains run off one staged tile); addDots reads both operands, addSums
+one.  One JSON line.
 
   python scripts/bn_perf.py
 """
@@ -40,7 +41,14 @@ def main():
         md, vd = torch.zeros(N, device="cuda"), torch.zeros(N, device="cuda")
         ms = timed(lambda: hip.meansAndVarsDelta(n, N, groups, d, x, 0, m, v, md, vd), 5)
         row["means_vars_delta_ms"] = round(ms, 4)
-        row["means_vars_delta_gbs"] = round(3 * n * 4 / ms / 1e6, 1)
+        row["means_vars_delta_gbs"] = round(2 * n * 4 / ms / 1e6, 1)
+        dsc = torch.zeros(N, device="cuda")
+        ms = timed(lambda: hip.addDots(n, N, groups, d, x, 0, dsc), 5)
+        row["add_dots_ms"] = round(ms, 4)
+        row["add_dots_gbs"] = round(2 * n * 4 / ms / 1e6, 1)
+        ms = timed(lambda: hip.backwardBias(N, dsc, n, d, 0, 1, groups), 5)
+        row["add_sums_ms"] = round(ms, 4)
+        row["add_sums_gbs"] = round(n * 4 / ms / 1e6, 1)
         out[f"{groups}x{N}x{bs}"] = row
     print(json.dumps(out))
 

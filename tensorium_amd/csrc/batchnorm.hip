@@ -79,98 +79,6 @@ __global__ void means_vars_seq(const float* __restrict__ x, int64_t groups, int6
   vars[i] = v / S2;
 }
 
-// one workgroup per channel (conv layers): 8 consecutive lanes own a block
-// (lane l = the vssum / srss lane), block results meet in LDS and one thread
-// adds them in group order
-constexpr int MV_SLOTS = TPB / 8;
-constexpr int MV_CHUNK = 1024;
-constexpr int MV_UNR = 64;
-__global__ __launch_bounds__(TPB) void means_vars_lanes(const float* __restrict__ x,
-                                                        int64_t groups, int64_t N, int64_t bs,
-                                                        float* __restrict__ means,
-                                                        float* __restrict__ vars, int quirk) {
-  __shared__ float tot[MV_CHUNK];
-  __shared__ float mean_s;
-  const int64_t i = blockIdx.x;
-  const int l = threadIdx.x & 7, q = threadIdx.x >> 3;
-  const int64_t nb = bs >> 3;
-  const bool tail = (bs & 7) != 0;
-  float m = 0.0f, v = 0.0f;
-  for (int pass = 0; pass < 2; ++pass) {
-    const float mu = pass ? mean_s : 0.0f;
-    float run = 0.0f;
-    for (int64_t j0 = 0; j0 < groups; j0 += MV_CHUNK) {
-      const int64_t jn = groups - j0 < MV_CHUNK ? groups - j0 : MV_CHUNK;
-      for (int64_t jj = q; jj < ((jn + MV_SLOTS - 1) / MV_SLOTS) * MV_SLOTS; jj += MV_SLOTS) {
-        const bool on = jj < jn;
-        const float* blk = x + ((j0 + (on ? jj : 0)) * N + i) * bs;
-        float acc = 0.0f;
-        if (on) {
-          const float* p = blk + l;
-          int64_t t = 0;
-          // MV_UNR loads in flight per lane ahead of its (sequential) adds:
-          // with one wave per channel-group set, memory-level parallelism
-          // per lane is what bounds this pass
-          for (; t + MV_UNR <= nb; t += MV_UNR) {
-            float w[MV_UNR];
-#pragma unroll
-            for (int u = 0; u < MV_UNR; ++u) w[u] = p[8 * (t + u)];
-#pragma unroll
-            for (int u = 0; u < MV_UNR; ++u) {
-              if (pass) {
-                const float d = mu - w[u];
-                acc = acc + d * d;
-              } else {
-                acc = acc + w[u];
-              }
-            }
-          }
-          for (; t < nb; ++t) {
-            if (pass) {
-              const float d = mu - p[8 * t];
-              acc = acc + d * d;
-            } else {
-              acc = acc + p[8 * t];
-            }
-          }
-        }
-        const bool drop = pass && !tail && quirk;          // srss without a tail
-        const float up = __shfl_down(acc, 4, 8);           // lane l+4
-        float x0 = drop ? acc : acc + up;                  // lanes 0..3: x_l
-        if (pass && tail && on && l == 0)                  // srss: tail into lane 0
-          for (int64_t u = nb * 8; u < bs; ++u) {
-            const float d = mu - blk[u];
-            x0 = x0 + d * d;
-          }
-        const float h = x0 + __shfl_down(x0, 1, 8);        // x0+x1 (l=0), x2+x3 (l=2)
-        float r = h + __shfl_down(h, 2, 8);                // (x0+x1)+(x2+x3)
-        if (on && l == 0) {
-          if (!pass)                                       // vssum: tail after the fold
-            for (int64_t u = nb * 8; u < bs; ++u) r = r + blk[u];
-          tot[jj] = r;
-        }
-      }
-      __syncthreads();
-      if (threadIdx.x == 0)
-        for (int64_t jj = 0; jj < jn; ++jj) run = run + tot[jj];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-      if (pass) {
-        v = run / (float)(groups * bs - 1);
-      } else {
-        m = run / (float)(groups * bs);
-        mean_s = m;
-      }
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    means[i] = m;
-    vars[i] = v;
-  }
-}
-
 // ---- normalize / scale / bias ----------------------------------------------
 __global__ void normalize_k(float* __restrict__ x, int64_t total, int64_t N, int64_t bs,
                             const float* __restrict__ means, int64_t mstride,
@@ -238,61 +146,6 @@ __global__ void add_dots_seq(float* __restrict__ dst, const float* __restrict__ 
   }
 }
 
-// conv blocks: one workgroup per channel, one thread per group computing its
-// block's sdot_avx2 (same lanes, same fold); thread 0 sums them in group
-// order and adds to dst as add_dots_seq does
-__device__ __forceinline__ float sdot8_block(const float* pa, const float* pb, int64_t bs) {
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int64_t blocks = bs >> 3;
-  int64_t t = 0;
-  for (; t + 4 <= blocks; t += 4) {  // 32 operand pairs ahead of the FMAs
-    float wa[32], wb[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      wa[u] = pa[8 * t + u];
-      wb[u] = pb[8 * t + u];
-    }
-#pragma unroll
-    for (int u = 0; u < 32; ++u) acc[u & 7] = fmaf(wa[u], wb[u], acc[u & 7]);
-  }
-  for (; t < blocks; ++t)
-#pragma unroll
-    for (int l = 0; l < 8; ++l) acc[l] = fmaf(pa[8 * t + l], pb[8 * t + l], acc[l]);
-  const int64_t rem = bs & 7;
-  if (rem) {
-#pragma unroll
-    for (int l = 0; l < 8; ++l) {
-      const float xa = l < rem ? pa[8 * blocks + l] : 0.0f;
-      const float xb = l < rem ? pb[8 * blocks + l] : 0.0f;
-      acc[l] = fmaf(xa, xb, acc[l]);
-    }
-  }
-  const float s0 = acc[0] + acc[4], s1 = acc[1] + acc[5], s2 = acc[2] + acc[6],
-              s3 = acc[3] + acc[7];
-  return (s0 + s1) + (s2 + s3);
-}
-
-__global__ __launch_bounds__(TPB) void add_dots_blocks(float* __restrict__ dst,
-                                                       const float* __restrict__ a,
-                                                       const float* __restrict__ b,
-                                                       int64_t groups, int64_t N, int64_t bs) {
-  __shared__ float part[TPB];
-  const int64_t i = blockIdx.x;
-  float sum = 0.0f;
-  for (int64_t j0 = 0; j0 < groups; j0 += TPB) {
-    const int64_t jn = groups - j0 < TPB ? groups - j0 : TPB;
-    if (threadIdx.x < jn) {
-      const int64_t g = j0 + threadIdx.x;
-      part[threadIdx.x] = sdot8_block(a + (i + g * N) * bs, b + (i + g * N) * bs, bs);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int64_t jj = 0; jj < jn; ++jj) sum = sum + part[jj];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) dst[i] = dst[i] + sum;
-}
-
 __global__ void add_sums_seq(float* __restrict__ dst, const float* __restrict__ src,
                              int64_t groups, int64_t N) {
   const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
@@ -324,10 +177,33 @@ __device__ __forceinline__ float vssum8(const float* a, int64_t n) {  // vssum_a
   return r;
 }
 
+// sVarinceDelta_avx (ntensors.pas:8721-8757): 8 lanes of (x - mean) * delta
+// (sub, mul, add each rounded) over the full 8-blocks; with a tail, lanes
+// l+4 folded into l and the tail added to lane 0; then (x0+x1)+(x2+x3).  A
+// tail-less block skips the fold in the reference (lanes 4..7 dropped):
+// reproduced when quirk != 0, folded otherwise.
+__device__ __forceinline__ float var_delta8(const float* dd, const float* xx, int64_t n, float mu,
+                                            int quirk) {
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const int64_t blocks = n >> 3;
+  for (int64_t t = 0; t < blocks; ++t)
+#pragma unroll
+    for (int l = 0; l < 8; ++l) acc[l] = acc[l] + (xx[8 * t + l] - mu) * dd[8 * t + l];
+  float x0, x1, x2, x3;
+  if ((n & 7) == 0 && quirk) {
+    x0 = acc[0]; x1 = acc[1]; x2 = acc[2]; x3 = acc[3];
+  } else {
+    x0 = acc[0] + acc[4]; x1 = acc[1] + acc[5]; x2 = acc[2] + acc[6]; x3 = acc[3] + acc[7];
+    for (int64_t k = blocks * 8; k < n; ++k) x0 = x0 + (xx[k] - mu) * dd[k];
+  }
+  return (x0 + x1) + (x2 + x3);
+}
+
 __global__ void mean_var_delta_seq(const float* __restrict__ delta, const float* __restrict__ x,
                                    const float* __restrict__ mean, const float* __restrict__ var,
                                    int64_t groups, int64_t N, int64_t bs,
-                                   float* __restrict__ mean_delta, float* __restrict__ var_delta) {
+                                   float* __restrict__ mean_delta, float* __restrict__ var_delta,
+                                   int quirk) {
   const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= N) return;
   float m = 0.0f, v = 0.0f;
@@ -336,64 +212,12 @@ __global__ void mean_var_delta_seq(const float* __restrict__ delta, const float*
     const float* dd = delta + (i + j * N) * bs;
     const float* xx = x + (i + j * N) * bs;
     m = m + vssum8(dd, bs);
-    float t = 0.0f;
-    for (int64_t k = 0; k < bs; ++k) t = t + (xx[k] - mu) * dd[k];
-    v = v + t;
+    v = v + var_delta8(dd, xx, bs, mu, quirk);
   }
   const float ve = var[i] > SEPS ? var[i] : SEPS;
   const float inv = -1.0f / sqrtf(ve);
   mean_delta[i] = m * inv;
   var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
-}
-
-// conv blocks: one workgroup per channel, one thread per group — each
-// group's block sums (vssum8 of delta, the sequential (x-mu)*delta chain) are
-// independent; thread 0 adds them in group order as mean_var_delta_seq does
-__global__ __launch_bounds__(TPB) void mean_var_delta_blocks(
-    const float* __restrict__ delta, const float* __restrict__ x, const float* __restrict__ mean,
-    const float* __restrict__ var, int64_t groups, int64_t N, int64_t bs,
-    float* __restrict__ mean_delta, float* __restrict__ var_delta) {
-  __shared__ float ms[TPB], vs[TPB];
-  const int64_t i = blockIdx.x;
-  const float mu = mean[i];
-  float m = 0.0f, v = 0.0f;
-  for (int64_t j0 = 0; j0 < groups; j0 += TPB) {
-    const int64_t jn = groups - j0 < TPB ? groups - j0 : TPB;
-    if (threadIdx.x < jn) {
-      const int64_t j = j0 + threadIdx.x;
-      const float* dd = delta + (i + j * N) * bs;
-      const float* xx = x + (i + j * N) * bs;
-      ms[threadIdx.x] = vssum8(dd, bs);
-      // the chain is sequential; its operands are loaded MV_UNR ahead
-      float t = 0.0f;
-      int64_t k = 0;
-      for (; k + MV_UNR <= bs; k += MV_UNR) {
-        float xa[MV_UNR], da[MV_UNR];
-#pragma unroll
-        for (int u = 0; u < MV_UNR; ++u) {
-          xa[u] = xx[k + u];
-          da[u] = dd[k + u];
-        }
-#pragma unroll
-        for (int u = 0; u < MV_UNR; ++u) t = t + (xa[u] - mu) * da[u];
-      }
-      for (; k < bs; ++k) t = t + (xx[k] - mu) * dd[k];
-      vs[threadIdx.x] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0)
-      for (int64_t jj = 0; jj < jn; ++jj) {
-        m = m + ms[jj];
-        v = v + vs[jj];
-      }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    const float ve = var[i] > SEPS ? var[i] : SEPS;
-    const float inv = -1.0f / sqrtf(ve);
-    mean_delta[i] = m * inv;
-    var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
-  }
 }
 
 __global__ void normalize_delta_k(const float* __restrict__ x, const float* __restrict__ mean,
@@ -453,20 +277,215 @@ __global__ void vssum_k(int64_t n, const float* __restrict__ a, float* __restric
   if (blockIdx.x == 0 && threadIdx.x == 0) *out = vssum8(a, n);
 }
 
+
+// ---- conv-sized blocks: lane chains over one (group, channel) block ---------
+// The reference reduces every contiguous block with an AVX2 routine whose 8
+// lanes are strictly sequential chains (vssum_avx2, srss, sVarinceDelta_avx,
+// sdot_avx2), then adds the block results over the groups in order.  Only
+// groups x channels x 8 chains exist (2048 for YOLOv3's first layer at batch
+// 8, each 21632 long), so the chains cannot be the unit of memory traffic:
+// one workgroup per block streams it through LDS in coalesced tiles
+// (double-buffered, the next tile's loads in flight while the chains run),
+// the elementwise part (mean - x)^2 or (x - mean) * delta is formed by all
+// threads while staging (one rounding each, as vsubps / vmulps), and the
+// first 8 (or 16) lanes of wave 0 run the lane chains out of LDS.  The block
+// results go to part[block] (block = g*N + i, memory order) and a per-channel
+// pass adds them in group order.
+enum ChainMode { CH_SUM = 0, CH_SRSS = 1, CH_VDELTA = 2, CH_DOT = 3 };
+
+template <int MODE, int NT, int E>
+__global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
+                                                   const float* __restrict__ b,
+                                                   const float* __restrict__ mu_arr,
+                                                   int64_t nblocks, int64_t N, int64_t bs,
+                                                   int quirk, float* __restrict__ part0,
+                                                   float* __restrict__ part1) {
+  constexpr int TILE = NT * E;
+  constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;  // two LDS streams
+  __shared__ float U[2][TILE];
+  __shared__ float V[TWO ? 2 : 1][TWO ? TILE : 1];
+  const int tid = threadIdx.x;
+  const int l = tid & 7, grp = tid >> 3;  // chain lane, chain set (wave 0)
+  const bool chain = grp == 0 || (MODE == CH_VDELTA && grp == 1);
+  const int64_t nb8 = (bs >> 3) << 3;  // elements in full 8-blocks
+  const int ntile = (int)((nb8 + TILE - 1) / TILE);
+  const int tail = (int)(bs & 7);
+  for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    const int64_t i = blk % N;
+    const float* pa = a + blk * bs;
+    const float* pb = TWO ? b + blk * bs : nullptr;
+    const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA) ? mu_arr[i] : 0.0f;
+    float ra[E], rb[TWO ? E : 1];
+    auto load = [&](int t) {
+      const int64_t base = (int64_t)t * TILE + tid;
+#pragma unroll
+      for (int u = 0; u < E; ++u) {
+        const int64_t k = base + NT * u;
+        ra[u] = k < nb8 ? pa[k] : 0.0f;
+        if constexpr (TWO) rb[u] = k < nb8 ? pb[k] : 0.0f;
+      }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+      for (int u = 0; u < E; ++u) {
+        const int e = tid + NT * u;
+        if constexpr (MODE == CH_SUM) {
+          U[buf][e] = ra[u];
+        } else if constexpr (MODE == CH_SRSS) {  // srss: vsubps (mean - a), vmulps
+          const float d = mu - ra[u];
+          U[buf][e] = d * d;
+        } else if constexpr (MODE == CH_VDELTA) {  // a = delta, b = x
+          U[buf][e] = ra[u];
+          V[buf][e] = (rb[u] - mu) * ra[u];
+        } else {
+          U[buf][e] = ra[u];
+          V[buf][e] = rb[u];
+        }
+      }
+    };
+    float acc = 0.0f;
+    if (ntile > 0) {
+      load(0);
+      store(0);
+    }
+    __syncthreads();
+    for (int t = 0; t < ntile; ++t) {
+      if (t + 1 < ntile) load(t + 1);
+      if (tid < 64 && chain) {
+        const int64_t rem = nb8 - (int64_t)t * TILE;
+        const int cnt = (int)((rem < TILE ? rem : TILE) >> 3);
+        const float* row = ((MODE == CH_VDELTA && grp == 1) ? &V[t & 1][0] : &U[t & 1][0]) + l;
+        const float* rowb = TWO ? &V[t & 1][0] + l : row;
+        int q = 0;
+        for (; q + 16 <= cnt; q += 16) {
+          float v[16], w[16];
+#pragma unroll
+          for (int z = 0; z < 16; ++z) {
+            v[z] = row[8 * (q + z)];
+            if constexpr (MODE == CH_DOT) w[z] = rowb[8 * (q + z)];
+          }
+#pragma unroll
+          for (int z = 0; z < 16; ++z) {
+            if constexpr (MODE == CH_DOT) acc = fmaf(v[z], w[z], acc);
+            else acc = acc + v[z];
+          }
+        }
+        for (; q < cnt; ++q) {
+          if constexpr (MODE == CH_DOT) acc = fmaf(row[8 * q], rowb[8 * q], acc);
+          else acc = acc + row[8 * q];
+        }
+      }
+      if (t + 1 < ntile) store((t + 1) & 1);
+      __syncthreads();
+    }
+    if (tid < 64) {  // lane-order epilogues (8-lane groups of wave 0)
+      // vssum_avx2: fold, hadd, hadd, then the tail in order
+      // srss / sVarinceDelta_avx: fold (unless quirk and no tail), tail into
+      //   lane 0, hadd, hadd
+      // sdot_avx2: masked-FMA tail into lanes 0..tail-1, fold, hadd, hadd
+      const bool lanes_form = MODE == CH_SRSS || (MODE == CH_VDELTA && grp == 1);
+      if constexpr (MODE == CH_DOT) {
+        if (tail && grp == 0) {
+          const float xa = l < tail ? pa[nb8 + l] : 0.0f;
+          const float xb = l < tail ? pb[nb8 + l] : 0.0f;
+          acc = fmaf(xa, xb, acc);
+        }
+      }
+      const float up = __shfl_down(acc, 4, 8);
+      float x0 = (lanes_form && tail == 0 && quirk) ? acc : acc + up;
+      if (lanes_form && l == 0)
+        for (int k = 0; k < tail; ++k) {
+          if (MODE == CH_SRSS) {
+            const float d = mu - pa[nb8 + k];
+            x0 = x0 + d * d;
+          } else {
+            x0 = x0 + (pb[nb8 + k] - mu) * pa[nb8 + k];
+          }
+        }
+      const float h = x0 + __shfl_down(x0, 1, 8);
+      float r = h + __shfl_down(h, 2, 8);
+      if (l == 0 && chain) {
+        if (!lanes_form && MODE != CH_DOT)
+          for (int k = 0; k < tail; ++k) r = r + pa[nb8 + k];
+        if (grp == 0) part0[blk] = r;
+        else part1[blk] = r;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// per-channel passes: block results added over the groups in order
+enum FinMode { FIN_MEAN = 0, FIN_VAR = 1, FIN_VDELTA = 2, FIN_ADD = 3 };
+template <int MODE>
+__global__ void chains_finish(const float* __restrict__ part0, const float* __restrict__ part1,
+                              int64_t groups, int64_t N, int64_t bs, const float* __restrict__ var,
+                              float* __restrict__ out0, float* __restrict__ out1) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= N) return;
+  float m = 0.0f, v = 0.0f;
+  for (int64_t g = 0; g < groups; ++g) {
+    m = m + part0[g * N + i];
+    if (MODE == FIN_VDELTA) v = v + part1[g * N + i];
+  }
+  if (MODE == FIN_MEAN) {
+    out0[i] = m / (float)(groups * bs);
+  } else if (MODE == FIN_VAR) {
+    out0[i] = m / (float)(groups * bs - 1);
+  } else if (MODE == FIN_VDELTA) {
+    const float ve = var[i] > SEPS ? var[i] : SEPS;
+    const float inv = -1.0f / sqrtf(ve);
+    out0[i] = m * inv;
+    out1[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
+  } else {
+    out0[i] = out0[i] + m;
+  }
+}
+
+template <int MODE>
+hipError_t run_chains(const float* a, const float* b, const float* mu, int64_t groups, int64_t N,
+                      int64_t bs, int quirk, float* part0, float* part1, hipStream_t s) {
+  const int64_t nblocks = groups * N;
+  const unsigned grid = (unsigned)(nblocks < (1 << 20) ? nblocks : (1 << 20));
+  if (bs >= 4096)
+    hipLaunchKernelGGL((block_chains<MODE, 256, 16>), dim3(grid), dim3(256), 0, s, a, b, mu,
+                       nblocks, N, bs, quirk, part0, part1);
+  else
+    hipLaunchKernelGGL((block_chains<MODE, 64, 8>), dim3(grid), dim3(64), 0, s, a, b, mu, nblocks,
+                       N, bs, quirk, part0, part1);
+  return hipGetLastError();
+}
+
+template <int MODE>
+hipError_t run_finish(const float* part0, const float* part1, int64_t groups, int64_t N,
+                      int64_t bs, const float* var, float* out0, float* out1, hipStream_t s) {
+  hipLaunchKernelGGL(chains_finish<MODE>, dim3(nblk(N)), dim3(TPB), 0, s, part0, part1, groups,
+                     N, bs, var, out0, out1);
+  return hipGetLastError();
+}
+
+// blocks long enough for the chain kernels (shorter ones: one thread per
+// channel, which is also the only form for blockSize 1)
+bool use_chains(int64_t bs, const float* part) { return part != nullptr && bs >= 64; }
 }  // namespace
 
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
-                             float* vars, int quirk, hipStream_t s) {
+                             float* vars, int quirk, float* part, hipStream_t s) {
   if (N <= 0) return hipSuccess;
   // one thread per channel for FC shapes (blockSize 1) and short blocks;
-  // blocks of >= 64 use 8 lanes each (their chains are the reference's lanes)
-  if (bs == 1 || (bs < 64 && groups * bs <= kSeqMax))
+  // longer blocks: the lane chains per block, then the group-order sums
+  // (the variance pass needs the finished means)
+  if (!use_chains(bs, part)) {
     hipLaunchKernelGGL(means_vars_seq, dim3(nblk(N)), dim3(TPB), 0, s, x, groups, N, bs, means,
                        vars, quirk);
-  else
-    hipLaunchKernelGGL(means_vars_lanes, dim3((unsigned)N), dim3(TPB), 0, s, x, groups, N, bs,
-                       means, vars, quirk);
-  return hipGetLastError();
+    return hipGetLastError();
+  }
+  hipError_t e;
+  if ((e = run_chains<CH_SUM>(x, nullptr, nullptr, groups, N, bs, 0, part, nullptr, s)) ||
+      (e = run_finish<FIN_MEAN>(part, nullptr, groups, N, bs, nullptr, means, nullptr, s)) ||
+      (e = run_chains<CH_SRSS>(x, nullptr, means, groups, N, bs, quirk, part, nullptr, s)))
+    return e;
+  return run_finish<FIN_VAR>(part, nullptr, groups, N, bs, nullptr, vars, nullptr, s);
 }
 
 hipError_t launch_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
@@ -488,18 +507,19 @@ hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, con
 }
 
 hipError_t launch_add_dots(float* dst, const float* a, const float* b, int64_t groups, int64_t N,
-                           int64_t bs, hipStream_t s) {
+                           int64_t bs, float* part, hipStream_t s) {
   if (N <= 0) return hipSuccess;
-  if (bs >= 64 && N <= 0x7fffffffLL)
-    hipLaunchKernelGGL(add_dots_blocks, dim3((unsigned)N), dim3(TPB), 0, s, dst, a, b, groups, N,
-                       bs);
-  else
+  if (!use_chains(bs, part)) {
     hipLaunchKernelGGL(add_dots_seq, dim3(nblk(N)), dim3(TPB), 0, s, dst, a, b, groups, N, bs);
-  return hipGetLastError();
+    return hipGetLastError();
+  }
+  if (hipError_t e = run_chains<CH_DOT>(a, b, nullptr, groups, N, bs, 0, part, nullptr, s))
+    return e;
+  return run_finish<FIN_ADD>(part, nullptr, groups, N, bs, nullptr, dst, nullptr, s);
 }
 
 hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs,
-                           hipStream_t s) {
+                           float* part, hipStream_t s) {
   if (N <= 0) return hipSuccess;
   if (bs == 1 && N == 1)  // stride 1: sumv is vssum_avx2 over the groups
     return launch_backward_bias(dst, 1, src, groups, 1, 1, s);
@@ -507,20 +527,27 @@ hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t
     hipLaunchKernelGGL(add_sums_seq, dim3(nblk(N)), dim3(TPB), 0, s, dst, src, groups, N);
     return hipGetLastError();
   }
-  return launch_backward_bias(dst, N, src, bs, groups, 1, s);
+  if (!use_chains(bs, part)) return launch_backward_bias(dst, N, src, bs, groups, 1, s);
+  if (hipError_t e = run_chains<CH_SUM>(src, nullptr, nullptr, groups, N, bs, 0, part, nullptr, s))
+    return e;
+  return run_finish<FIN_ADD>(part, nullptr, groups, N, bs, nullptr, dst, nullptr, s);
 }
 
 hipError_t launch_mean_var_delta(const float* delta, const float* x, const float* mean,
                                  const float* var, int64_t groups, int64_t N, int64_t bs,
-                                 float* mean_delta, float* var_delta, hipStream_t s) {
+                                 float* mean_delta, float* var_delta, int quirk, float* part,
+                                 hipStream_t s) {
   if (N <= 0) return hipSuccess;
-  if (bs >= 64 && N <= 0x7fffffffLL)
-    hipLaunchKernelGGL(mean_var_delta_blocks, dim3((unsigned)N), dim3(TPB), 0, s, delta, x, mean,
-                       var, groups, N, bs, mean_delta, var_delta);
-  else
+  if (!use_chains(bs, part)) {
     hipLaunchKernelGGL(mean_var_delta_seq, dim3(nblk(N)), dim3(TPB), 0, s, delta, x, mean, var,
-                       groups, N, bs, mean_delta, var_delta);
-  return hipGetLastError();
+                       groups, N, bs, mean_delta, var_delta, quirk);
+    return hipGetLastError();
+  }
+  float* part1 = part + groups * N;
+  if (hipError_t e =
+          run_chains<CH_VDELTA>(delta, x, mean, groups, N, bs, quirk, part, part1, s))
+    return e;
+  return run_finish<FIN_VDELTA>(part, part1, groups, N, bs, var, mean_delta, var_delta, s);
 }
 
 hipError_t launch_normalize_delta(const float* x, const float* mean, const float* var,

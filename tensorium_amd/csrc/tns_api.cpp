@@ -56,9 +56,11 @@ struct tns_ctx {
   bool own_stream = false;
   // device scratch (im2col workspace, host-API staging)
   // 0 col workspace, 1 padded images / host staging, 2-3 host staging,
-  // 4 per-image dW partial sums of the conv backward
-  float* scratch[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-  size_t scratch_elems[5] = {0, 0, 0, 0, 0};
+  // 4 per-image dW partial sums of the conv backward, 5 per-block results of
+  // the batch-norm reductions
+  static constexpr int kSlots = 8;
+  float* scratch[kSlots] = {};
+  size_t scratch_elems[kSlots] = {};
   // telemetry (TTensorMetrics-style, nopmetrics.pas:25-44)
   bool telemetry = false;
   double op_ms[TNS_OP_COUNT] = {0};
@@ -69,6 +71,8 @@ struct tns_ctx {
 };
 
 namespace {
+
+enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5 };
 
 int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   if (elems < 1) elems = 1;
@@ -290,7 +294,7 @@ int tns_hip_destroy(tns_ctx* c) {
   if (!c) return TNS_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
-  for (int i = 0; i < 5; ++i)
+  for (int i = 0; i < tns_ctx::kSlots; ++i)
     if (c->scratch[i]) hipFree(c->scratch[i]);
   for (auto& kv : c->ktabs) hipFree(kv.second);
   if (c->ev0) hipEventDestroy(c->ev0);
@@ -444,8 +448,14 @@ int tns_hip_backward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t srcSi
   const int64_t bs = srcSize / (dstSize * batch);
   OpTimer t(c, TNS_OP_BIAS);
   if (bs == 1 && incb == 1)  // FC layers: the reference's sequential strided sum
-    return hip_status(launch_add_sums(dst, src + srcOffset, batch, dstSize, 1, c->stream),
+    return hip_status(launch_add_sums(dst, src + srcOffset, batch, dstSize, 1, nullptr, c->stream),
                       "backwardBias launch");
+  if (incb == 1 && bs >= 64) {  // conv blocks: lane chains per block
+    float* part;
+    if (int r = ensure_scratch(c, SLOT_BN, batch * dstSize, &part)) return r;
+    return hip_status(launch_add_sums(dst, src + srcOffset, batch, dstSize, bs, part, c->stream),
+                      "backwardBias launch");
+  }
   return hip_status(launch_backward_bias(dst, dstSize, src + srcOffset, bs, batch, incb, c->stream),
                     "backwardBias launch");
 }
@@ -562,8 +572,10 @@ int tns_hip_means_and_vars(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t
   int64_t bs;
   if (int r = blocks_of(srcSize, dstSize, groups, &bs, "meansAndVars")) return r;
   if (!src || !means || !vars) return set_error(TNS_ERR_ARG, "meansAndVars: null pointer");
+  float* part;
+  if (int r = ensure_scratch(c, SLOT_BN, 2 * groups * dstSize, &part)) return r;
   return hip_status(launch_means_vars(src + offset, groups, dstSize, bs, means, vars,
-                                      (int)g_srss_quirk, c->stream),
+                                      (int)g_srss_quirk, part, c->stream),
                     "meansAndVars");
 }
 
@@ -604,8 +616,13 @@ int tns_hip_means_and_vars_delta(tns_ctx* c, int64_t srcSize, int64_t dstSize, i
   if (int r = check_ctx(c)) return r;
   int64_t bs;
   if (int r = blocks_of(srcSize, dstSize, groups, &bs, "meansAndVarsDelta")) return r;
+  if (!delta || !x || !mean || !variance || !mean_delta || !variance_delta)
+    return set_error(TNS_ERR_ARG, "meansAndVarsDelta: null pointer");
+  float* part;
+  if (int r = ensure_scratch(c, SLOT_BN, 2 * groups * dstSize, &part)) return r;
   return hip_status(launch_mean_var_delta(delta + offset, x + offset, mean, variance, groups,
-                                          dstSize, bs, mean_delta, variance_delta, c->stream),
+                                          dstSize, bs, mean_delta, variance_delta,
+                                          (int)g_srss_quirk, part, c->stream),
                     "meansAndVarsDelta");
 }
 
@@ -616,6 +633,8 @@ int tns_hip_normalize_delta(tns_ctx* c, int64_t deltaSize, int64_t meanSize, int
   if (int r = check_ctx(c)) return r;
   int64_t bs;
   if (int r = blocks_of(deltaSize, meanSize, groups, &bs, "normalizeDelta")) return r;
+  if (!delta || !x || !mean || !variance || !mean_delta || !variance_delta)
+    return set_error(TNS_ERR_ARG, "normalizeDelta: null pointer");
   return hip_status(launch_normalize_delta(x + offset, mean, variance, mean_delta,
                                            variance_delta, delta + offset, groups, meanSize, bs,
                                            c->stream),
@@ -627,8 +646,11 @@ int tns_hip_add_dots(tns_ctx* c, int64_t N, int64_t dstSize, int64_t groups, con
   if (int r = check_ctx(c)) return r;
   int64_t bs;
   if (int r = blocks_of(N, dstSize, groups, &bs, "addDots")) return r;
+  if (!dst || !src1 || !src2) return set_error(TNS_ERR_ARG, "addDots: null pointer");
+  float* part;
+  if (int r = ensure_scratch(c, SLOT_BN, 2 * groups * dstSize, &part)) return r;
   return hip_status(launch_add_dots(dst, src1 + srcOffset, src2 + srcOffset, groups, dstSize, bs,
-                                    c->stream),
+                                    part, c->stream),
                     "addDots");
 }
 
@@ -902,8 +924,10 @@ int tns_hip_conv_backward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64
                                        c->stream), "derive launch"))
     return r;
   // bias_updates.addSums(delta)
-  if (int r = hip_status(launch_add_sums(bias_updates, delta, batch, filters, i_k, c->stream),
-                         "addSums launch"))
+  float* part;
+  if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
+  if (int r = hip_status(launch_add_sums(bias_updates, delta, batch, filters, i_k, part,
+                                         c->stream), "addSums launch"))
     return r;
   // state.input.im2Col(...) — a 1x1/s1/p0 col matrix is the input itself
   const bool needs_col = kSize != 1 || stride != 1 || padding != 0;

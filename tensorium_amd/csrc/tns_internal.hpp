@@ -146,19 +146,23 @@ hipError_t launch_clamp(int64_t n, float alpha, const float* src, float* dst, in
 // ---- batch-norm / softmax (batchnorm.hip) ----------------------------------
 // x laid out [groups][N][bs]; one statistic per channel i in [0, N)
 // quirk != 0: srss drops lanes 4..7 of tail-less blocks, as the reference
+// part: device scratch of >= 2*groups*N floats for per-block results (conv
+// blocks, bs >= 64, take the lane-chain kernels with it); nullptr = the
+// one-thread-per-channel kernels only
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
-                             float* vars, int quirk, hipStream_t s);
+                             float* vars, int quirk, float* part, hipStream_t s);
 hipError_t launch_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
                             int64_t mstride, const float* vars, int64_t vstride, hipStream_t s);
 hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales,
                             const float* biases, int64_t incb, hipStream_t s);
 hipError_t launch_add_dots(float* dst, const float* a, const float* b, int64_t groups, int64_t N,
-                           int64_t bs, hipStream_t s);
+                           int64_t bs, float* part, hipStream_t s);
 hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs,
-                           hipStream_t s);
+                           float* part, hipStream_t s);
 hipError_t launch_mean_var_delta(const float* delta, const float* x, const float* mean,
                                  const float* var, int64_t groups, int64_t N, int64_t bs,
-                                 float* mean_delta, float* var_delta, hipStream_t s);
+                                 float* mean_delta, float* var_delta, int quirk, float* part,
+                                 hipStream_t s);
 hipError_t launch_normalize_delta(const float* x, const float* mean, const float* var,
                                   const float* mean_delta, const float* var_delta, float* delta,
                                   int64_t groups, int64_t N, int64_t bs, hipStream_t s);

@@ -188,6 +188,96 @@ def add_bias(x, bias, F_, bs, batch):
     return x
 
 
+def vssum(a):
+    """vssum_avx2 (ntensors.pas:3592-3620): 8 lanes over the full 8-blocks,
+    lane_l + lane_{l+4}, haddps twice, then the remainder in order."""
+    acc = [Fraction(0)] * 8
+    nb = len(a) // 8
+    for t in range(nb):
+        for l in range(8):
+            acc[l] = add(acc[l], a[8 * t + l])
+    s = [add(acc[l], acc[l + 4]) for l in range(4)]
+    r = add(add(s[0], s[1]), add(s[2], s[3]))
+    for v in a[8 * nb:]:
+        r = add(r, v)
+    return r
+
+
+def lanes_tail_fold(acc, tail_terms, quirk):
+    """Common epilogue of srss (ntensors.pas:1508-1523) and sVarinceDelta_avx
+    (8738-8756): with a tail, fold lanes l+4 into l and add the tail terms to
+    lane 0; without one the fold is skipped (lanes 4..7 dropped) when quirk."""
+    if not tail_terms and quirk:
+        x = list(acc[:4])
+    else:
+        x = [add(acc[l], acc[l + 4]) for l in range(4)]
+        for t in tail_terms:
+            x[0] = add(x[0], t)
+    return add(add(x[0], x[1]), add(x[2], x[3]))
+
+
+def srss(mean, a, quirk):
+    """srss (ntensors.pas:1493-1523): lanes of (mean - a)^2."""
+    acc = [Fraction(0)] * 8
+    nb = len(a) // 8
+    for t in range(nb):
+        for l in range(8):
+            d = f32(mean - a[8 * t + l])
+            acc[l] = add(acc[l], mul(d, d))
+    tail = []
+    for v in a[8 * nb:]:
+        d = f32(mean - v)
+        tail.append(mul(d, d))
+    return lanes_tail_fold(acc, tail, quirk)
+
+
+def var_delta_avx(mean, delta, x, quirk):
+    """sVarinceDelta_avx (ntensors.pas:8721-8757): lanes of (x - mean)*delta."""
+    acc = [Fraction(0)] * 8
+    nb = len(x) // 8
+    for t in range(nb):
+        for l in range(8):
+            k = 8 * t + l
+            acc[l] = add(acc[l], mul(f32(x[k] - mean), delta[k]))
+    tail = [mul(f32(x[k] - mean), delta[k]) for k in range(8 * nb, len(x))]
+    return lanes_tail_fold(acc, tail, quirk)
+
+
+def mean_var_delta_sums(delta, x, mean, groups, N, bs, quirk):
+    """sMeanAndVarianceDelta (ntensors.pas:8831-8871) before the final
+    scaling: per channel m = sum_j vsSumI(block), v = sum_j
+    sVarinceDelta_avx(block), groups in order."""
+    ms, vs = [], []
+    for i in range(N):
+        m = v = Fraction(0)
+        for j in range(groups):
+            o = (i + j * N) * bs
+            m = add(m, vssum(delta[o:o + bs]))
+            v = add(v, var_delta_avx(mean[i], delta[o:o + bs], x[o:o + bs], quirk))
+        ms.append(m)
+        vs.append(v)
+    return ms, vs
+
+
+def means_and_vars(x, groups, N, bs, quirk):
+    """MeansAndVars (ntensors.pas:9102-9177) with vssum_avx2 / srss blocks."""
+    S, S2 = F(groups * bs), F(groups * bs - 1)
+    ms, vs = [], []
+    for i in range(N):
+        m = Fraction(0)
+        for j in range(groups):
+            o = (i + j * N) * bs
+            m = add(m, vssum(x[o:o + bs]))
+        m = f32(m / S)
+        v = Fraction(0)
+        for j in range(groups):
+            o = (i + j * N) * bs
+            v = add(v, srss(m, x[o:o + bs], quirk))
+        ms.append(m)
+        vs.append(f32(v / S2))
+    return ms, vs
+
+
 # ---------------------------------------------------------------- cases
 def rnd(rng, n, lo=-1.0, hi=1.0):
     v = rng.uniform(lo, hi, n).astype(np.float32)
@@ -265,6 +355,29 @@ def main() -> None:
     g["bias_out"] = to_np(yb)
     g["leaky_out"] = to_np(leaky(yb))
     g["relu_out"] = to_np(relu(yb))
+
+    # batch-norm block reductions: vssum / srss / sVarinceDelta_avx lane
+    # orders, tail and tail-less blocks, both settings of the quirk
+    for n in (5, 8, 13, 16, 37, 64, 67):
+        a, aq = rnd(rng, n, -2.0, 3.0)
+        d, dq = rnd(rng, n)
+        mu, muq = rnd(rng, 1, -0.5, 0.5)
+        g[f"bn_{n}_a"], g[f"bn_{n}_d"], g[f"bn_{n}_mu"] = a, d, mu
+        g[f"bn_{n}_vssum"] = to_np([vssum(aq)])
+        for q in (0, 1):
+            g[f"bn_{n}_srss_q{q}"] = to_np([srss(muq[0], aq, q)])
+            g[f"bn_{n}_vdelta_q{q}"] = to_np([var_delta_avx(muq[0], dq, aq, q)])
+    for gi, (groups, N, bs) in enumerate([(3, 2, 16), (2, 3, 13), (4, 1, 9)]):
+        n = groups * N * bs
+        x, xq = rnd(rng, n, -2.0, 2.0)
+        d, dq = rnd(rng, n)
+        g[f"bnc_{gi}_dims"] = np.array([groups, N, bs], np.int64)
+        g[f"bnc_{gi}_x"], g[f"bnc_{gi}_d"] = x, d
+        for q in (0, 1):
+            m, v = means_and_vars(xq, groups, N, bs, q)
+            g[f"bnc_{gi}_mean_q{q}"], g[f"bnc_{gi}_var_q{q}"] = to_np(m), to_np(v)
+            ms, vs = mean_var_delta_sums(dq, xq, m, groups, N, bs, q)
+            g[f"bnc_{gi}_msum_q{q}"], g[f"bnc_{gi}_vsum_q{q}"] = to_np(ms), to_np(vs)
 
     np.savez_compressed(OUT, **g)
     print(f"wrote {OUT} ({len(g)} arrays)")

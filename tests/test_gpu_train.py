@@ -17,7 +17,8 @@ def dev(torch, x):
 
 
 @pytest.mark.parametrize("groups,N,bs", [(32, 64, 1), (32, 10, 1), (4, 8, 9), (2, 3, 2704),
-                                         (8, 16, 2704), (3, 4, 1029), (1100, 2, 9)])
+                                         (8, 16, 2704), (3, 4, 1029), (1100, 2, 9),
+                                         (8, 4, 173056), (8, 5, 169), (6, 3, 64)])
 def test_means_vars_normalize_scale(hip, torch_cuda, ora, groups, N, bs):
     x = ora.uniform(groups * N * bs, 21, N, -2.0, 3.0)
     m, v = ora.means_and_vars(x, groups, N, bs)
@@ -40,7 +41,7 @@ def test_means_vars_normalize_scale(hip, torch_cuda, ora, groups, N, bs):
     assert np.array_equal(dx.cpu().numpy(), y2)
 
 
-@pytest.mark.parametrize("groups,N,bs", [(4, 8, 16), (8, 16, 2704), (3, 5, 24)])
+@pytest.mark.parametrize("groups,N,bs", [(4, 8, 16), (8, 16, 2704), (3, 5, 24), (8, 2, 173056)])
 def test_means_vars_srss_quirk(hip, torch_cuda, ora, groups, N, bs):
     """TNS_OPT_SRSS_QUIRK: blocks a multiple of 8 long lose lanes 4..7 of the
     variance sum, as the reference's srss does; off by default."""
@@ -60,30 +61,56 @@ def test_means_vars_srss_quirk(hip, torch_cuda, ora, groups, N, bs):
         assert np.array_equal(dm.cpu().numpy(), m) and np.array_equal(dv.cpu().numpy(), v)
 
 
-@pytest.mark.parametrize("groups,N,bs", [(32, 64, 1), (4, 8, 9), (8, 16, 2704), (300, 3, 65),
-                                         (2, 5, 1029)])
-def test_bn_backward_ops(hip, torch_cuda, ora, groups, N, bs):
+BN_BWD = [(32, 64, 1), (4, 8, 9), (8, 16, 2704), (300, 3, 65), (2, 5, 1029), (3, 4, 16),
+          (8, 4, 173056), (2, 3, 43264), (8, 6, 169), (5, 2, 64)]
+
+
+@pytest.mark.parametrize("quirk", [0, 1])
+@pytest.mark.parametrize("groups,N,bs", BN_BWD)
+def test_bn_backward_ops(hip, torch_cuda, ora, groups, N, bs, quirk):
+    """batchNormBack's reductions (addDots, sMeanAndVarianceDelta with the
+    sVarinceDelta_avx lane order, sNormalizeDelta) bit-exact, with and
+    without the reference's tail-less lane drop (TNS_OPT_SRSS_QUIRK)."""
     n = groups * N * bs
     x = ora.uniform(n, 31, N, -2.0, 2.0)
-    m, v = ora.means_and_vars(x, groups, N, bs)
+    m, v = ora.means_and_vars(x, groups, N, bs, quirk=quirk)
     xn = ora.normalize(x.copy(), groups, N, bs, m, v)
     delta = ora.uniform(n, 32, N)
     dsc = ora.uniform(N, 33, N)
     ref_dsc = ora.add_dots(dsc.copy(), xn, delta, groups, N, bs)
-    md, vd = ora.mean_var_delta(delta, x, m, v, groups, N, bs)
+    md, vd = ora.mean_var_delta(delta, x, m, v, groups, N, bs, quirk=quirk)
     ref_delta = ora.normalize_delta(x, m, v, md, vd, delta.copy(), groups, N, bs)
     T = torch_cuda
     d_dsc = dev(T, dsc)
-    hip.addDots(n, N, groups, dev(T, xn), dev(T, delta), 0, d_dsc)
     dmd, dvd = T.zeros(N, device="cuda"), T.zeros(N, device="cuda")
     d_delta = dev(T, delta)
-    hip.meansAndVarsDelta(n, N, groups, d_delta, dev(T, x), 0, dev(T, m), dev(T, v), dmd, dvd)
-    hip.normalizeDelta(n, N, groups, d_delta, dev(T, x), 0, dev(T, m), dev(T, v), dmd, dvd)
+    hip.setSrssQuirk(bool(quirk))
+    try:
+        hip.addDots(n, N, groups, dev(T, xn), dev(T, delta), 0, d_dsc)
+        hip.meansAndVarsDelta(n, N, groups, d_delta, dev(T, x), 0, dev(T, m), dev(T, v), dmd, dvd)
+        hip.normalizeDelta(n, N, groups, d_delta, dev(T, x), 0, dev(T, m), dev(T, v), dmd, dvd)
+        hip.finish()
+    finally:
+        hip.setSrssQuirk(False)
+    assert np.array_equal(d_dsc.cpu().numpy(), ref_dsc), "addDots"
+    assert np.array_equal(dmd.cpu().numpy(), md), "mean_delta"
+    assert np.array_equal(dvd.cpu().numpy(), vd), "variance_delta"
+    assert np.array_equal(d_delta.cpu().numpy(), ref_delta), "normalizeDelta"
+    if bs % 8 == 0 and bs >= 8:  # the quirk must matter on tail-less blocks
+        md2, vd2 = ora.mean_var_delta(delta, x, m, v, groups, N, bs, quirk=1 - quirk)
+        assert not np.array_equal(vd, vd2)
+
+
+@pytest.mark.parametrize("groups,N,bs", [(8, 4, 173056), (8, 16, 2704), (3, 5, 169), (2, 7, 65)])
+def test_conv_block_bias_sums(hip, torch_cuda, ora, groups, N, bs):
+    """addSums over conv blocks (backwardBias, bs >= 64: lane-chain path)."""
+    src = ora.uniform(groups * N * bs, 53, 0)
+    dst = ora.uniform(N, 54, 0)
+    ref = ora.add_sums(dst.copy(), src, groups, N, bs)
+    d = dev(torch_cuda, dst)
+    hip.backwardBias(N, d, src.size, dev(torch_cuda, src), 0, 1, groups)
     hip.finish()
-    assert np.array_equal(d_dsc.cpu().numpy(), ref_dsc)
-    assert np.array_equal(dmd.cpu().numpy(), md)
-    assert np.array_equal(dvd.cpu().numpy(), vd), "vd"
-    assert np.array_equal(d_delta.cpu().numpy(), ref_delta), "ndelta"
+    assert np.array_equal(d.cpu().numpy(), ref)
 
 
 def test_softmax_xent_sum(hip, torch_cuda, ora):
@@ -195,3 +222,15 @@ def test_sgd_update_fused(hip, torch_cuda, ora, nw, n, bn, offset):
     for x, r in zip(g, ref):
         if r is not None:
             assert np.array_equal(x.cpu().numpy(), r)
+
+
+def test_bn_null_pointers_are_arg_errors(hip, torch_cuda):
+    """A null pointer from the binding is TNS_ERR_ARG (1), not a GPU fault."""
+    L, T = hip.lib, torch_cuda
+    x = T.zeros(64, device="cuda")
+    p = x.data_ptr()
+    assert L.tns_hip_means_and_vars_delta(hip.ctx, 64, 4, 2, None, p, 0, p, p, p, p) == 1
+    assert L.tns_hip_normalize_delta(hip.ctx, 64, 4, 2, p, None, 0, p, p, p, p) == 1
+    assert L.tns_hip_add_dots(hip.ctx, 64, 4, 2, p, None, 0, p) == 1
+    assert L.tns_hip_means_and_vars(hip.ctx, 64, 4, 2, None, 0, p, p) == 1
+    hip.finish()

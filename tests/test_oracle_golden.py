@@ -84,3 +84,53 @@ def test_bias_and_activations(ora, golden):
     y = x.copy()
     ora.activate(y, 1)
     assert eq(y, golden["relu_out"])
+
+
+BN_N = [5, 8, 13, 16, 37, 64, 67]
+
+
+@pytest.mark.parametrize("n", BN_N)
+@pytest.mark.parametrize("quirk", [0, 1])
+def test_bn_block_reductions_golden(ora, golden, n, quirk):
+    """vssum_avx2 / srss / sVarinceDelta_avx over one block, in the
+    reference's lane order, with and without the tail-less lane drop."""
+    a, d, mu = golden[f"bn_{n}_a"], golden[f"bn_{n}_d"], float(golden[f"bn_{n}_mu"][0])
+    assert np.float32(ora.vssum(a)) == golden[f"bn_{n}_vssum"][0]
+    assert np.float32(ora.srss(mu, a, quirk)) == golden[f"bn_{n}_srss_q{quirk}"][0]
+    assert np.float32(ora.var_delta_avx(mu, d, a, quirk)) == golden[f"bn_{n}_vdelta_q{quirk}"][0]
+
+
+def test_var_delta_lane_order_matters(ora, golden):
+    """The 8-lane order is not a sequential chain on at least one block, and
+    the quirk changes tail-less blocks only."""
+    diffs = 0
+    for n in BN_N:
+        a, d, mu = golden[f"bn_{n}_a"], golden[f"bn_{n}_d"], np.float32(golden[f"bn_{n}_mu"][0])
+        s = np.float32(0)
+        for x, y in zip(a, d):
+            s = np.float32(s + np.float32(np.float32(x - mu) * y))
+        diffs += int(s != golden[f"bn_{n}_vdelta_q0"][0])
+        q0, q1 = golden[f"bn_{n}_vdelta_q0"][0], golden[f"bn_{n}_vdelta_q1"][0]
+        if n % 8:
+            assert q0 == q1
+    assert diffs >= 1
+    assert golden["bn_64_vdelta_q0"][0] != golden["bn_64_vdelta_q1"][0]
+
+
+@pytest.mark.parametrize("gi", range(3))
+@pytest.mark.parametrize("quirk", [0, 1])
+def test_bn_channel_statistics_golden(ora, golden, gi, quirk):
+    """MeansAndVars and sMeanAndVarianceDelta over [groups][N][bs] tensors:
+    block sums added in group order; mean_delta / variance_delta are the
+    golden sums scaled as ntensors.pas:8869-8870 (Power in double)."""
+    groups, N, bs = (int(v) for v in golden[f"bnc_{gi}_dims"])
+    x, d = golden[f"bnc_{gi}_x"], golden[f"bnc_{gi}_d"]
+    m, v = ora.means_and_vars(x, groups, N, bs, quirk=quirk)
+    assert eq(m, golden[f"bnc_{gi}_mean_q{quirk}"]) and eq(v, golden[f"bnc_{gi}_var_q{quirk}"])
+    md, vd = ora.mean_var_delta(d, x, m, v, groups, N, bs, quirk=quirk)
+    ve = np.maximum(v, np.float32(1e-6)).astype(np.float32)
+    inv = (np.float32(-1.0) / np.sqrt(ve)).astype(np.float32)
+    assert eq(md, (golden[f"bnc_{gi}_msum_q{quirk}"] * inv).astype(np.float32))
+    vref = (golden[f"bnc_{gi}_vsum_q{quirk}"].astype(np.float64) * -0.5
+            * np.power(ve.astype(np.float64), -1.5)).astype(np.float32)
+    assert eq(vd, vref)
