@@ -233,16 +233,45 @@ int tns_hip_copy(tns_ctx* ctx, int64_t N, const float* src, int64_t srcOffset, i
                  float* dst, int64_t dstOffset, int64_t incb);
 int tns_hip_clamp(tns_ctx* ctx, int64_t N, float alpha, const float* src, float* dst,
                   int64_t stride, int64_t offset);
+/* TNNCuda.addvv / subvv / mulvv / fmavv (nncuda.pas:120-123):
+ * dst[i*incc] = src1[i*inca] op src2[i*incb] (offsets in elements); fmavv:
+ * src1*src2 rounded, then + src3 rounded (no fused multiply-add, as the CPU
+ * sfmavss).  fmavss (nncuda.pas:137): dst = src*scalar + bias over N
+ * contiguous elements at offset.  inverseSqrt (nncuda.pas:151):
+ * dst = 1/sqrt(max(src, 1e-6)) strided; alpha unused (as the reference). */
+int tns_hip_addvv(tns_ctx* ctx, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, float* dst,
+                  int64_t dstOffset, int64_t incc);
+int tns_hip_subvv(tns_ctx* ctx, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, float* dst,
+                  int64_t dstOffset, int64_t incc);
+int tns_hip_mulvv(tns_ctx* ctx, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, float* dst,
+                  int64_t dstOffset, int64_t incc);
+int tns_hip_fmavv(tns_ctx* ctx, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, const float* src3,
+                  int64_t src3Offset, int64_t incc, float* dst, int64_t dstOffset,
+                  int64_t incd);
+int tns_hip_fmavss(tns_ctx* ctx, int64_t N, const float* src, int64_t offset, float scalar,
+                   float bias, float* dst);
+int tns_hip_inverse_sqrt(tns_ctx* ctx, int64_t N, float alpha, const float* src, float* dst,
+                         int64_t stride, int64_t offset);
 
 /* ---- non-convolutional YOLOv3 layers (forward) ------------------------- */
 /* TAddLayer.forward (naddlayer.pas:667-720), single input of equal size:
  * out = activate(a + b) (addvv, then the layer's activation). */
 int tns_hip_shortcut(tns_ctx* ctx, int64_t N, const float* a, int64_t aOffset, const float* b,
                      int64_t bOffset, float* out, int64_t outOffset, int32_t activation);
-/* upsample() forward (nupsamplelayer.pas:83-113): planes = batch*channels,
- * out[(p*H*s + y)*W*s + x] = scale * in[(p*H + y div s)*W + x div s]. */
-int tns_hip_upsample(tns_ctx* ctx, int64_t planes, int64_t H, int64_t W, int64_t stride,
-                     float scale, const float* in, float* out);
+/* TNNCuda.upSample (nncuda.pas:136, 1267-1286; CPU upsample()
+ * nupsamplelayer.pas:83-113).  outHeight/outWidth are the SMALL tensor's
+ * height and width (the reference's naming); planes = aBatch*aChannels.
+ * isForward != 0: out[(p*H*s + y)*W*s + x] = scale * in[(p*H + y div s)*W + x div s].
+ * isForward == 0: in[...] += scale*out[...] over each input pixel's s x s
+ * outputs in the CPU loop order (row outer), deterministic; zeroIn != 0
+ * starts from 0 (the reverse layer's output.fill(0)). */
+int tns_hip_upsample(tns_ctx* ctx, int64_t aBatch, int64_t aChannels, int64_t outHeight,
+                     int64_t outWidth, float* in, int64_t stride, int32_t isForward, float scale,
+                     float* out, int32_t zeroIn);
 /* TYoloLayer.forward inference part (nyololayer.pas:786-825): out = in with
  * the logistic applied to entries 0, 1 and 4 .. 4+classes of every anchor;
  * data [batch][anchors][classes+5][hw].  (Route/concat = tns_hip_copy of
@@ -345,9 +374,26 @@ int tns_hip_conv_backward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int
                           float* bias_updates, float* weight_updates, float* workspace,
                           float* state_delta);
 
-/* Multi-GPU batched GEMM (config 4): batchCount independent GEMMs on the
- * caller's device; sharding across ranks is done by the caller (one process
- * per GPU) — see bench.py.  Provided for completeness with the ctx API. */
+/* ---- several GPUs from ONE process (config 4) ---------------
+ * gemmStridedBatched over n devices (devices[i] for slot i; a device may
+ * appear twice): HOST pointers, as the op-table gemmStridedBatched
+ * (ntensors.pas:348-351), cblas_sgemm semantics.  The batch is split into n
+ * contiguous shards (the first batchCount % n one GEMM longer); each slot
+ * has its own context, stream and host thread and pipelines its shard's
+ * uploads, GEMMs and downloads.  A shared operand (strideA or strideB = 0,
+ * the conv weights of nConvolutionLayer.pas:773) crosses PCIe once, to slot
+ * 0, and reaches the other devices by peer copies (xGMI).  Results are bit
+ * identical to the single-device call.  Returns a status. */
+int tns_hip_sgemm_strided_batched_multi(const int32_t* devices, int32_t n, uint8_t transA,
+                                        uint8_t transB, int64_t M, int64_t N, int64_t K,
+                                        float alpha, const float* A, int64_t lda,
+                                        int64_t strideA, const float* B, int64_t ldb,
+                                        int64_t strideB, float beta, float* C, int64_t ldc,
+                                        int64_t strideC, int64_t batchCount);
+/* Spread the op-table drop-ins tns_cblas_sgemm_batch_strided / tns_cblas_sgemm
+ * over these devices (n <= 1: the default single context again), so an
+ * unmodified Pascal binding drives several GPUs. */
+int tns_set_op_devices(const int32_t* devices, int32_t n);
 
 /* ---- telemetry (TTensorMetrics-style per-op device timing) ------------ */
 int    tns_hip_set_telemetry(tns_ctx* ctx, int32_t enable);

@@ -146,7 +146,18 @@ def check(rc: int) -> None:
 
 PROTOTYPES.update({
     "tns_hip_shortcut": (C.c_int, [vp, i64, fptr, i64, fptr, i64, fptr, i64, i32]),
-    "tns_hip_upsample": (C.c_int, [vp, i64, i64, i64, i64, f32, fptr, fptr]),
+    "tns_hip_upsample": (C.c_int, [vp, i64, i64, i64, i64, fptr, i64, i32, f32, fptr, i32]),
+    "tns_hip_addvv": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64, fptr, i64, i64]),
+    "tns_hip_subvv": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64, fptr, i64, i64]),
+    "tns_hip_mulvv": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64, fptr, i64, i64]),
+    "tns_hip_fmavv": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64, fptr, i64, i64, fptr,
+                                i64, i64]),
+    "tns_hip_fmavss": (C.c_int, [vp, i64, fptr, i64, f32, f32, fptr]),
+    "tns_hip_inverse_sqrt": (C.c_int, [vp, i64, f32, fptr, fptr, i64, i64]),
+    "tns_hip_sgemm_strided_batched_multi": (C.c_int, [C.POINTER(i32), i32, u8, u8, i64, i64, i64,
+                                                      f32, fptr, i64, i64, fptr, i64, i64, f32,
+                                                      fptr, i64, i64, i64]),
+    "tns_set_op_devices": (C.c_int, [C.POINTER(i32), i32]),
     "tns_hip_yolo_forward": (C.c_int, [vp, i64, i64, i64, i64, fptr, fptr]),
     "tns_hip_means_and_vars": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, fptr]),
     "tns_hip_normalize": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, i64, fptr, i64]),

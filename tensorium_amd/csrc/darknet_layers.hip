@@ -58,6 +58,31 @@ __global__ void yolo_kernel(int64_t batch, int anchors, int classes, int64_t hw,
   }
 }
 
+// backward direction (isForward = 0): in[(p*H + Y)*W + X] accumulates
+// scale*out over its s x s output pixels in the CPU loop's order (output row
+// outer, column inner; nupsamplelayer.pas:101-110), each product and sum
+// rounded.  One thread per input pixel, so no races (the reference CUDA
+// kernel has all s*s threads add into the same input pixel).  zeroIn starts
+// from 0 instead of the current input (the reverse layer's output.fill(0)).
+__global__ void upsample_back_kernel(int64_t planes, int H, int W, int s, float scale,
+                                     float* __restrict__ in, const float* __restrict__ out,
+                                     int zero) {
+  const int64_t total = planes * H * W;
+  const int OW = W * s;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int X = (int)(i % W);
+    const int64_t r = i / W;  // (plane, Y)
+    const int Y = (int)(r % H);
+    const int64_t p = r / H;
+    float v = zero ? 0.0f : in[i];
+    const float* o = out + ((p * H + Y) * s) * (int64_t)OW + (int64_t)X * s;
+    for (int dy = 0; dy < s; ++dy)
+      for (int dx = 0; dx < s; ++dx) v = v + scale * o[(int64_t)dy * OW + dx];
+    in[i] = v;
+  }
+}
+
 int blocks_for(int64_t n) {
   int64_t b = (n + 255) / 256;
   return (int)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
@@ -83,6 +108,15 @@ hipError_t launch_upsample(int64_t planes, int H, int W, int stride, float scale
   else
     hipLaunchKernelGGL(upsample_kernel<1>, dim3(blocks_for(total)), dim3(256), 0, s, planes, H, W,
                        stride, scale, in, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_upsample_backward(int64_t planes, int H, int W, int stride, float scale,
+                                   float* in, const float* out, int zero, hipStream_t s) {
+  const int64_t total = planes * H * W;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(upsample_back_kernel, dim3(blocks_for(total)), dim3(256), 0, s, planes, H, W,
+                     stride, scale, in, out, zero);
   return hipGetLastError();
 }
 

@@ -310,6 +310,81 @@ __global__ __launch_bounds__(TPB) void clamp_kernel(int64_t n, float alpha,
   }
 }
 
+
+// TNNCuda.addvv / subvv / mulvv / fmavv (nncuda.pas:120-123; kernels
+// addv/subv/mulv/fmav): strided, one rounding per arithmetic operation
+// (fmavv = src1*src2 rounded, then + src3 rounded — the CPU sfmavss form;
+// the library is built without contraction)
+template <int OP>
+__global__ __launch_bounds__(TPB) void vv_kernel(int64_t n, const float* __restrict__ a,
+                                                 int64_t inca, const float* __restrict__ b,
+                                                 int64_t incb, const float* __restrict__ c,
+                                                 int64_t incc, float* __restrict__ d,
+                                                 int64_t incd) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * TPB) {
+    const float x = a[i * inca], y = b[i * incb];
+    float r;
+    if (OP == 0) r = x + y;
+    else if (OP == 1) r = x - y;
+    else if (OP == 2) r = x * y;
+    else r = x * y + c[i * incc];
+    d[i * incd] = r;
+  }
+}
+
+// TNNCuda.fmavss (nncuda.pas:137, kernel fmavss) / sfmavss (ntensors.pas:
+// 3355-3368): dst = src*scalar + bias, mul then add
+__global__ __launch_bounds__(TPB) void fmavss_kernel(int64_t n, const float* __restrict__ src,
+                                                     float scalar, float bias,
+                                                     float* __restrict__ dst) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * TPB)
+    dst[i] = src[i] * scalar + bias;
+}
+
+// TNNCuda.inverseSqrt (nncuda.pas:1563, kernel inverse_sqrt):
+// dst = 1 / sqrt(max(src, eps)) (alpha is unused by the reference)
+__global__ __launch_bounds__(TPB) void inverse_sqrt_kernel(int64_t n, const float* __restrict__ src,
+                                                           float* __restrict__ dst,
+                                                           int64_t stride) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * TPB) {
+    const float v = src[i * stride];
+    dst[i * stride] = 1.0f / sqrtf(v > 0.000001f ? v : 0.000001f);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_vv(int op, int64_t n, const float* a, int64_t inca, const float* b, int64_t incb,
+                     const float* c, int64_t incc, float* d, int64_t incd, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const unsigned g = grid_for(n);
+  switch (op) {
+    case 0: hipLaunchKernelGGL(vv_kernel<0>, dim3(g), dim3(TPB), 0, s, n, a, inca, b, incb, c, incc, d, incd); break;
+    case 1: hipLaunchKernelGGL(vv_kernel<1>, dim3(g), dim3(TPB), 0, s, n, a, inca, b, incb, c, incc, d, incd); break;
+    case 2: hipLaunchKernelGGL(vv_kernel<2>, dim3(g), dim3(TPB), 0, s, n, a, inca, b, incb, c, incc, d, incd); break;
+    default: hipLaunchKernelGGL(vv_kernel<3>, dim3(g), dim3(TPB), 0, s, n, a, inca, b, incb, c, incc, d, incd); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_fmavss(int64_t n, const float* src, float scalar, float bias, float* dst,
+                         hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fmavss_kernel, dim3(grid_for(n)), dim3(TPB), 0, s, n, src, scalar, bias, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_inverse_sqrt(int64_t n, const float* src, float* dst, int64_t stride,
+                               hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(inverse_sqrt_kernel, dim3(grid_for(n)), dim3(TPB), 0, s, n, src, dst, stride);
+  return hipGetLastError();
+}
+
+namespace {
 }  // namespace
 
 hipError_t launch_bias_activate(float* dst, int64_t F, int64_t bs, const float* bias,

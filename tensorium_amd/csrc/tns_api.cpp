@@ -17,6 +17,8 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
+#include <vector>
 #include <string>
 #include <tuple>
 
@@ -66,6 +68,9 @@ struct tns_ctx {
   double op_ms[TNS_OP_COUNT] = {0};
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::mutex mu;  // serialises host-API use of one context
+  // host-pointer pipeline: copy stream and per-chunk events
+  hipStream_t copy_stream = nullptr;
+  std::vector<hipEvent_t> pipe_ev;
   // implicit-GEMM conv k-tables, one per (C, H, W, kH, kW, dY, dX)
   std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int*> ktabs;
 };
@@ -225,6 +230,249 @@ tns_ctx* default_ctx() {
   return g_default_status == TNS_OK ? g_default : nullptr;
 }
 
+
+// ---- boundary A: the host-pointer GEMM pipeline ----------------------------
+// Operands arrive in host memory.  On the MI355X box PCIe moves ~56 GB/s in
+// either direction and no more with both at once (pageable and pinned alike;
+// scripts/pcie_probe.py, profiles/r02_pcie.json), so the copies bound the call
+// and the GEMM is hidden under them: the call is cut into chunks — rows of C
+// for a single GEMM (B, which every row needs, goes first), whole GEMMs for a
+// batch — and chunk j computes on the context's stream while chunk j+1
+// uploads and chunk j-1 downloads on the copy stream.  Device operands keep
+// the host layout (same element offsets) in context scratch; C is copied
+// back row by row (2-D copies) so host gaps between rows / GEMMs are never
+// overwritten.
+struct HostGemm {
+  bool ta, tb;
+  int64_t M, N, K;
+  float alpha, beta;
+  const float* A;
+  int64_t lda, sA;
+  const float* B;
+  int64_t ldb, sB;
+  float* C;
+  int64_t ldc, sC;
+  int64_t batch;
+};
+
+int64_t span_of(int64_t rows, int64_t ld, int64_t cols) {
+  return rows > 0 && cols > 0 ? (rows - 1) * ld + cols : 0;
+}
+
+// rows x cols sub-matrix with row pitch ld, same element offsets on both sides
+hipError_t copy_rows(float* dst, const float* src, int64_t rows, int64_t cols, int64_t ld,
+                     hipMemcpyKind kind, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (cols == ld || rows == 1)
+    return hipMemcpyAsync(dst, src, (size_t)span_of(rows, ld, cols) * 4, kind, s);
+  return hipMemcpy2DAsync(dst, (size_t)ld * 4, src, (size_t)ld * 4, (size_t)cols * 4,
+                          (size_t)rows, kind, s);
+}
+
+// GEMMs [b0, b1) of a strided operand (rows x cols, pitch ld, stride st)
+hipError_t copy_batch(float* dst, const float* src, int64_t b0, int64_t b1, int64_t rows,
+                      int64_t cols, int64_t ld, int64_t st, hipMemcpyKind kind, hipStream_t s) {
+  const int64_t one = span_of(rows, ld, cols);
+  if (b1 <= b0 || one == 0) return hipSuccess;
+  const bool dense = (cols == ld || rows == 1) && (st == one || b1 - b0 == 1);
+  if (dense)
+    return hipMemcpyAsync(dst + b0 * st, src + b0 * st, (size_t)((b1 - b0 - 1) * st + one) * 4,
+                          kind, s);
+  for (int64_t b = b0; b < b1; ++b)
+    if (hipError_t e = copy_rows(dst + b * st, src + b * st, rows, cols, ld, kind, s)) return e;
+  return hipSuccess;
+}
+
+int ensure_copy_stream(tns_ctx* c, int nev) {
+  if (!c->copy_stream)
+    TNS_HIP_TRY(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  while ((int)c->pipe_ev.size() < nev) {
+    hipEvent_t e;
+    TNS_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->pipe_ev.push_back(e);
+  }
+  return TNS_OK;
+}
+
+// dA_pre / dB_pre: device copies of a shared (stride 0) operand already on this
+// context's device (multi-device broadcast), or nullptr
+int host_gemm(tns_ctx* c, const HostGemm& g, const float* dA_pre, const float* dB_pre) {
+  std::lock_guard<std::mutex> lk(c->mu);
+  TNS_HIP_TRY(hipSetDevice(c->device));
+  const int64_t a_rows = g.ta ? g.K : g.M, a_cols = g.ta ? g.M : g.K;
+  const int64_t b_rows = g.tb ? g.N : g.K, b_cols = g.tb ? g.K : g.N;
+  const int64_t oneA = span_of(a_rows, g.lda, a_cols), oneB = span_of(b_rows, g.ldb, b_cols);
+  const int64_t oneC = span_of(g.M, g.ldc, g.N);
+  // one block of A / B serving every chunk: B of a single GEMM (chunked by
+  // rows of C, which need all of B) and stride-0 operands of a batch
+  const bool sharedA = g.sA == 0 || g.batch == 1, sharedB = g.sB == 0 || g.batch == 1;
+  const bool upfrontA = g.sA == 0 && g.batch > 1;
+  const int64_t nA = sharedA ? oneA : (g.batch - 1) * g.sA + oneA;
+  const int64_t nB = sharedB ? oneB : (g.batch - 1) * g.sB + oneB;
+  const int64_t nC = (g.batch - 1) * g.sC + oneC;
+  float *dA = nullptr, *dB = nullptr, *dC = nullptr;
+  if (!dA_pre && oneA)
+    if (int r = ensure_scratch(c, SLOT_STAGE1, nA, &dA)) return r;
+  if (!dB_pre && oneB)
+    if (int r = ensure_scratch(c, SLOT_STAGE2, nB, &dB)) return r;
+  if (int r = ensure_scratch(c, SLOT_STAGE3, nC, &dC)) return r;
+  const float* uA = dA_pre ? dA_pre : dA;
+  const float* uB = dB_pre ? dB_pre : dB;
+  // chunks: rows of C for one GEMM (>= 512 rows each, at most 4), GEMMs for
+  // a batch (at most 16)
+  const bool by_rows = g.batch == 1;
+  const int64_t units = by_rows ? g.M : g.batch;
+  int64_t R = by_rows ? std::min<int64_t>(4, std::max<int64_t>(1, g.M / 512))
+                      : std::min<int64_t>(16, g.batch);
+  if (int r = ensure_copy_stream(c, (int)(2 * R))) return r;
+  hipStream_t cs = c->copy_stream, ks = c->stream;
+  const bool needC = beta_mode_for(g.beta) != BETA_ZERO;
+  const hipMemcpyKind H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
+  // shared operands first
+  if (!dA_pre && upfrontA && oneA)
+    TNS_HIP_TRY(copy_rows(dA, g.A, a_rows, a_cols, g.lda, H2D, cs));
+  if (!dB_pre && sharedB && oneB)
+    TNS_HIP_TRY(copy_rows(dB, g.B, b_rows, b_cols, g.ldb, H2D, cs));
+  auto lo = [&](int64_t j) { return units * j / R; };
+  auto download = [&](int64_t j) -> hipError_t {
+    const int64_t u0 = lo(j), u1 = lo(j + 1);
+    if (by_rows)
+      return copy_rows(g.C + u0 * g.ldc, dC + u0 * g.ldc, u1 - u0, g.N, g.ldc, D2H, cs);
+    return copy_batch(g.C, dC, u0, u1, g.M, g.N, g.ldc, g.sC, D2H, cs);
+  };
+  for (int64_t j = 0; j < R; ++j) {
+    const int64_t u0 = lo(j), u1 = lo(j + 1);
+    hipEvent_t up = c->pipe_ev[2 * j], done = c->pipe_ev[2 * j + 1];
+    if (by_rows) {  // rows u0..u1 of C: rows of A (NoTrans) or its columns (Trans)
+      if (!dA_pre && oneA) {
+        if (g.ta)
+          TNS_HIP_TRY(copy_rows(dA + u0, g.A + u0, g.K, u1 - u0, g.lda, H2D, cs));
+        else
+          TNS_HIP_TRY(copy_rows(dA + u0 * g.lda, g.A + u0 * g.lda, u1 - u0, g.K, g.lda, H2D, cs));
+      }
+      if (needC)
+        TNS_HIP_TRY(copy_rows(dC + u0 * g.ldc, g.C + u0 * g.ldc, u1 - u0, g.N, g.ldc, H2D, cs));
+    } else {
+      if (!sharedA) TNS_HIP_TRY(copy_batch(dA, g.A, u0, u1, a_rows, a_cols, g.lda, g.sA, H2D, cs));
+      if (!sharedB) TNS_HIP_TRY(copy_batch(dB, g.B, u0, u1, b_rows, b_cols, g.ldb, g.sB, H2D, cs));
+      if (needC) TNS_HIP_TRY(copy_batch(dC, g.C, u0, u1, g.M, g.N, g.ldc, g.sC, H2D, cs));
+    }
+    TNS_HIP_TRY(hipEventRecord(up, cs));
+    TNS_HIP_TRY(hipStreamWaitEvent(ks, up, 0));
+    int r;
+    if (by_rows)
+      r = do_gemm(c, g.ta, g.tb, u1 - u0, g.N, g.K, g.alpha,
+                  uA ? uA + (g.ta ? u0 : u0 * g.lda) : nullptr, g.lda, 0, uB, g.ldb, 0, g.beta,
+                  dC + u0 * g.ldc, g.ldc, 0, 1, EPI_NONE, nullptr, 0);
+    else
+      r = do_gemm(c, g.ta, g.tb, g.M, g.N, g.K, g.alpha, uA ? uA + (sharedA ? 0 : u0 * g.sA) : nullptr,
+                  g.lda, sharedA ? 0 : g.sA, uB ? uB + (sharedB ? 0 : u0 * g.sB) : nullptr, g.ldb,
+                  sharedB ? 0 : g.sB, g.beta, dC + u0 * g.sC, g.ldc, g.sC, u1 - u0, EPI_NONE,
+                  nullptr, 0);
+    if (r) return r;
+    TNS_HIP_TRY(hipEventRecord(done, ks));
+    if (j > 0) {
+      TNS_HIP_TRY(hipStreamWaitEvent(cs, c->pipe_ev[2 * j - 1], 0));
+      TNS_HIP_TRY(download(j - 1));
+    }
+  }
+  TNS_HIP_TRY(hipStreamWaitEvent(cs, c->pipe_ev[2 * R - 1], 0));
+  TNS_HIP_TRY(download(R - 1));
+  TNS_HIP_TRY(hipStreamSynchronize(cs));
+  return TNS_OK;
+}
+
+// ---- several GPUs from one process (sgemm_strided_batched_multi)
+// Slot i of a call owns a context on devices[i] (two slots may share a
+// device); the batch is split into contiguous shards, the first batch % n
+// slots one GEMM longer (tensorium_amd/shard.py, the reference's MP.&For
+// blocks).  A shared operand (stride 0: the conv weights of
+// nConvolutionLayer.pas:773) crosses PCIe once, to slot 0, and reaches the
+// other devices by peer copies over xGMI.  Each slot runs the host pipeline
+// above on its own host thread.
+std::mutex g_pool_mu;
+std::vector<tns_ctx*> g_pool;
+std::mutex g_op_devices_mu;
+std::vector<int32_t> g_op_devices;
+
+int pool_ctx(int slot, int device, tns_ctx** out) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  if ((int)g_pool.size() <= slot) g_pool.resize(slot + 1, nullptr);
+  if (g_pool[slot] && g_pool[slot]->device != device) {
+    tns_hip_destroy(g_pool[slot]);
+    g_pool[slot] = nullptr;
+  }
+  if (!g_pool[slot])
+    if (int r = tns_hip_create(device, &g_pool[slot])) return r;
+  *out = g_pool[slot];
+  return TNS_OK;
+}
+
+int multi_host_gemm(const int32_t* devices, int n, const HostGemm& g) {
+  std::vector<tns_ctx*> ctx(n);
+  for (int i = 0; i < n; ++i)
+    if (int r = pool_ctx(i, devices[i], &ctx[i])) return r;
+  const int64_t a_rows = g.ta ? g.K : g.M, a_cols = g.ta ? g.M : g.K;
+  const int64_t b_rows = g.tb ? g.N : g.K, b_cols = g.tb ? g.K : g.N;
+  const int64_t oneA = span_of(a_rows, g.lda, a_cols), oneB = span_of(b_rows, g.ldb, b_cols);
+  // shared operands: host -> slot 0 once, slot 0 -> every other slot by peer copy
+  std::vector<const float*> preA(n, nullptr), preB(n, nullptr);
+  auto broadcast = [&](const float* host, int64_t rows, int64_t cols, int64_t ld, int64_t elems,
+                       int slot, std::vector<const float*>& pre) -> int {
+    float* root;
+    {
+      std::lock_guard<std::mutex> lk(ctx[0]->mu);
+      TNS_HIP_TRY(hipSetDevice(ctx[0]->device));
+      if (int r = ensure_scratch(ctx[0], slot, elems, &root)) return r;
+      TNS_HIP_TRY(copy_rows(root, host, rows, cols, ld, hipMemcpyHostToDevice, ctx[0]->stream));
+      TNS_HIP_TRY(hipStreamSynchronize(ctx[0]->stream));
+    }
+    pre[0] = root;
+    for (int i = 1; i < n; ++i) {
+      std::lock_guard<std::mutex> lk(ctx[i]->mu);
+      TNS_HIP_TRY(hipSetDevice(ctx[i]->device));
+      float* d;
+      if (int r = ensure_scratch(ctx[i], slot, elems, &d)) return r;
+      if (ctx[i]->device == ctx[0]->device)
+        TNS_HIP_TRY(hipMemcpyAsync(d, root, (size_t)elems * 4, hipMemcpyDeviceToDevice,
+                                   ctx[i]->stream));
+      else
+        TNS_HIP_TRY(hipMemcpyPeerAsync(d, ctx[i]->device, root, ctx[0]->device,
+                                       (size_t)elems * 4, ctx[i]->stream));
+      TNS_HIP_TRY(hipStreamSynchronize(ctx[i]->stream));
+      pre[i] = d;
+    }
+    return TNS_OK;
+  };
+  if (g.sA == 0 && oneA && n > 1)
+    if (int r = broadcast(g.A, a_rows, a_cols, g.lda, oneA, SLOT_STAGE1, preA)) return r;
+  if (g.sB == 0 && oneB && n > 1)
+    if (int r = broadcast(g.B, b_rows, b_cols, g.ldb, oneB, SLOT_STAGE2, preB)) return r;
+  std::vector<int> status(n, TNS_OK);
+  std::vector<std::string> errs(n);
+  std::vector<std::thread> th;
+  const int64_t base = g.batch / n, extra = g.batch % n;
+  for (int i = 0; i < n; ++i) {
+    const int64_t s0 = i * base + std::min<int64_t>(i, extra);
+    const int64_t cnt = base + (i < extra ? 1 : 0);
+    if (cnt == 0) continue;
+    HostGemm gi = g;
+    gi.A = g.sA ? g.A + s0 * g.sA : g.A;
+    gi.B = g.sB ? g.B + s0 * g.sB : g.B;
+    gi.C = g.C + s0 * g.sC;
+    gi.batch = cnt;
+    th.emplace_back([&, i, gi] {
+      status[i] = host_gemm(ctx[i], gi, preA[i], preB[i]);
+      if (status[i]) errs[i] = g_err;  // the error string is thread-local
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int i = 0; i < n; ++i)
+    if (status[i]) return set_error(status[i], "slot %d (device %d): %s", i, devices[i],
+                                    errs[i].c_str());
+  return TNS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -300,6 +548,8 @@ int tns_hip_destroy(tns_ctx* c) {
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+  if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+  for (hipEvent_t e : c->pipe_ev) hipEventDestroy(e);
   delete c;
   return TNS_OK;
 }
@@ -529,14 +779,113 @@ int tns_hip_shortcut(tns_ctx* c, int64_t N, const float* a, int64_t aOffset, con
                     "shortcut");
 }
 
-int tns_hip_upsample(tns_ctx* c, int64_t planes, int64_t H, int64_t W, int64_t stride, float scale,
-                     const float* in, float* out) {
+int tns_hip_upsample(tns_ctx* c, int64_t aBatch, int64_t aChannels, int64_t outHeight,
+                     int64_t outWidth, float* in, int64_t stride, int32_t isForward, float scale,
+                     float* out, int32_t zeroIn) {
   if (int r = check_ctx(c)) return r;
-  if (planes < 0 || H < 0 || W < 0 || stride < 1 || H * stride > 0x7fffffff ||
-      W * stride > 0x7fffffff || (planes * H * W > 0 && (!in || !out)))
+  const int64_t planes = aBatch * aChannels, H = outHeight, W = outWidth;
+  if (aBatch < 0 || aChannels < 0 || H < 0 || W < 0 || stride < 1 ||
+      H * stride > 0x7fffffff || W * stride > 0x7fffffff ||
+      (planes * H * W > 0 && (!in || !out)))
     return set_error(TNS_ERR_ARG, "upsample: bad args");
-  return hip_status(launch_upsample(planes, (int)H, (int)W, (int)stride, scale, in, out, c->stream),
-                    "upsample");
+  if (isForward)
+    return hip_status(launch_upsample(planes, (int)H, (int)W, (int)stride, scale, in, out,
+                                      c->stream),
+                      "upsample");
+  return hip_status(launch_upsample_backward(planes, (int)H, (int)W, (int)stride, scale, in, out,
+                                             zeroIn, c->stream),
+                    "upsample backward");
+}
+
+// TNNCuda.addvv / subvv / mulvv / fmavv / fmavss / inverseSqrt (nncuda.pas:120-151)
+namespace {
+int vv(tns_ctx* c, int op, int64_t N, const float* a, int64_t aOff, int64_t inca, const float* b,
+       int64_t bOff, int64_t incb, const float* cc, int64_t cOff, int64_t incc, float* d,
+       int64_t dOff, int64_t incd, const char* what) {
+  if (int r = check_ctx(c)) return r;
+  if (N < 0 || (N > 0 && (!a || !b || !d || (op == 3 && !cc))))
+    return set_error(TNS_ERR_ARG, "%s: bad args", what);
+  return hip_status(launch_vv(op, N, a + aOff, inca, b + bOff, incb, cc ? cc + cOff : nullptr,
+                              incc, d + dOff, incd, c->stream),
+                    what);
+}
+}  // namespace
+
+int tns_hip_addvv(tns_ctx* c, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, float* dst,
+                  int64_t dstOffset, int64_t incc) {
+  return vv(c, 0, N, src1, src1Offset, inca, src2, src2Offset, incb, nullptr, 0, 0, dst,
+            dstOffset, incc, "addvv");
+}
+
+int tns_hip_subvv(tns_ctx* c, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, float* dst,
+                  int64_t dstOffset, int64_t incc) {
+  return vv(c, 1, N, src1, src1Offset, inca, src2, src2Offset, incb, nullptr, 0, 0, dst,
+            dstOffset, incc, "subvv");
+}
+
+int tns_hip_mulvv(tns_ctx* c, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, float* dst,
+                  int64_t dstOffset, int64_t incc) {
+  return vv(c, 2, N, src1, src1Offset, inca, src2, src2Offset, incb, nullptr, 0, 0, dst,
+            dstOffset, incc, "mulvv");
+}
+
+int tns_hip_fmavv(tns_ctx* c, int64_t N, const float* src1, int64_t src1Offset, int64_t inca,
+                  const float* src2, int64_t src2Offset, int64_t incb, const float* src3,
+                  int64_t src3Offset, int64_t incc, float* dst, int64_t dstOffset,
+                  int64_t incd) {
+  return vv(c, 3, N, src1, src1Offset, inca, src2, src2Offset, incb, src3, src3Offset, incc, dst,
+            dstOffset, incd, "fmavv");
+}
+
+int tns_hip_fmavss(tns_ctx* c, int64_t N, const float* src, int64_t offset, float scalar,
+                   float bias, float* dst) {
+  if (int r = check_ctx(c)) return r;
+  if (N < 0 || (N > 0 && (!src || !dst))) return set_error(TNS_ERR_ARG, "fmavss: bad args");
+  return hip_status(launch_fmavss(N, src + offset, scalar, bias, dst + offset, c->stream),
+                    "fmavss");
+}
+
+int tns_hip_inverse_sqrt(tns_ctx* c, int64_t N, float alpha, const float* src, float* dst,
+                         int64_t stride, int64_t offset) {
+  (void)alpha;  // unused by the reference kernel too
+  if (int r = check_ctx(c)) return r;
+  if (N < 0 || stride < 1 || (N > 0 && (!src || !dst)))
+    return set_error(TNS_ERR_ARG, "inverseSqrt: bad args");
+  return hip_status(launch_inverse_sqrt(N, src + offset, dst + offset, stride, c->stream),
+                    "inverseSqrt");
+}
+
+int tns_hip_sgemm_strided_batched_multi(const int32_t* devices, int32_t n, uint8_t transA,
+                                        uint8_t transB, int64_t M, int64_t N, int64_t K,
+                                        float alpha, const float* A, int64_t lda,
+                                        int64_t strideA, const float* B, int64_t ldb,
+                                        int64_t strideB, float beta, float* C, int64_t ldc,
+                                        int64_t strideC, int64_t batchCount) {
+  if (!devices || n <= 0) return set_error(TNS_ERR_ARG, "sgemm_multi: no devices");
+  const int nd = tns_device_count();
+  for (int i = 0; i < n; ++i)
+    if (devices[i] < 0 || devices[i] >= nd)
+      return set_error(TNS_ERR_ARG, "sgemm_multi: device %d out of range [0,%d)", devices[i], nd);
+  if (M < 0 || N < 0 || K < 0 || batchCount < 0)
+    return set_error(TNS_ERR_ARG, "sgemm_multi: negative dimension");
+  if (M == 0 || N == 0 || batchCount == 0) return TNS_OK;
+  if (!C || (K > 0 && (!A || !B))) return set_error(TNS_ERR_ARG, "sgemm_multi: null operand");
+  HostGemm g{transA != 0, transB != 0, M, N, K, alpha, beta, A, lda, strideA, B, ldb, strideB,
+             C, ldc, strideC, batchCount};
+  return multi_host_gemm(devices, n, g);
+}
+
+int tns_set_op_devices(const int32_t* devices, int32_t n) {
+  const int nd = tns_device_count();
+  for (int i = 0; i < n; ++i)
+    if (!devices || devices[i] < 0 || devices[i] >= nd)
+      return set_error(TNS_ERR_ARG, "set_op_devices: bad device list");
+  std::lock_guard<std::mutex> lk(g_op_devices_mu);
+  g_op_devices.assign(devices, devices + (n > 0 ? n : 0));
+  return TNS_OK;
 }
 
 int tns_hip_yolo_forward(tns_ctx* c, int64_t batch, int64_t anchors, int64_t classes, int64_t hw,
@@ -1025,47 +1374,24 @@ void tns_cblas_sgemm_batch_strided(int32_t Layout, int32_t TransA, int32_t Trans
                                    float beta, float* C, int64_t ldc, int64_t strideC,
                                    int64_t batch_size) {
   (void)Layout;  // ignored, as cblas_sgemm ignores Order (ntensors.pas:2231)
-  tns_ctx* c = default_ctx();
-  if (!c) return;
   if ((TransA != TNS_CblasNoTrans && TransA != TNS_CblasTrans) ||
       (TransB != TNS_CblasNoTrans && TransB != TNS_CblasTrans)) {
     set_error(TNS_ERR_ARG, "cblas_sgemm: bad transpose enum");
     return;
   }
   if (M <= 0 || N <= 0 || batch_size <= 0) return;
-  std::lock_guard<std::mutex> lk(c->mu);
-  hipSetDevice(c->device);
-  const bool ta = TransA == TNS_CblasTrans, tb = TransB == TNS_CblasTrans;
-  const int64_t a_rows = ta ? K : M, b_rows = tb ? N : K;
-  // extent of each operand (last batch's last element + 1)
-  auto extent = [](int64_t rows, int64_t ld, int64_t cols, int64_t stride, int64_t batch) {
-    if (rows <= 0 || cols <= 0) return (int64_t)0;
-    return (batch - 1) * stride + (rows - 1) * ld + cols;
-  };
-  const int64_t nA = extent(a_rows, lda, ta ? M : K, strideA, batch_size);
-  const int64_t nB = extent(b_rows, ldb, tb ? K : N, strideB, batch_size);
-  const int64_t nC = extent(M, ldc, N, strideC, batch_size);
-  float *dA = nullptr, *dB = nullptr, *dC = nullptr;
-  if (ensure_scratch(c, 1, nA, &dA) || ensure_scratch(c, 2, nB, &dB) ||
-      ensure_scratch(c, 3, nC, &dC))
-    return;
-  hipStream_t s = c->stream;
-  if (nA && hip_status(hipMemcpyAsync(dA, A, nA * 4, hipMemcpyHostToDevice, s), "H2D A")) return;
-  if (nB && hip_status(hipMemcpyAsync(dB, B, nB * 4, hipMemcpyHostToDevice, s), "H2D B")) return;
-  const bool needC = beta_mode_for(beta) != BETA_ZERO;
-  if (needC && hip_status(hipMemcpyAsync(dC, C, nC * 4, hipMemcpyHostToDevice, s), "H2D C"))
-    return;
-  if (!needC && strideC != M * ldc && batch_size > 1) {
-    // gaps between batches must survive the copy back
-    if (hip_status(hipMemcpyAsync(dC, C, nC * 4, hipMemcpyHostToDevice, s), "H2D C")) return;
-  } else if (!needC && ldc != N) {
-    if (hip_status(hipMemcpyAsync(dC, C, nC * 4, hipMemcpyHostToDevice, s), "H2D C")) return;
+  HostGemm g{TransA == TNS_CblasTrans, TransB == TNS_CblasTrans, M, N, K, alpha, beta,
+             A, lda, strideA, B, ldb, strideB, C, ldc, strideC, batch_size};
+  {
+    std::lock_guard<std::mutex> lk(g_op_devices_mu);
+    if (g_op_devices.size() > 1) {  // tns_set_op_devices: spread over several GPUs
+      multi_host_gemm(g_op_devices.data(), (int)g_op_devices.size(), g);
+      return;
+    }
   }
-  if (do_gemm(c, ta, tb, M, N, K, alpha, dA, lda, strideA, dB, ldb, strideB, beta, dC, ldc,
-              strideC, batch_size, EPI_NONE, nullptr, 0))
-    return;
-  if (hip_status(hipMemcpyAsync(C, dC, nC * 4, hipMemcpyDeviceToHost, s), "D2H C")) return;
-  hip_status(hipStreamSynchronize(s), "sync");
+  tns_ctx* c = default_ctx();
+  if (!c) return;
+  host_gemm(c, g, nullptr, nullptr);
 }
 
 void tns_cblas_sgemm(int32_t Order, int32_t TransA, int32_t TransB, int64_t M, int64_t N,

@@ -125,6 +125,15 @@ hipError_t launch_shortcut(int64_t n, const float* a, const float* b, float* out
                            hipStream_t s);
 hipError_t launch_upsample(int64_t planes, int H, int W, int stride, float scale, const float* in,
                            float* out, hipStream_t s);
+hipError_t launch_upsample_backward(int64_t planes, int H, int W, int stride, float scale,
+                                   float* in, const float* out, int zero, hipStream_t s);
+// TNNCuda addvv/subvv/mulvv/fmavv (op 0..3), fmavss, inverseSqrt
+hipError_t launch_vv(int op, int64_t n, const float* a, int64_t inca, const float* b, int64_t incb,
+                     const float* c, int64_t incc, float* d, int64_t incd, hipStream_t s);
+hipError_t launch_fmavss(int64_t n, const float* src, float scalar, float bias, float* dst,
+                         hipStream_t s);
+hipError_t launch_inverse_sqrt(int64_t n, const float* src, float* dst, int64_t stride,
+                               hipStream_t s);
 hipError_t launch_yolo(int64_t batch, int anchors, int classes, int64_t hw, const float* in,
                        float* out, hipStream_t s);
 hipError_t launch_bias_activate(float* dst, int64_t nFilters, int64_t blockSize,

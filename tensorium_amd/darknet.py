@@ -318,7 +318,7 @@ class HipDarknet:
                     hip.copy(n, self.out[s], 0, 1, out, off, 1)
                     off += n
             elif l.kind == "upsample":
-                hip.upsample(B * l.c, l.h, l.w, l.stride, 1.0, prev, out)
+                hip.upSample(B, l.c, l.h, l.w, prev, l.stride, 1, 1.0, out)
             elif l.kind == "yolo":
                 hip.yoloForward(B, l.anchors, l.classes, l.h * l.w, prev, out)
             prev = out

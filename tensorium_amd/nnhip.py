@@ -191,9 +191,39 @@ class TNNHip:
         check(self.lib.tns_hip_shortcut(self.ctx, N, _ptr(a), aOffset, _ptr(b), bOffset, _ptr(out),
                                         outOffset, int(activation)))
 
-    def upsample(self, planes, H, W, stride, scale, inp, out):
-        check(self.lib.tns_hip_upsample(self.ctx, planes, H, W, stride, float(scale), _ptr(inp),
-                                        _ptr(out)))
+    def upSample(self, aBatch, aChannels, outHeight, outWidth, in_, stride, isForward, scale,
+                 out, zeroIn=0):
+        """TNNCuda.upSample (nncuda.pas:136): outHeight/outWidth are the small
+        tensor's; isForward=1 writes out, isForward=0 accumulates into in_."""
+        check(self.lib.tns_hip_upsample(self.ctx, aBatch, aChannels, outHeight, outWidth,
+                                        _ptr(in_), stride, int(isForward), float(scale),
+                                        _ptr(out), int(zeroIn)))
+
+    def addvv(self, N, src1, src1Offset, inca, src2, src2Offset, incb, dst, dstOffset, incc):
+        check(self.lib.tns_hip_addvv(self.ctx, N, _ptr(src1), src1Offset, inca, _ptr(src2),
+                                     src2Offset, incb, _ptr(dst), dstOffset, incc))
+
+    def subvv(self, N, src1, src1Offset, inca, src2, src2Offset, incb, dst, dstOffset, incc):
+        check(self.lib.tns_hip_subvv(self.ctx, N, _ptr(src1), src1Offset, inca, _ptr(src2),
+                                     src2Offset, incb, _ptr(dst), dstOffset, incc))
+
+    def mulvv(self, N, src1, src1Offset, inca, src2, src2Offset, incb, dst, dstOffset, incc):
+        check(self.lib.tns_hip_mulvv(self.ctx, N, _ptr(src1), src1Offset, inca, _ptr(src2),
+                                     src2Offset, incb, _ptr(dst), dstOffset, incc))
+
+    def fmavv(self, N, src1, src1Offset, inca, src2, src2Offset, incb, src3, src3Offset, incc,
+              dst, dstOffset, incd):
+        check(self.lib.tns_hip_fmavv(self.ctx, N, _ptr(src1), src1Offset, inca, _ptr(src2),
+                                     src2Offset, incb, _ptr(src3), src3Offset, incc, _ptr(dst),
+                                     dstOffset, incd))
+
+    def fmavss(self, N, src, offset, scalar, bias, dst):
+        check(self.lib.tns_hip_fmavss(self.ctx, N, _ptr(src), offset, float(scalar), float(bias),
+                                      _ptr(dst)))
+
+    def inverseSqrt(self, N, alpha, src, dst, stride=1, offset=0):
+        check(self.lib.tns_hip_inverse_sqrt(self.ctx, N, float(alpha), _ptr(src), _ptr(dst),
+                                            stride, offset))
 
     def yoloForward(self, batch, anchors, classes, hw, inp, out):
         check(self.lib.tns_hip_yolo_forward(self.ctx, batch, anchors, classes, hw, _ptr(inp),

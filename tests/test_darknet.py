@@ -95,9 +95,24 @@ def test_upsample_shortcut_yolo_ops(hip, torch_cuda, ora):
     T = torch_cuda
     x = ora.uniform(3 * 7 * 9, 12, 0)
     out = T.empty(3 * 14 * 18, device="cuda")
-    hip.upsample(3, 7, 9, 2, 1.0, T.from_numpy(x).cuda(), out)
+    hip.upSample(1, 3, 7, 9, T.from_numpy(x).cuda(), 2, 1, 1.0, out)
     hip.finish()
     assert np.array_equal(out.cpu().numpy(), ora.upsample(x, 3, 7, 9, 2))
+    # backward direction (isForward = 0): in += scale*out over each pixel's
+    # stride x stride block, row-major (nupsamplelayer.pas:101-110)
+    for zero, scale, s in ((0, 1.0, 2), (1, 0.5, 2), (0, 0.3, 3)):
+        g = ora.uniform(3 * 7 * s * 9 * s, 15, s)
+        base = ora.uniform(3 * 7 * 9, 16, s)
+        dev_in = T.from_numpy(base.copy()).cuda()
+        hip.upSample(1, 3, 7, 9, dev_in, s, 0, scale, T.from_numpy(g).cuda(), zero)
+        hip.finish()
+        ref = np.zeros_like(base) if zero else base.copy()
+        g4 = g.reshape(3, 7, s, 9, s)
+        sc = np.float32(scale)
+        for dy in range(s):
+            for dx in range(s):
+                ref = (ref + (sc * g4[:, :, dy, :, dx]).reshape(-1)).astype(np.float32)
+        assert np.array_equal(dev_in.cpu().numpy(), ref), (zero, scale, s)
     a, b = ora.uniform(1000, 13, 0), ora.uniform(1000, 13, 1)
     o = T.empty(1000, device="cuda")
     for act in (4, 9, 1):

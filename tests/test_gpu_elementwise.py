@@ -90,3 +90,38 @@ def test_blas1(hip, torch_cuda, ora):
     got = dy.cpu().numpy()
     assert np.array_equal(got[: n // 2], np.clip(x, -1, 1)[0:2 * (n // 2):2])
     assert np.all(got[n // 2:] == 3.0)
+
+
+def test_tnncuda_vector_ops(hip, torch_cuda):
+    """TNNCuda addvv / subvv / mulvv / fmavv / fmavss / inverseSqrt
+    (nncuda.pas:120-151): strided, offsets in elements, one rounding per
+    arithmetic operation (numpy float32 arithmetic is the same IEEE op)."""
+    T = torch_cuda
+    rng = np.random.default_rng(9)
+    n = 1000
+    a = rng.uniform(-2, 2, 3 * n + 5).astype(np.float32)
+    b = rng.uniform(-2, 2, 2 * n + 3).astype(np.float32)
+    c = rng.uniform(-2, 2, n + 7).astype(np.float32)
+    da, db, dc = (T.from_numpy(x).cuda() for x in (a, b, c))
+    A, B, Cc = a[5::3][:n], b[3::2][:n], c[7:][:n]
+    for name, ref in (("addvv", A + B), ("subvv", A - B), ("mulvv", A * B)):
+        out = T.zeros(2 * n + 1, device="cuda")
+        getattr(hip, name)(n, da, 5, 3, db, 3, 2, out, 1, 2)
+        hip.finish()
+        assert np.array_equal(out.cpu().numpy()[1::2][:n], ref.astype(np.float32)), name
+    out = T.zeros(n, device="cuda")
+    hip.fmavv(n, da, 5, 3, db, 3, 2, dc, 7, 1, out, 0, 1)
+    hip.finish()
+    assert np.array_equal(out.cpu().numpy(), ((A * B).astype(np.float32) + Cc).astype(np.float32))
+    out = T.zeros(c.size, device="cuda")
+    hip.fmavss(n, dc, 7, 1.5, -0.25, out)
+    hip.finish()
+    ref = ((Cc * np.float32(1.5)).astype(np.float32) + np.float32(-0.25)).astype(np.float32)
+    assert np.array_equal(out.cpu().numpy()[7:7 + n], ref)
+    v = np.abs(rng.uniform(-1e-5, 4, 2 * n)).astype(np.float32)
+    v[::50] = 0.0
+    dv, out = T.from_numpy(v).cuda(), T.zeros(2 * n, device="cuda")
+    hip.inverseSqrt(n, 0.0, dv, out, 2, 1)
+    hip.finish()
+    ref = (np.float32(1) / np.sqrt(np.maximum(v[1::2], np.float32(1e-6)))).astype(np.float32)
+    assert np.array_equal(out.cpu().numpy()[1::2], ref)
