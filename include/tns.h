@@ -360,19 +360,52 @@ int tns_hip_conv_forward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int6
                          int64_t dilation, int32_t activation, float* workspace,
                          float* out, int32_t fused);
 
+/* TConvolutionalLayer.forward in TRAINING with batch norm (nConvolutionLayer.
+ * pas:457-569 -> TBaseLayer.batchNorm, nbaselayer.pas:336-370): Conv2D into
+ * out; training != 0: MeansAndVars -> mean/variance, rolling_mean/variance
+ * *= (1 - bnMomentum) then += bnMomentum*stat (axpy), x := out,
+ * blockNormalize, x_norm := out; training == 0: blockNormalize with the
+ * rolling statistics; then forwardScale(scales), forwardBias(biases),
+ * activate.  Tensors [batch][filters][oH*oW]; statistics per filter.  The
+ * layer's bnMomentum is 0.1 (nbaselayer.pas:188).  In-place and
+ * bit-exact against the reference order (one fused pass after the stats). */
+int tns_hip_conv_forward_train(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
+                               const float* input, const float* weights, int64_t filters,
+                               int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                               int32_t activation, const float* scales, const float* biases,
+                               float* rolling_mean, float* rolling_variance, float bnMomentum,
+                               int32_t training, float* mean, float* variance, float* x,
+                               float* x_norm, float* workspace, float* out);
+
 /* TConvolutionalLayer.backward without batch-norm (nConvolutionLayer.pas:
  * 571-671): delta *= f'(output) (Derivative), bias_updates += addSums(delta),
  * im2col(input), weight_updates += delta_b . col_b^T per image (NT, beta 1),
  * and if state_delta != NULL: col = W^T . delta (TN strided batched, beta 0)
  * then col2im accumulates into state_delta.  delta is updated in place.
  * workspace (batch*C*k*k*outH*outW floats) may be NULL (context scratch).
- * dilation must be 1 (TNS_ERR_UNSUPPORTED otherwise). */
+ * The backward im2col / col2im pad with padding*dilation (640, 665); a
+ * dilation whose columns differ from the layer's outH x outW (92-100) is
+ * refused with TNS_ERR_UNSUPPORTED ("same" paddings work at any dilation). */
 int tns_hip_conv_backward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
                           const float* input, const float* weights, int64_t filters,
                           int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
                           int32_t activation, const float* output, float* delta,
                           float* bias_updates, float* weight_updates, float* workspace,
                           float* state_delta);
+/* The same with batch norm (isBatchNormalized, nConvolutionLayer.pas:601-602):
+ * batchNormBack (nbaselayer.pas:372-395) replaces the bias term —
+ * scale_updates += addDots(x_norm, delta); delta *= scales (forwardScale);
+ * MeansAndVarsDelta(delta, x, mean, variance) -> mean_delta / variance_delta;
+ * normalizeDelta — then the weight / input gradients as above.  x, x_norm,
+ * mean, variance are the forward's (tns_hip_conv_forward_train). */
+int tns_hip_conv_backward_bn(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
+                             const float* input, const float* weights, int64_t filters,
+                             int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                             int32_t activation, const float* output, float* delta,
+                             const float* scales, const float* x, const float* x_norm,
+                             const float* mean, const float* variance, float* scale_updates,
+                             float* mean_delta, float* variance_delta, float* weight_updates,
+                             float* workspace, float* state_delta);
 
 /* ---- several GPUs from ONE process (config 4) ---------------
  * gemmStridedBatched over n devices (devices[i] for slot i; a device may

@@ -47,6 +47,11 @@ _PROTO = {
     "ora_conv_backward": (C.c_int, [i64, i64, i64, i64, fp, fp, i64, i64, i64, i64, i64, i32,
                                     fp, fp, fp, fp, fp, fp]),
     "ora_fill_uniform": (None, [fp, i64, C.c_uint64, C.c_uint64, f32, f32]),
+    "ora_conv_backward_oh": (i64, [i64, i64, i64, i64, i64]),
+    "ora_conv_forward_train": (None, [i64, i64, i64, i64, fp, fp, i64, i64, i64, i64, i64, i32,
+                                      fp, fp, fp, fp, f32, i32, fp, fp, fp, fp, fp, fp, i32]),
+    "ora_conv_backward_bn": (C.c_int, [i64, i64, i64, i64, fp, fp, i64, i64, i64, i64, i64, i32,
+                                       fp, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp, fp, i32]),
 }
 
 _lib = None
@@ -189,16 +194,53 @@ def conv_forward(x, w, b, filters, k, stride, pad, act, dil=1):
 
 
 def conv_backward(x, w, filters, k, stride, pad, act, output, delta, bias_updates,
-                  weight_updates, state_delta=None):
+                  weight_updates, state_delta=None, dil=1):
     """Restated TConvolutionalLayer.backward; updates delta, bias_updates,
     weight_updates (and state_delta if given) in place."""
     batch, C_, H, W = x.shape
-    oh, ow = out_dim(H, pad, k, 1, stride), out_dim(W, pad, k, 1, stride)
+    oh, ow = out_dim(H, pad * dil, k, dil, stride), out_dim(W, pad * dil, k, dil, stride)
     ws = np.zeros(max(batch * C_ * k * k * oh * ow, 1), np.float32)
-    rc = lib().ora_conv_backward(batch, C_, H, W, _p(x), _p(w), filters, k, stride, pad, 1, act,
-                                 _p(output), _p(delta), _p(bias_updates), _p(weight_updates),
-                                 _p(ws), _p(state_delta) if state_delta is not None else None)
+    rc = lib().ora_conv_backward(batch, C_, H, W, _p(x), _p(w), filters, k, stride, pad, dil,
+                                 act, _p(output), _p(delta), _p(bias_updates),
+                                 _p(weight_updates), _p(ws),
+                                 _p(state_delta) if state_delta is not None else None)
     assert rc == 0, rc
+
+
+def conv_forward_train(x, w, filters, k, stride, pad, act, scales, biases, rmean, rvar,
+                       momentum, training, dil=1, quirk=0):
+    """Restated TConvolutionalLayer.forward with batch norm.  Updates
+    rmean / rvar in place; returns (out, mean, var, x, x_norm)."""
+    batch, C_, H, W = x.shape
+    oh, ow = out_dim(H, pad, k, dil, stride), out_dim(W, pad, k, dil, stride)
+    ws = np.zeros(max(batch * C_ * k * k * oh * ow, 1), np.float32)
+    out = np.zeros((batch, filters, oh, ow), np.float32)
+    m, v = np.zeros(filters, np.float32), np.zeros(filters, np.float32)
+    xs, xn = np.zeros_like(out), np.zeros_like(out)
+    lib().ora_conv_forward_train(batch, C_, H, W, _p(x), _p(w), filters, k, stride, pad, dil, act,
+                                 _p(scales), _p(biases), _p(rmean), _p(rvar), momentum,
+                                 int(training), _p(m), _p(v), _p(xs), _p(xn), _p(ws), _p(out),
+                                 int(quirk))
+    return out, m, v, xs, xn
+
+
+def conv_backward_bn(x, w, filters, k, stride, pad, act, output, delta, scales, xs, xn, mean,
+                     var, scale_updates, weight_updates, state_delta=None, dil=1, quirk=0):
+    """Restated TConvolutionalLayer.backward with batchNormBack; updates delta,
+    scale_updates, weight_updates (and state_delta) in place; returns
+    (mean_delta, variance_delta)."""
+    batch, C_, H, W = x.shape
+    oh, ow = out_dim(H, pad * dil, k, dil, stride), out_dim(W, pad * dil, k, dil, stride)
+    ws = np.zeros(max(batch * C_ * k * k * oh * ow, 1), np.float32)
+    md, vd = np.zeros(filters, np.float32), np.zeros(filters, np.float32)
+    rc = lib().ora_conv_backward_bn(batch, C_, H, W, _p(x), _p(w), filters, k, stride, pad, dil,
+                                    act, _p(output), _p(delta), _p(scales), _p(xs), _p(xn),
+                                    _p(mean), _p(var), _p(scale_updates), _p(md), _p(vd),
+                                    _p(weight_updates), _p(ws),
+                                    _p(state_delta) if state_delta is not None else None,
+                                    int(quirk))
+    assert rc == 0, rc
+    return md, vd
 
 
 _PROTO2 = {

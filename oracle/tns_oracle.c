@@ -509,21 +509,28 @@ void ora_conv_forward(int64_t batch, int64_t C, int64_t H, int64_t W, const floa
   ora_activate(out, batch * filters * oh * ow, act);
 }
 
-int ora_conv_backward(int64_t batch, int64_t C, int64_t H, int64_t W, const float* input,
-                      const float* weights, int64_t filters, int64_t kSize, int64_t stride,
-                      int64_t padding, int64_t dilation, int32_t act, const float* output,
-                      float* delta, float* bias_updates, float* weight_updates,
-                      float* workspace, float* state_delta) {
-  /* TConvolutionalLayer.backward, no batch-norm (nConvolutionLayer.pas:571-671) */
-  if (dilation != 1) return -1; /* backward pads with padding*dilation (632) while the
-                                   forward pads with padding (508): only d=1 is consistent */
-  int64_t oh = out_dim(H, padding, kSize, dilation, stride);
-  int64_t ow = out_dim(W, padding, kSize, dilation, stride);
+/* The backward's geometry (nConvolutionLayer.pas:571-671): delta and output
+ * are [batch][filters][outH*outW] with the layer's outH = (h + 2p - k) div s
+ * + 1 (92-100, no dilation), while the backward im2col / col2im pad with
+ * padding*dilation (640, 665).  Their column count equals outH*outW for the
+ * "same" paddings p = (k-1)/2 at any dilation; other combinations make the
+ * reference read past its workspace and are refused (returns 0). */
+int64_t ora_conv_backward_oh(int64_t H, int64_t kSize, int64_t stride, int64_t padding,
+                             int64_t dilation) {
+  int64_t layer = (H + 2 * padding - kSize) / stride + 1;
+  int64_t col = out_dim(H, padding * dilation, kSize, dilation, stride);
+  return layer == col ? layer : 0;
+}
+
+/* everything after the bias / batch-norm gradient: im2col, dW, dX + col2im */
+int ora_conv_backward_core(int64_t batch, int64_t C, int64_t H, int64_t W, const float* input,
+                           const float* weights, int64_t filters, int64_t kSize, int64_t stride,
+                           int64_t padding, int64_t dilation, const float* delta,
+                           float* weight_updates, float* workspace, float* state_delta) {
+  int64_t oh = ora_conv_backward_oh(H, kSize, stride, padding, dilation);
+  int64_t ow = ora_conv_backward_oh(W, kSize, stride, padding, dilation);
+  if (!oh || !ow) return -1;
   int64_t i_m = filters, i_n = kSize * kSize * C, i_k = oh * ow, colSize = i_n * i_k;
-  /* Derivative(): delta *= f'(output) */
-  if (ora_gradient(output, batch * filters * i_k, act, delta)) return -2;
-  /* bias_updates.addSums(delta) */
-  ora_add_sums(bias_updates, delta, batch, filters, i_k);
   /* state.input.im2Col(k, k, p*d, p*d, stride_y, stride_x, d, d, workspace) */
   ora_im2col_strided_batched(C, H, W, kSize, kSize, padding * dilation, padding * dilation,
                              stride, stride, dilation, dilation, input, C * H * W, 0, workspace,
@@ -541,6 +548,24 @@ int ora_conv_backward(int64_t batch, int64_t C, int64_t H, int64_t W, const floa
                                state_delta, C * H * W, 0, batch);
   }
   return 0;
+}
+
+int ora_conv_backward(int64_t batch, int64_t C, int64_t H, int64_t W, const float* input,
+                      const float* weights, int64_t filters, int64_t kSize, int64_t stride,
+                      int64_t padding, int64_t dilation, int32_t act, const float* output,
+                      float* delta, float* bias_updates, float* weight_updates,
+                      float* workspace, float* state_delta) {
+  /* TConvolutionalLayer.backward, no batch-norm (nConvolutionLayer.pas:571-671) */
+  int64_t oh = ora_conv_backward_oh(H, kSize, stride, padding, dilation);
+  int64_t ow = ora_conv_backward_oh(W, kSize, stride, padding, dilation);
+  if (!oh || !ow) return -1;
+  int64_t i_k = oh * ow;
+  /* Derivative(): delta *= f'(output) */
+  if (ora_gradient(output, batch * filters * i_k, act, delta)) return -2;
+  /* bias_updates.addSums(delta) */
+  ora_add_sums(bias_updates, delta, batch, filters, i_k);
+  return ora_conv_backward_core(batch, C, H, W, input, weights, filters, kSize, stride, padding,
+                                dilation, delta, weight_updates, workspace, state_delta);
 }
 
 void ora_fuse_batchnorm(int64_t filters, int64_t filterSize, float* weights, float* biases,

@@ -104,13 +104,46 @@ void    ora_conv_forward(int64_t batch, int64_t C, int64_t H, int64_t W,
  * 571-671): delta *= f'(output); bias_updates.addSums(delta); im2col(input);
  * weight_updates += delta_b.col_b^T per image (NT, beta 1); if state_delta:
  * col = W^T.delta (TN strided batched, beta 0) and col2im-accumulate.
- * Returns -1 for dilation != 1 (the reference pads the backward im2col with
- * padding*dilation but the forward with padding). */
+ * The backward im2col / col2im pad with padding*dilation (640, 665); returns
+ * -1 when that geometry does not give the layer's outH x outW columns. */
 int     ora_conv_backward(int64_t batch, int64_t C, int64_t H, int64_t W,
                           const float* input, const float* weights, int64_t filters,
                           int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
                           int32_t act, const float* output, float* delta, float* bias_updates,
                           float* weight_updates, float* workspace, float* state_delta);
+/* output rows of the backward's im2col (padding*dilation) when they equal
+ * the layer's outH (no dilation), else 0 (refused geometry) */
+int64_t ora_conv_backward_oh(int64_t H, int64_t kSize, int64_t stride, int64_t padding,
+                             int64_t dilation);
+int     ora_conv_backward_core(int64_t batch, int64_t C, int64_t H, int64_t W,
+                               const float* input, const float* weights, int64_t filters,
+                               int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                               const float* delta, float* weight_updates, float* workspace,
+                               float* state_delta);
+/* TConvolutionalLayer.forward in training with batch norm (nConvolutionLayer.
+ * pas:457-569 -> TBaseLayer.batchNorm, nbaselayer.pas:336-370): Conv2D, then
+ * (training) MeansAndVars, rolling updates with bnMomentum, x := output,
+ * blockNormalize, x_norm := output, or (inference) blockNormalize with the
+ * rolling statistics; forwardScale, forwardBias, activate. */
+void    ora_conv_forward_train(int64_t batch, int64_t C, int64_t H, int64_t W,
+                               const float* input, const float* weights, int64_t filters,
+                               int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                               int32_t act, const float* scales, const float* biases,
+                               float* rolling_mean, float* rolling_variance, float momentum,
+                               int32_t training, float* mean, float* variance, float* x,
+                               float* x_norm, float* workspace, float* out, int32_t quirk);
+/* TConvolutionalLayer.backward with batch norm: Derivative, batchNormBack
+ * (nbaselayer.pas:372-395: addDots into scale_updates, forwardScale,
+ * MeansAndVarsDelta, normalizeDelta — no bias_updates term), then the
+ * weight and input gradients as ora_conv_backward. */
+int     ora_conv_backward_bn(int64_t batch, int64_t C, int64_t H, int64_t W,
+                             const float* input, const float* weights, int64_t filters,
+                             int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                             int32_t act, const float* output, float* delta,
+                             const float* scales, const float* x, const float* x_norm,
+                             const float* mean, const float* variance, float* scale_updates,
+                             float* mean_delta, float* variance_delta, float* weight_updates,
+                             float* workspace, float* state_delta, int32_t quirk);
 /* fuseBatchNorm (nConvolutionLayer.pas:102-126). */
 void    ora_fuse_batchnorm(int64_t filters, int64_t filterSize, float* weights,
                            float* biases, const float* scales, const float* rollingMean,

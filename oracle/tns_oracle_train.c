@@ -15,9 +15,13 @@
  *
  * Where the reference's AVX2 kernels are approximate or buggy (snormvss_avx
  * uses rcpss; srss drops upper lanes when N%8==0 — SURVEY Appendix B.5/B.6)
- * the scalar Pascal form is restated instead.  Transcendentals (exp, ln,
- * Power) are evaluated in double and rounded once, so these functions are a
- * tolerance oracle (1e-4 relative), not a bit-exact one.
+ * the scalar Pascal form is restated instead (quirk switches reproduce the
+ * srss / sVarinceDelta_avx lane drop).  Transcendentals (exp, ln, Power) are
+ * evaluated in double and rounded once, as the device does; FPC evaluates
+ * them in extended precision, so a last-ulp difference from the reference
+ * itself is possible (parity unpinned).
+ *   conv layer with batch norm: nConvolutionLayer.pas:457-671 with
+ *   TBaseLayer.batchNorm / batchNormBack (nbaselayer.pas:336-395)
  */
 #include <math.h>
 #include <stdlib.h>
@@ -239,6 +243,62 @@ void ora_normalize_delta(const float* x, const float* mean, const float* var,
         dd[k] = a + t;
       }
     }
+}
+
+/* ---- convolutional layer with batch norm (training) ----------------------- */
+void ora_conv_forward_train(int64_t batch, int64_t C, int64_t H, int64_t W, const float* input,
+                            const float* weights, int64_t filters, int64_t kSize, int64_t stride,
+                            int64_t padding, int64_t dilation, int32_t act, const float* scales,
+                            const float* biases, float* rolling_mean, float* rolling_variance,
+                            float momentum, int32_t training, float* mean, float* variance,
+                            float* x, float* x_norm, float* workspace, float* out,
+                            int32_t quirk) {
+  /* state.input.Conv2D(weights, output, ...) (nConvolutionLayer.pas:508) */
+  ora_conv2d(batch, C, H, W, input, weights, filters, kSize, kSize, padding, padding, stride,
+             stride, dilation, dilation, workspace, out);
+  const int64_t bs = (H + 2 * padding - (dilation * (kSize - 1) + 1)) / stride + 1;
+  const int64_t bsw = (W + 2 * padding - (dilation * (kSize - 1) + 1)) / stride + 1;
+  const int64_t blk = bs * bsw, n = batch * filters * blk;
+  if (training) { /* TBaseLayer.batchNorm (nbaselayer.pas:351-359) */
+    ora_means_and_vars_q(out, batch, filters, blk, mean, variance, quirk);
+    const float keep = 1.0f - momentum;
+    for (int64_t i = 0; i < filters; i++) { /* Multiply(1-m), then axpy(m, stat) (saxpy FMA) */
+      rolling_mean[i] = rolling_mean[i] * keep;
+      rolling_mean[i] = fmaf(momentum, mean[i], rolling_mean[i]);
+      rolling_variance[i] = rolling_variance[i] * keep;
+      rolling_variance[i] = fmaf(momentum, variance[i], rolling_variance[i]);
+    }
+    memcpy(x, out, sizeof(float) * n);
+    ora_normalize(out, batch, filters, blk, mean, variance);
+    memcpy(x_norm, out, sizeof(float) * n);
+  } else {
+    ora_normalize(out, batch, filters, blk, rolling_mean, rolling_variance);
+  }
+  ora_forward_scale(out, batch, filters, blk, scales); /* forwardScale (vsMulB) */
+  ora_add_bias(filters, out, blk, biases, 1, batch);  /* forwardBias (vsAddB) */
+  ora_activate(out, n, act);
+}
+
+int ora_conv_backward_bn(int64_t batch, int64_t C, int64_t H, int64_t W, const float* input,
+                         const float* weights, int64_t filters, int64_t kSize, int64_t stride,
+                         int64_t padding, int64_t dilation, int32_t act, const float* output,
+                         float* delta, const float* scales, const float* x, const float* x_norm,
+                         const float* mean, const float* variance, float* scale_updates,
+                         float* mean_delta, float* variance_delta, float* weight_updates,
+                         float* workspace, float* state_delta, int32_t quirk) {
+  const int64_t oh = ora_conv_backward_oh(H, kSize, stride, padding, dilation);
+  const int64_t ow = ora_conv_backward_oh(W, kSize, stride, padding, dilation);
+  if (!oh || !ow) return -1;
+  const int64_t blk = oh * ow;
+  if (ora_gradient(output, batch * filters * blk, act, delta)) return -2;
+  /* batchNormBack (nbaselayer.pas:372-395) */
+  ora_add_dots(scale_updates, x_norm, delta, batch, filters, blk);
+  ora_forward_scale(delta, batch, filters, blk, scales);
+  ora_mean_var_delta_q(delta, x, mean, variance, batch, filters, blk, mean_delta, variance_delta,
+                       quirk);
+  ora_normalize_delta(x, mean, variance, mean_delta, variance_delta, delta, batch, filters, blk);
+  return ora_conv_backward_core(batch, C, H, W, input, weights, filters, kSize, stride, padding,
+                                dilation, delta, weight_updates, workspace, state_delta);
 }
 
 /* softmax (nsoftmaxlayer.pas:83-106) over n elements with stride. */

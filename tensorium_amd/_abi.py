@@ -87,6 +87,12 @@ PROTOTYPES: dict[str, tuple] = {
                                        i64, i64, i32, fptr, fptr, i32]),
     "tns_hip_conv_backward": (C.c_int, [vp, i64, i64, i64, i64, fptr, fptr, i64, i64, i64, i64,
                                         i64, i32, fptr, fptr, fptr, fptr, fptr, fptr]),
+    "tns_hip_conv_forward_train": (C.c_int, [vp, i64, i64, i64, i64, fptr, fptr, i64, i64, i64,
+                                             i64, i64, i32, fptr, fptr, fptr, fptr, f32, i32,
+                                             fptr, fptr, fptr, fptr, fptr, fptr]),
+    "tns_hip_conv_backward_bn": (C.c_int, [vp, i64, i64, i64, i64, fptr, fptr, i64, i64, i64,
+                                           i64, i64, i32, fptr, fptr, fptr, fptr, fptr, fptr,
+                                           fptr, fptr, fptr, fptr, fptr, fptr, fptr]),
     "tns_hip_set_telemetry": (C.c_int, [vp, i32]),
     "tns_gemm_variant_count": (C.c_int, []),
     "tns_gemm_variant_name": (C.c_char_p, [i32]),

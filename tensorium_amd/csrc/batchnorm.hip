@@ -12,6 +12,7 @@
 // blockSize 1, groups = batch); larger channels (conv BN) give each block's
 // 8 AVX2 lanes to 8 GPU lanes and add the block results in order.  Transcendentals (exp, ln, pow) are evaluated in
 // double and rounded once, as the oracle does.
+#include "tns_act.hpp"
 #include "tns_internal.hpp"
 
 namespace tns {
@@ -467,6 +468,98 @@ hipError_t run_finish(const float* part0, const float* part1, int64_t groups, in
 // blocks long enough for the chain kernels (shorter ones: one thread per
 // channel, which is also the only form for blockSize 1)
 bool use_chains(int64_t bs, const float* part) { return part != nullptr && bs >= 64; }
+
+// ---- conv layer batch norm, forward (TBaseLayer.batchNorm + activate) -----
+// One pass instead of the reference's six (CopyTo(x), blockNormalize,
+// copyTo(x_norm), forwardScale, forwardBias, activate; nbaselayer.pas:351-
+// 365, nConvolutionLayer.pas:530-545) with the same per-element roundings:
+// x := y; xn := (y - m) / sd; out := act(xn*scale + bias), sd as
+// blockNormalize (bs == 1: sqrt(max(v, eps)); bs > 1: max(sqrt(v), eps)).
+template <int V>
+__global__ __launch_bounds__(TPB) void bn_apply_k(const float* y,  // may alias out
+                                                  float* __restrict__ x, float* __restrict__ xn,
+                                                  float* out, int64_t total_v,
+                                                  int64_t N, int64_t bs,
+                                                  const float* __restrict__ means,
+                                                  const float* __restrict__ vars,
+                                                  const float* __restrict__ scales,
+                                                  const float* __restrict__ biases, int act) {
+  for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < total_v;
+       e += (int64_t)gridDim.x * TPB) {
+    float v[V], a[V], o[V];
+    if constexpr (V == 4) {
+      const float4 t = reinterpret_cast<const float4*>(y)[e];
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+    } else {
+      v[0] = y[e];
+    }
+    const int64_t i = ((e * V) / bs) % N;  // bs % V == 0: one channel per vector
+    const float m = means[i], var = vars[i], sc = scales[i], bi = biases[i];
+    float sd;
+    if (bs == 1) {
+      sd = sqrtf(var > SEPS ? var : SEPS);
+    } else {
+      sd = sqrtf(var);
+      sd = sd > SEPS ? sd : SEPS;
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      a[j] = (v[j] - m) / sd;
+      float t = a[j] * sc;
+      t = t + bi;
+      o[j] = act_apply(t, act);
+    }
+    if constexpr (V == 4) {
+      if (x) reinterpret_cast<float4*>(x)[e] = make_float4(v[0], v[1], v[2], v[3]);
+      if (xn) reinterpret_cast<float4*>(xn)[e] = make_float4(a[0], a[1], a[2], a[3]);
+      reinterpret_cast<float4*>(out)[e] = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+      if (x) x[e] = v[0];
+      if (xn) xn[e] = a[0];
+      out[e] = o[0];
+    }
+  }
+}
+
+// rolling_mean.Multiply(1 - m); rolling_mean.axpy(m, mean) and the same for
+// the variance (nbaselayer.pas:353-356): one multiply, then one FMA
+__global__ void rolling_update_k(int64_t n, float* __restrict__ rm, float* __restrict__ rv,
+                                 const float* __restrict__ mean, const float* __restrict__ var,
+                                 float keep, float mom) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= n) return;
+  rm[i] = fmaf(mom, mean[i], rm[i] * keep);
+  rv[i] = fmaf(mom, var[i], rv[i] * keep);
+}
+
+}  // namespace
+
+hipError_t launch_bn_apply(const float* y, float* x, float* xn, float* out, int64_t groups,
+                           int64_t N, int64_t bs, const float* means, const float* vars,
+                           const float* scales, const float* biases, int act, hipStream_t s) {
+  const int64_t total = groups * N * bs;
+  if (total <= 0) return hipSuccess;
+  const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  const bool v4 = bs % 4 == 0 && al(y) && al(out) && (!x || al(x)) && (!xn || al(xn));
+  if (v4)
+    hipLaunchKernelGGL(bn_apply_k<4>, dim3(nblk(total / 4)), dim3(TPB), 0, s, y, x, xn, out,
+                       total / 4, N, bs, means, vars, scales, biases, act);
+  else
+    hipLaunchKernelGGL(bn_apply_k<1>, dim3(nblk(total)), dim3(TPB), 0, s, y, x, xn, out, total,
+                       N, bs, means, vars, scales, biases, act);
+  return hipGetLastError();
+}
+
+hipError_t launch_rolling_update(int64_t n, float* rm, float* rv, const float* mean,
+                                 const float* var, float momentum, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const float keep = 1.0f - momentum;
+  hipLaunchKernelGGL(rolling_update_k, dim3(nblk(n)), dim3(TPB), 0, s, n, rm, rv, mean, var, keep,
+                     momentum);
+  return hipGetLastError();
+}
+
+namespace {
 }  // namespace
 
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,

@@ -1113,20 +1113,22 @@ int tns_hip_conv2d(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
                  0.0f, out, outImg, outImg * filters, batch, EPI_NONE, nullptr, 0, true);
 }
 
-int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
-                         const float* input, const float* weights, const float* biases,
-                         int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
-                         int64_t dilation, int32_t activation, float* workspace, float* out,
-                         int32_t fused) {
-  if (int r = check_ctx(c)) return r;
-  if (!act_supported(activation))
-    return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
+namespace {
+// TConvolutionalLayer.forward's Conv2D, with forwardBias + activate fused into
+// the GEMM epilogue (bias_act) or the bare convolution (the batch-norm path,
+// whose statistics need the raw output)
+int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                      const float* input, const float* weights, const float* biases,
+                      int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
+                      int64_t dilation, int32_t activation, float* workspace, float* out,
+                      int32_t fused, bool bias_act) {
   const int64_t oh = out_dim(H, padding, kSize, dilation, stride);
   const int64_t ow = out_dim(W, padding, kSize, dilation, stride);
   if (!fused) {
     if (int r = tns_hip_conv2d(c, batch, C, H, W, input, weights, filters, kSize, kSize, padding,
                                padding, stride, stride, dilation, dilation, workspace, out))
       return r;
+    if (!bias_act) return TNS_OK;
     OpTimer t(c, TNS_OP_BIAS);
     return hip_status(launch_bias_activate(out, filters, oh * ow, biases, batch, activation,
                                            c->stream),
@@ -1155,7 +1157,7 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
       direct_ok && (fused == TNS_CONV_IMPLICIT || (fused == TNS_CONV_FUSED && fits));
   if (implicit) {
     // implicit GEMM: batch folded into N, B gathered from zero-padded images
-    if (!input || !weights || !out || !biases)
+    if (!input || !weights || !out || (bias_act && !biases))
       return set_error(TNS_ERR_ARG, "conv_forward: null operand");
     // Materialise the zero border (padded images, no bounds checks in the
     // GEMM) when that copy costs under ~5% of the GEMM: copy time
@@ -1194,7 +1196,7 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
       a.A = weights; a.lda = k; a.strideA = 0;
       a.B = src + b0 * img; a.ldb = outImg; a.strideB = img;
       a.C = out + b0 * outImg * filters; a.ldc = outImg; a.strideC = outImg * filters;
-      a.batch = 1; a.epi = EPI_BIAS_ACT; a.bias = biases;
+      a.batch = 1; a.epi = bias_act ? EPI_BIAS_ACT : EPI_NONE; a.bias = biases;
       a.act = act_transcendental(activation) ? 4 : activation;
       a.conv = padded ? 1 : 2; a.ktab = kt; a.ktab_n = (int)(k + KTAB_PAD);
       a.conv_H = (int)Hs; a.conv_W = (int)Ws; a.conv_ow = (int)ow; a.conv_ohw = (int)outImg;
@@ -1208,7 +1210,7 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
                          (long long)g_conv_variant);
       if (int r = hip_status(e, "implicit conv launch")) return r;
     }
-    if (act_transcendental(activation)) {
+    if (bias_act && act_transcendental(activation)) {
       OpTimer t(c, TNS_OP_ACTIVATE);
       return hip_status(launch_activate(out, batch * filters * outImg, activation, c->stream),
                         "activate launch");
@@ -1237,49 +1239,144 @@ int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_
   // (logistic / tanh: bias in the epilogue, activation in its own pass)
   const bool transc = act_transcendental(activation);
   if (int r = do_gemm(c, false, false, filters, outImg, k, 1.0f, weights, k, 0, Bp, outImg,
-                      strideB, 0.0f, out, outImg, outImg * filters, batch, EPI_BIAS_ACT, biases,
-                      transc ? 4 : activation, true))
+                      strideB, 0.0f, out, outImg, outImg * filters, batch,
+                      bias_act ? EPI_BIAS_ACT : EPI_NONE, biases, transc ? 4 : activation, true))
     return r;
-  if (!transc) return TNS_OK;
+  if (!transc || !bias_act) return TNS_OK;
   OpTimer t(c, TNS_OP_ACTIVATE);
   return hip_status(launch_activate(out, batch * filters * outImg, activation, c->stream),
                     "activate launch");
 }
+}  // namespace
 
-int tns_hip_conv_backward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
-                          const float* input, const float* weights, int64_t filters,
-                          int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
-                          int32_t activation, const float* output, float* delta,
-                          float* bias_updates, float* weight_updates, float* workspace,
-                          float* state_delta) {
+int tns_hip_conv_forward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                         const float* input, const float* weights, const float* biases,
+                         int64_t filters, int64_t kSize, int64_t stride, int64_t padding,
+                         int64_t dilation, int32_t activation, float* workspace, float* out,
+                         int32_t fused) {
   if (int r = check_ctx(c)) return r;
-  if (dilation != 1)
-    return set_error(TNS_ERR_UNSUPPORTED,
-                     "conv_backward: dilation %lld (the reference pads the backward im2col "
-                     "with padding*dilation, nConvolutionLayer.pas:632, but the forward with "
-                     "padding; only dilation 1 is consistent)",
-                     (long long)dilation);
   if (!act_supported(activation))
     return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
-  ConvGeom g = geom(C, H, W, kSize, kSize, padding, padding, stride, stride, 1, 1);
+  return conv_forward_impl(c, batch, C, H, W, input, weights, biases, filters, kSize, stride,
+                           padding, dilation, activation, workspace, out, fused, true);
+}
+
+int tns_hip_conv_forward_train(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                               const float* input, const float* weights, int64_t filters,
+                               int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                               int32_t activation, const float* scales, const float* biases,
+                               float* rolling_mean, float* rolling_variance, float bnMomentum,
+                               int32_t training, float* mean, float* variance, float* x,
+                               float* x_norm, float* workspace, float* out) {
+  if (int r = check_ctx(c)) return r;
+  if (!act_supported(activation))
+    return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
+  if (!scales || !biases || !rolling_mean || !rolling_variance || !out ||
+      (training && (!mean || !variance || !x || !x_norm)))
+    return set_error(TNS_ERR_ARG, "conv_forward_train: null operand");
+  const int64_t oh = out_dim(H, padding, kSize, dilation, stride);
+  const int64_t ow = out_dim(W, padding, kSize, dilation, stride);
+  if (oh <= 0 || ow <= 0 || batch <= 0 || filters <= 0) return TNS_OK;
+  const int64_t bs = oh * ow;
+  // state.input.Conv2D(weights, output, ...) (nConvolutionLayer.pas:508)
+  if (int r = conv_forward_impl(c, batch, C, H, W, input, weights, nullptr, filters, kSize,
+                                stride, padding, dilation, activation, workspace, out,
+                                TNS_CONV_FUSED, false))
+    return r;
+  OpTimer t(c, TNS_OP_BIAS);
+  if (!training)  // blockNormalize with the rolling statistics, scale, bias, activate
+    return hip_status(launch_bn_apply(out, nullptr, nullptr, out, batch, filters, bs,
+                                      rolling_mean, rolling_variance, scales, biases, activation,
+                                      c->stream),
+                      "batchNorm launch");
+  float* part;
+  if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
+  if (int r = hip_status(launch_means_vars(out, batch, filters, bs, mean, variance,
+                                           (int)g_srss_quirk, part, c->stream),
+                         "meansAndVars launch"))
+    return r;
+  if (int r = hip_status(launch_rolling_update(filters, rolling_mean, rolling_variance, mean,
+                                               variance, bnMomentum, c->stream),
+                         "rolling update launch"))
+    return r;
+  return hip_status(launch_bn_apply(out, x, x_norm, out, batch, filters, bs, mean, variance,
+                                    scales, biases, activation, c->stream),
+                    "batchNorm launch");
+}
+
+namespace {
+struct ConvBN {  // batchNormBack operands (nbaselayer.pas:372-395); scales == nullptr: none
+  const float *scales, *x, *x_norm, *mean, *variance;
+  float *scale_updates, *mean_delta, *variance_delta;
+};
+
+int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                       const float* input, const float* weights, int64_t filters, int64_t kSize,
+                       int64_t stride, int64_t padding, int64_t dilation, int32_t activation,
+                       const float* output, float* delta, float* bias_updates,
+                       float* weight_updates, float* workspace, float* state_delta,
+                       const ConvBN& bn) {
+  if (int r = check_ctx(c)) return r;
+  if (!act_supported(activation))
+    return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
+  // delta / output are [batch][filters][outH*outW] with the layer's outH =
+  // (h + 2p - k) div s + 1 (nConvolutionLayer.pas:92-100); the backward
+  // im2col / col2im pad with padding*dilation (640, 665), which yields those
+  // columns for the "same" paddings at any dilation — other geometries make
+  // the reference read past its workspace and are refused
+  ConvGeom g = geom(C, H, W, kSize, kSize, padding * dilation, padding * dilation, stride, stride,
+                    dilation, dilation);
   if (int r = check_geom(g)) return r;
+  if (g.oh != (H + 2 * padding - kSize) / stride + 1 ||
+      g.ow != (W + 2 * padding - kSize) / stride + 1)
+    return set_error(TNS_ERR_UNSUPPORTED,
+                     "conv_backward: dilation %lld with padding %lld gives %lldx%lld im2col "
+                     "columns but the layer's output is %lldx%lld (nConvolutionLayer.pas:92-100, "
+                     "640)",
+                     (long long)dilation, (long long)padding, (long long)g.oh, (long long)g.ow,
+                     (long long)((H + 2 * padding - kSize) / stride + 1),
+                     (long long)((W + 2 * padding - kSize) / stride + 1));
   const int64_t i_m = filters, i_n = kSize * kSize * C, i_k = g.oh * g.ow;
   const int64_t colSize = i_n * i_k;
   if (batch <= 0 || i_k <= 0 || filters <= 0) return TNS_OK;
-  if (!input || !weights || !output || !delta || !bias_updates || !weight_updates)
+  if (!input || !weights || !output || !delta || !weight_updates || (!bn.scales && !bias_updates))
     return set_error(TNS_ERR_ARG, "conv_backward: null operand");
+  if (bn.scales && (!bn.x || !bn.x_norm || !bn.mean || !bn.variance || !bn.scale_updates ||
+                    !bn.mean_delta || !bn.variance_delta))
+    return set_error(TNS_ERR_ARG, "conv_backward: null batch-norm operand");
   // Derivative(): delta *= f'(output)
   if (int r = hip_status(launch_derive(output, batch * filters * i_k, activation, delta,
                                        c->stream), "derive launch"))
     return r;
-  // bias_updates.addSums(delta)
   float* part;
   if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
-  if (int r = hip_status(launch_add_sums(bias_updates, delta, batch, filters, i_k, part,
-                                         c->stream), "addSums launch"))
-    return r;
+  if (bn.scales) {
+    // batchNormBack: scale_updates.addDots(x_norm, delta); delta.forwardScale
+    // (scales); MeansAndVarsDelta; normalizeDelta — and no bias_updates term
+    // (nConvolutionLayer.pas:601-604)
+    if (int r = hip_status(launch_add_dots(bn.scale_updates, bn.x_norm, delta, batch, filters, i_k,
+                                           part, c->stream), "addDots launch"))
+      return r;
+    if (int r = hip_status(launch_scale_add(delta, batch, filters, i_k, bn.scales, nullptr, 1,
+                                            c->stream), "forwardScale launch"))
+      return r;
+    if (int r = hip_status(launch_mean_var_delta(delta, bn.x, bn.mean, bn.variance, batch, filters,
+                                                 i_k, bn.mean_delta, bn.variance_delta,
+                                                 (int)g_srss_quirk, part, c->stream),
+                           "meansAndVarsDelta launch"))
+      return r;
+    if (int r = hip_status(launch_normalize_delta(bn.x, bn.mean, bn.variance, bn.mean_delta,
+                                                  bn.variance_delta, delta, batch, filters, i_k,
+                                                  c->stream), "normalizeDelta launch"))
+      return r;
+  } else {
+    // bias_updates.addSums(delta)
+    if (int r = hip_status(launch_add_sums(bias_updates, delta, batch, filters, i_k, part,
+                                           c->stream), "addSums launch"))
+      return r;
+  }
   // state.input.im2Col(...) — a 1x1/s1/p0 col matrix is the input itself
-  const bool needs_col = kSize != 1 || stride != 1 || padding != 0;
+  const bool needs_col = kSize != 1 || stride != 1 || padding != 0 || dilation != 1;
   float* ws = workspace;
   if (!ws && (needs_col || state_delta))
     if (int r = ensure_scratch(c, 0, batch * colSize, &ws)) return r;
@@ -1331,6 +1428,33 @@ int tns_hip_conv_backward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64
   OpTimer t(c, TNS_OP_COL2IM);
   return hip_status(launch_col2im(g, ws, colSize, state_delta, C * H * W, batch, c->stream),
                     "col2im launch");
+}
+}  // namespace
+
+int tns_hip_conv_backward(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                          const float* input, const float* weights, int64_t filters,
+                          int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                          int32_t activation, const float* output, float* delta,
+                          float* bias_updates, float* weight_updates, float* workspace,
+                          float* state_delta) {
+  return conv_backward_impl(c, batch, C, H, W, input, weights, filters, kSize, stride, padding,
+                            dilation, activation, output, delta, bias_updates, weight_updates,
+                            workspace, state_delta, ConvBN{});
+}
+
+int tns_hip_conv_backward_bn(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W,
+                             const float* input, const float* weights, int64_t filters,
+                             int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
+                             int32_t activation, const float* output, float* delta,
+                             const float* scales, const float* x, const float* x_norm,
+                             const float* mean, const float* variance, float* scale_updates,
+                             float* mean_delta, float* variance_delta, float* weight_updates,
+                             float* workspace, float* state_delta) {
+  if (!scales) return set_error(TNS_ERR_ARG, "conv_backward_bn: null scales");
+  ConvBN bn{scales, x, x_norm, mean, variance, scale_updates, mean_delta, variance_delta};
+  return conv_backward_impl(c, batch, C, H, W, input, weights, filters, kSize, stride, padding,
+                            dilation, activation, output, delta, nullptr, weight_updates,
+                            workspace, state_delta, bn);
 }
 
 int tns_gemm_variant_count(void) { return sgemm_variant_count(); }

@@ -175,6 +175,13 @@ hipError_t launch_mean_var_delta(const float* delta, const float* x, const float
 hipError_t launch_normalize_delta(const float* x, const float* mean, const float* var,
                                   const float* mean_delta, const float* var_delta, float* delta,
                                   int64_t groups, int64_t N, int64_t bs, hipStream_t s);
+// fused conv-layer BN forward: x := y, xn := normalize(y), out :=
+// act(xn*scale + bias); x / xn may be nullptr (inference); out may alias y
+hipError_t launch_bn_apply(const float* y, float* x, float* xn, float* out, int64_t groups,
+                           int64_t N, int64_t bs, const float* means, const float* vars,
+                           const float* scales, const float* biases, int act, hipStream_t s);
+hipError_t launch_rolling_update(int64_t n, float* rm, float* rv, const float* mean,
+                                 const float* var, float momentum, hipStream_t s);
 hipError_t launch_softmax_batch(int64_t n, const float* in, int64_t batch, int64_t batch_size,
                                 int64_t groups, int64_t group_size, int64_t stride, float temp,
                                 float* out, hipStream_t s);

@@ -255,6 +255,27 @@ class TNNHip:
             padding, dilation, int(activation), _ptr(output), _ptr(delta), _ptr(bias_updates),
             _ptr(weight_updates), _ptr(workspace), _ptr(state_delta)))
 
+    def convForwardTrain(self, batch, C_, H, W, input, weights, filters, kSize, stride, padding,
+                         dilation, activation, scales, biases, rolling_mean, rolling_variance,
+                         bnMomentum, training, mean, variance, x, x_norm, workspace, out):
+        """TConvolutionalLayer.forward with batch norm (training or not)."""
+        check(self.lib.tns_hip_conv_forward_train(
+            self.ctx, batch, C_, H, W, _ptr(input), _ptr(weights), filters, kSize, stride, padding,
+            dilation, int(activation), _ptr(scales), _ptr(biases), _ptr(rolling_mean),
+            _ptr(rolling_variance), float(bnMomentum), int(bool(training)), _ptr(mean),
+            _ptr(variance), _ptr(x), _ptr(x_norm), _ptr(workspace), _ptr(out)))
+
+    def convBackwardBN(self, batch, C_, H, W, input, weights, filters, kSize, stride, padding,
+                       dilation, activation, output, delta, scales, x, x_norm, mean, variance,
+                       scale_updates, mean_delta, variance_delta, weight_updates, workspace=None,
+                       state_delta=None):
+        """TConvolutionalLayer.backward with batchNormBack; delta in place."""
+        check(self.lib.tns_hip_conv_backward_bn(
+            self.ctx, batch, C_, H, W, _ptr(input), _ptr(weights), filters, kSize, stride, padding,
+            dilation, int(activation), _ptr(output), _ptr(delta), _ptr(scales), _ptr(x),
+            _ptr(x_norm), _ptr(mean), _ptr(variance), _ptr(scale_updates), _ptr(mean_delta),
+            _ptr(variance_delta), _ptr(weight_updates), _ptr(workspace), _ptr(state_delta)))
+
     def setConvVariant(self, variant: int = -1):
         """Force the implicit-GEMM tile shape (-1 = heuristic); process-wide."""
         check(self.lib.tns_set_option(1, int(variant)))

@@ -175,6 +175,140 @@ def test_conv_backward_yolov3_batch8(hip, torch_cuda, ora, idx):
     assert np.array_equal(dbu.cpu().numpy(), rbu)
 
 
+def _t(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()
+
+
+BN_CASES = [(2, 3, 17, 8, 3, 1, 1, 9, 1), (3, 5, 12, 7, 3, 2, 1, 9, 1), (2, 16, 9, 5, 1, 1, 0, 4, 1),
+            (2, 6, 13, 33, 3, 1, 1, 0, 1), (2, 4, 15, 6, 3, 1, 1, 9, 2)]
+
+
+@pytest.mark.parametrize("quirk", [0, 1])
+@pytest.mark.parametrize("batch,C,H,F,k,s,p,act,dil", BN_CASES)
+def test_conv_train_batchnorm_forward_backward(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act,
+                                               dil, quirk):
+    """TConvolutionalLayer.forward (training, batch norm) and .backward with
+    batchNormBack, bit-exact: output, x, x_norm, mean, variance, rolling
+    statistics; delta, scale_updates, mean/variance_delta, weight_updates,
+    state_delta — with and without the srss / sVarinceDelta lane drop."""
+    T = torch_cuda
+    rng = np.random.default_rng(batch * 7 + C + H + dil)
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.3, 0.3, F * C * k * k).astype(np.float32)
+    sc = rng.uniform(0.5, 1.5, F).astype(np.float32)
+    b = rng.uniform(-0.2, 0.2, F).astype(np.float32)
+    rm, rv = rng.uniform(-0.1, 0.1, F).astype(np.float32), rng.uniform(0.5, 2, F).astype(np.float32)
+    R = [a.copy() for a in (rm, rv)]
+    out, m, v, xs, xn = ora.conv_forward_train(x, w, F, k, s, p, act, sc, b, R[0], R[1], 0.1,
+                                               True, dil=dil, quirk=quirk)
+    dx, dw, dsc, db, drm, drv = (_t(T, a) for a in (x, w, sc, b, rm, rv))
+    g = {n: T.zeros(a.shape, device="cuda") for n, a in
+         (("out", out), ("m", m), ("v", v), ("xs", xs), ("xn", xn))}
+    hip.setSrssQuirk(bool(quirk))
+    try:
+        hip.convForwardTrain(batch, C, H, H, dx, dw, F, k, s, p, dil, act, dsc, db, drm, drv, 0.1,
+                             True, g["m"], g["v"], g["xs"], g["xn"], None, g["out"])
+        hip.finish()
+        for n, r in (("out", out), ("m", m), ("v", v), ("xs", xs), ("xn", xn)):
+            assert np.array_equal(g[n].cpu().numpy(), r), n
+        assert np.array_equal(drm.cpu().numpy(), R[0]) and np.array_equal(drv.cpu().numpy(), R[1])
+        # backward with batchNormBack: its geometry is the layer's outH (no
+        # dilation, nConvolutionLayer.pas:92-100), which differs from the
+        # dilated forward's rows — the reference's dilated layer cannot run
+        # forward and backward on one tensor, so that case stops here
+        if ora.lib().ora_conv_backward_oh(H, k, s, p, dil) != out.shape[2]:
+            return
+        d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+        su0 = rng.uniform(-1, 1, F).astype(np.float32)
+        wu0 = rng.uniform(-1, 1, w.size).astype(np.float32)
+        sd0 = rng.uniform(-1, 1, x.shape).astype(np.float32)
+        rd, rsu, rwu, rsd = d0.copy(), su0.copy(), wu0.copy(), sd0.copy()
+        md, vd = ora.conv_backward_bn(x, w, F, k, s, p, act, out, rd, sc, xs, xn, m, v, rsu, rwu,
+                                      rsd, dil=dil, quirk=quirk)
+        dd, dsu, dwu, dsd = (_t(T, a) for a in (d0, su0, wu0, sd0))
+        dmd, dvd = T.zeros(F, device="cuda"), T.zeros(F, device="cuda")
+        hip.convBackwardBN(batch, C, H, H, dx, dw, F, k, s, p, dil, act, _t(T, out), dd, dsc,
+                           _t(T, xs), _t(T, xn), _t(T, m), _t(T, v), dsu, dmd, dvd, dwu, None, dsd)
+        hip.finish()
+    finally:
+        hip.setSrssQuirk(False)
+    for n, gg, r in (("delta", dd, rd), ("scale_updates", dsu, rsu), ("mean_delta", dmd, md),
+                     ("variance_delta", dvd, vd), ("weight_updates", dwu, rwu),
+                     ("state_delta", dsd, rsd)):
+        assert np.array_equal(gg.cpu().numpy(), r), n
+
+
+@pytest.mark.parametrize("idx", [0, 1, 2, 11, 62, 74])
+def test_conv_train_batchnorm_yolov3_batch8(hip, torch_cuda, ora, idx):
+    """YOLOv3 shapes at batch 8 / 416 px: the training forward with batch norm
+    (inference mode too) and the backward with batchNormBack, bit-exact."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    T = torch_cuda
+    spec = yolov3_conv_table()[idx]
+    batch, C, H, F, k, s, p, act = 8, spec.c, spec.h, spec.filters, spec.size, spec.stride, \
+        spec.pad, spec.activation
+    x = ora.uniform(batch * C * H * H, 3, idx, 0.0, 1.0).reshape(batch, C, H, H)
+    scl = float(np.sqrt(2.0 / (k * k * C)))
+    w = ora.uniform(F * C * k * k, 30 + idx, idx, -scl, scl)
+    sc, b = ora.uniform(F, 70, idx, 0.5, 1.5), ora.uniform(F, 71, idx, -0.1, 0.1)
+    rm, rv = np.zeros(F, np.float32), np.ones(F, np.float32)
+    R = [rm.copy(), rv.copy()]
+    out, m, v, xs, xn = ora.conv_forward_train(x, w, F, k, s, p, act, sc, b, R[0], R[1], 0.1, True)
+    dx, dw, dsc, db, drm, drv = (_t(T, a) for a in (x, w, sc, b, rm, rv))
+    g = {n: T.zeros(a.shape, device="cuda") for n, a in
+         (("out", out), ("m", m), ("v", v), ("xs", xs), ("xn", xn))}
+    hip.convForwardTrain(batch, C, H, H, dx, dw, F, k, s, p, 1, act, dsc, db, drm, drv, 0.1, True,
+                         g["m"], g["v"], g["xs"], g["xn"], None, g["out"])
+    hip.finish()
+    for n, r in (("out", out), ("m", m), ("v", v), ("xs", xs), ("xn", xn)):
+        assert np.array_equal(g[n].cpu().numpy(), r), n
+    assert np.array_equal(drm.cpu().numpy(), R[0]) and np.array_equal(drv.cpu().numpy(), R[1])
+    # inference mode: rolling statistics
+    inf, *_ = ora.conv_forward_train(x, w, F, k, s, p, act, sc, b, R[0].copy(), R[1].copy(), 0.1,
+                                     False)
+    gi = T.zeros(out.shape, device="cuda")
+    hip.convForwardTrain(batch, C, H, H, dx, dw, F, k, s, p, 1, act, dsc, db, drm, drv, 0.1,
+                         False, None, None, None, None, None, gi)
+    hip.finish()
+    assert np.array_equal(gi.cpu().numpy(), inf)
+    rng = np.random.default_rng(idx)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    su0 = np.zeros(F, np.float32)
+    wu0 = np.zeros(w.size, np.float32)
+    rd, rsu, rwu = d0.copy(), su0.copy(), wu0.copy()
+    md, vd = ora.conv_backward_bn(x, w, F, k, s, p, act, out, rd, sc, xs, xn, m, v, rsu, rwu)
+    dd, dsu, dwu = (_t(T, a) for a in (d0, su0, wu0))
+    dmd, dvd = T.zeros(F, device="cuda"), T.zeros(F, device="cuda")
+    hip.convBackwardBN(batch, C, H, H, dx, dw, F, k, s, p, 1, act, _t(T, out), dd, dsc, _t(T, xs),
+                       _t(T, xn), _t(T, m), _t(T, v), dsu, dmd, dvd, dwu)
+    hip.finish()
+    for n, gg, r in (("delta", dd, rd), ("scale_updates", dsu, rsu), ("mean_delta", dmd, md),
+                     ("variance_delta", dvd, vd), ("weight_updates", dwu, rwu)):
+        assert np.array_equal(gg.cpu().numpy(), r), n
+
+
+def test_conv_backward_dilation_same_padding(hip, torch_cuda, ora):
+    """Dilation 2 with k=3, p=1: the backward's padding*dilation im2col gives
+    the layer's outH columns; bit-exact incl. col2im's dilation formula."""
+    T = torch_cuda
+    rng = np.random.default_rng(21)
+    batch, C, H, F, k, s, p, d = 2, 3, 14, 5, 3, 1, 1, 2
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.3, 0.3, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, H, H)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0, wu0 = rng.uniform(-1, 1, F).astype(np.float32), rng.uniform(-1, 1, w.size).astype(np.float32)
+    sd0 = rng.uniform(-1, 1, x.shape).astype(np.float32)
+    rd, rbu, rwu, rsd = d0.copy(), bu0.copy(), wu0.copy(), sd0.copy()
+    ora.conv_backward(x, w, F, k, s, p, 9, out, rd, rbu, rwu, rsd, dil=d)
+    dd, dbu, dwu, dsd = (_t(T, a) for a in (d0, bu0, wu0, sd0))
+    hip.convBackward(batch, C, H, H, _t(T, x), _t(T, w), F, k, s, p, d, 9, _t(T, out), dd, dbu, dwu,
+                     None, dsd)
+    hip.finish()
+    for gg, r in ((dd, rd), (dbu, rbu), (dwu, rwu), (dsd, rsd)):
+        assert np.array_equal(gg.cpu().numpy(), r)
+
+
 def test_conv_backward_rejects_dilation(hip, torch_cuda):
     from tensorium_amd._abi import TnsError
     z = torch_cuda.zeros(4096, device="cuda")
