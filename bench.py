@@ -163,6 +163,129 @@ def bench_yolo(torch, hip, ctx, rank, steps, warmup=1):
     }
 
 
+def bench_yolo_dp(torch, hip, ctx, steps):
+    """Config 3 data-parallel over the ranks: the batch of 8
+    images is split by image (tensorium_amd.shard.shard_range), every rank
+    runs the 75 conv layers on its images.  The weights and biases of all 75
+    layers (247.6 MB) exist on rank 0 only and reach the others through ONE
+    RCCL broadcast of a packed buffer, outside the timed region (timed on
+    its own).  images/s = 8 / max-over-ranks time per batch."""
+    from tensorium_amd.dist import pack_flat, unpack_flat
+    from tensorium_amd.shard import shard_range
+    from tensorium_amd.yolo import yolov3_conv_table
+    specs = yolov3_conv_table()
+    batch = 8
+    lo, hi = shard_range(batch, ctx.rank, ctx.world)
+    mine = hi - lo
+    params = []
+    for s in specs:
+        sc = float(np.sqrt(2.0 / (s.size * s.size * s.c)))
+        if ctx.rank == 0:
+            params.append(synthetic(torch, (s.filters, s.K), 3 * 200000 + s.index, -sc, sc))
+            params.append(synthetic(torch, (s.filters,), 3 * 300000 + s.index, -0.1, 0.1))
+        else:
+            params.append(torch.empty((s.filters, s.K), device="cuda"))
+            params.append(torch.empty((s.filters,), device="cuda"))
+    flat, meta = pack_flat(torch, params, "cuda")
+    del params
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    ctx.broadcast(flat, src=0)
+    torch.cuda.synchronize()
+    bcast_ms = ctx.max((time.perf_counter() - t0) * 1e3)
+    views = unpack_flat(flat, meta)
+    # this rank's images: global image index -> its own synthetic plane stack
+    layers = []
+    max_ws = 0
+    for i, s in enumerate(specs):
+        x = torch.empty((max(mine, 1), s.c, s.h, s.h), device="cuda")
+        for j, g in enumerate(range(lo, hi)):
+            x[j] = synthetic(torch, (s.c, s.h, s.h), 3 * 400000 + g * 1000 + s.index, 0.0, 1.0)
+        out = torch.empty((max(mine, 1), s.filters, s.out_h, s.out_h), device="cuda")
+        layers.append((s, x, views[2 * i], views[2 * i + 1], out))
+        max_ws = max(max_ws, max(mine, 1) * s.col_elems)
+    ws = torch.empty(max(max_ws, 1), device="cuda")
+
+    def step():
+        if mine == 0:
+            return
+        for s, x, w, b, out in layers:
+            hip.convForward(mine, s.c, s.h, s.h, x, w, b, s.filters, s.size, s.stride, s.pad, 1,
+                            s.activation, ws, out, fused=True)
+
+    step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    ms = ctx.max((time.perf_counter() - t0) / steps * 1e3)
+    # every image of the batch computed exactly once across the ranks
+    covered = ctx.sum(float(mine))
+    wbytes = int(flat.numel()) * 4
+    del layers, ws, flat, views
+    torch.cuda.empty_cache()
+    return {"batch_total": batch, "images_per_rank_max": -(-batch // ctx.world),
+            "images_covered": int(covered), "ms_per_batch": round(ms, 4),
+            "images_per_s_total": round(batch / (ms / 1e3), 2),
+            "weights_bytes": wbytes, "weights_broadcast_ms": round(bcast_ms, 3),
+            "collective": "one RCCL broadcast of the packed weights (untimed in ms_per_batch)"
+                          if ctx.world > 1 else "none (one rank)",
+            "scaling": "strong (fixed batch of 8 split by image)"}
+
+
+def bench_config1(steps=20):
+    """BASELINE config 1: TSingleTensor.matMul 256x256x256 (beta = One,
+    ntensors.pas:8059-8140) through the op-table drop-in (host pointers, HIP
+    SGEMM) beside the restated CPU path (oracle sgemm_nn, host cores)."""
+    from oracle import oracle as ora
+    from tensorium_amd.ntensors import matMul
+    n = 256
+    a = ora.uniform(n * n, 1, 0).reshape(n, n)
+    b = ora.uniform(n * n, 1, 1).reshape(n, n)
+    c0 = np.zeros((n, n), np.float32)
+    c = c0.copy()
+    matMul(a, b, c)
+    ref = c0.copy()
+    ora.sgemm(False, False, n, n, n, 1.0, a, n, b, n, 1.0, ref, n)
+    same = bool(np.array_equal(c, ref))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        matMul(a, b, c)
+    hip_ms = (time.perf_counter() - t0) / steps * 1e3
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ora.sgemm(False, False, n, n, n, 1.0, a, n, b, n, 1.0, ref, n)
+    cpu_ms = (time.perf_counter() - t0) / steps * 1e3
+    flop = 2.0 * n ** 3
+    return {"workload": "TSingleTensor.matMul 256x256x256 (beta=1)", "bit_exact_vs_cpu": same,
+            "hip_op_table_ms": round(hip_ms, 4),
+            "hip_op_table_gflops": round(flop / hip_ms / 1e6, 2),
+            "cpu_port_ms": round(cpu_ms, 4), "cpu_port_gflops": round(flop / cpu_ms / 1e6, 2),
+            "cpu_threads": ora.lib().ora_get_threads(),
+            "note": "host pointers: both include nothing but the call; the HIP path moves "
+                    "768 KB over PCIe per call"}
+
+
+def host_cpus():
+    """CPUs this process may use: the cgroup CPU quota (cpu.max) when set,
+    else the affinity mask.  os.cpu_count() is the whole machine (on the GPU
+    box many times the box's share)."""
+    info = {"machine_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cgroup_quota_cpus": None}
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = max(1, int(int(q) // int(period)))
+    except Exception:
+        pass
+    info["threads_used"] = info["cgroup_quota_cpus"] or info["affinity_cpus"]
+    return info
+
+
 def bench_conv_backward(torch, hip, ctx, rank, steps=2):
     """Row f-2: TConvolutionalLayer.backward over the 75 YOLOv3-416 conv
     layers at batch 8 (tns_hip_conv_backward: derive, addSums, im2col,
@@ -272,9 +395,10 @@ def bench_batched(torch, hip, ctx, n_gemm=1024, n=1024, steps=3):
 
 def bench_host_api(n, steps=3):
     """Boundary A (host pointers, the reference's `gemm` op-table slot):
-    tns_cblas_sgemm on pageable numpy arrays, i.e. H2D of A and B, the kernel
-    and D2H of C inside each call (beta = 0 skips the C upload).  Reported as
-    the PCIe-inclusive rate beside `value`, never as `value`."""
+    tns_cblas_sgemm on pageable numpy arrays: H2D of A and B, the kernel and
+    D2H of C inside each call, pipelined by row chunks of C over a copy
+    stream (strict beta = 0 is 0*C, so C is uploaded too: 268 MB per call).
+    Reported as the PCIe-inclusive rate beside `value`, never as `value`."""
     from tensorium_amd.ntensors import bind_hip_op_table
     ops = bind_hip_op_table()
     rng = np.random.default_rng(6)
@@ -293,7 +417,9 @@ def bench_host_api(n, steps=3):
     ms = (time.perf_counter() - t0) / steps * 1e3
     return {"entry": "tns_cblas_sgemm (host pointers, pageable)", "ms_per_call": round(ms, 3),
             "gflops_pcie_inclusive": round(2.0 * n ** 3 / ms / 1e6, 1),
-            "bytes_moved_per_call": 3 * n * n * 4}
+            "bytes_moved_per_call": 4 * n * n * 4,
+            "pcie_bound_ms": round(4 * n * n * 4 / 56e9 * 1e3, 3),
+            "pcie_note": "56 GB/s per direction and total on the box (profiles/r02_pcie.json)"}
 
 
 def bench_mnist(torch, hip, ctx, steps=200):
@@ -341,8 +467,8 @@ def bench_mnist(torch, hip, ctx, steps=200):
 def cpu_baseline(n, target_s):
     """Oracle sgemm_nn (port of the reference CPU path) on a row sample."""
     from oracle import oracle as ora
-    threads = int(os.environ.get("TNS_ORACLE_THREADS") or os.environ.get("OMP_NUM_THREADS") or
-                  min(os.cpu_count() or 4, 16))
+    cpus = host_cpus()
+    threads = int(os.environ.get("TNS_ORACLE_THREADS") or cpus["threads_used"])
     ora.set_threads(threads)
     A = ora.uniform(n * n, 2, 0).reshape(n, n)
     B = ora.uniform(n * n, 2, 1).reshape(n, n)
@@ -364,7 +490,8 @@ def cpu_baseline(n, target_s):
     gflops = 2.0 * rows_t * n * n / secs / 1e9
     out = {"value": round(gflops, 3), "unit": "GFLOP/s", "cores": threads, "kind": "port",
            "sample": f"{rows_t} of {n} rows of the {n}^3 NN product "
-                     f"(restated sgemm_nn/saxpy_avx2 FMA chain, {secs:.1f} s)"}
+                     f"(restated sgemm_nn/saxpy_avx2 FMA chain, {secs:.1f} s)",
+           "host": cpus}
     out.update(cpu_yolo_mnist())
     return out
 
@@ -449,9 +576,18 @@ def main():
     conv_bwd = None
     if not args.no_yolo and args.yolo_steps > 0:
         conv_bwd = bench_conv_backward(torch, hip, ctx, rank)
+    yolo_dp = None
+    if not args.no_yolo and args.yolo_steps > 0:
+        yolo_dp = bench_yolo_dp(torch, hip, ctx, args.yolo_steps)
     batched = None if args.no_batched else bench_batched(torch, hip, ctx)
     mnist = None if args.no_mnist else bench_mnist(torch, hip, ctx)
     host_api = bench_host_api(n) if rank == 0 and world == 1 and not args.no_cpu else None
+    config1 = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            config1 = bench_config1()
+        except Exception as e:  # reported, never required
+            config1 = {"error": str(e)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -488,6 +624,8 @@ def main():
             "yolo": yolo,
             "yolo_network": yolo_net,
             "yolo_conv_backward": conv_bwd,
+            "yolo_dp": yolo_dp,
+            "config1_matmul": config1,
             "batched_gemm": batched,
             "mnist_train": mnist,
             "host_api": host_api,

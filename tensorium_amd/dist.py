@@ -1,9 +1,11 @@
 """One-process-per-GPU plumbing for the benchmark and multi-GPU runs.
 
-torch.distributed is used only for rendezvous, barriers and scalar
-reductions (timing max, checksums): the GEMM data path has no collective
-(SURVEY §8e).  Backend "nccl" is RCCL on ROCm; "gloo" is used by the CPU
-tests.
+torch.distributed carries rendezvous, barriers and scalar reductions
+(timing max, checksums) everywhere; the only data-path collective is the
+one-time broadcast of the YOLOv3 weights before the image-sharded forward
+ — the independent GEMMs of config 4 exchange nothing.
+Backend "nccl" is RCCL on ROCm (over xGMI between the GPUs of a node);
+"gloo" is used by the CPU tests.
 """
 from __future__ import annotations
 
@@ -48,6 +50,14 @@ class DistCtx:
         self.dist.all_gather(out, t)
         return [o.tolist() for o in out]
 
+    def broadcast(self, t, src: int = 0):
+        """Broadcast one tensor (on this rank's device for RCCL) from src, in
+        place.  One call per packed buffer: pack small tensors first
+        (pack_flat) so the exchange is one large collective."""
+        if self.dist is not None:
+            self.dist.broadcast(t, src=src)
+        return t
+
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()
@@ -82,3 +92,28 @@ def init(backend: str | None = None) -> DistCtx:
         kw["device_id"] = torch.device("cuda", gpu)
     dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     return DistCtx(dist, rank, world, local, device, gpu)
+
+
+def pack_flat(torch, tensors, device):
+    """One contiguous fp32 buffer holding `tensors` back to back, and the
+    (offset, shape) list to view them out of it again (unpack_flat)."""
+    total = sum(int(t.numel()) for t in tensors)
+    flat = torch.empty(total, dtype=torch.float32, device=device)
+    meta, off = [], 0
+    for t in tensors:
+        n = int(t.numel())
+        flat[off:off + n].copy_(t.reshape(-1))
+        meta.append((off, tuple(t.shape)))
+        off += n
+    return flat, meta
+
+
+def unpack_flat(flat, meta):
+    return [flat[o:o + _numel(shape)].view(*shape) for o, shape in meta]
+
+
+def _numel(shape) -> int:
+    n = 1
+    for d in shape:
+        n *= int(d)
+    return n

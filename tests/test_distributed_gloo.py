@@ -94,3 +94,66 @@ def test_shard_range_partitions():
             assert covered == list(range(n))
             sizes = [b - a for a, b in sh]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, str(ROOT))
+    try:
+        import torch
+        from oracle import oracle as ora
+        from tensorium_amd import dist as tdist
+        from tensorium_amd.shard import shard_range
+        ctx = tdist.init("gloo")
+        ora.set_threads(1)
+        batch, C, H, F, k = 8, 3, 9, 4, 3
+        # weights exist on rank 0 only; one broadcast of the packed buffer
+        if ctx.rank == 0:
+            w = torch.from_numpy(ora.uniform(F * C * k * k, 7, 0, -0.3, 0.3))
+            b = torch.from_numpy(ora.uniform(F, 7, 1, -0.1, 0.1))
+        else:
+            w, b = torch.zeros(F * C * k * k), torch.zeros(F)
+        flat, meta = tdist.pack_flat(torch, [w, b], "cpu")
+        ctx.broadcast(flat, src=0)
+        w, b = (t.numpy().copy() for t in tdist.unpack_flat(flat, meta))
+        lo, hi = shard_range(batch, ctx.rank, ctx.world)
+        sums = []
+        for g in range(lo, hi):
+            x = ora.uniform(C * H * H, 8, g, 0.0, 1.0).reshape(1, C, H, H)
+            y = ora.conv_forward(x, w, b, F, k, 1, 1, 9)
+            sums.append(float(y.astype(np.float64).sum()))
+        per = -(-batch // ctx.world)
+        gathered = ctx.gather_floats(sums + [float("nan")] * (per - len(sums)))
+        ctx.barrier()
+        ctx.close()
+        q.put((rank, gathered))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_yolo_image_sharded_with_weight_broadcast_gloo(ora, world):
+    """Config 3's data-parallel path (bench.py bench_yolo_dp): weights on rank
+    0 only reach every rank by one broadcast of the packed buffer; images
+    split by shard_range; the per-image results equal one process."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert not isinstance(r[1], str), r[1]
+    flat = [v for per_rank in res[0][1] for v in per_rank if not np.isnan(v)]
+    w = ora.uniform(4 * 27, 7, 0, -0.3, 0.3)
+    b = ora.uniform(4, 7, 1, -0.1, 0.1)
+    ref = []
+    for g in range(8):
+        x = ora.uniform(3 * 81, 8, g, 0.0, 1.0).reshape(1, 3, 9, 9)
+        ref.append(float(ora.conv_forward(x, w, b, 4, 3, 1, 1, 9).astype(np.float64).sum()))
+    assert flat == ref
