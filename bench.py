@@ -237,6 +237,69 @@ def bench_yolo_dp(torch, hip, ctx, steps):
             "scaling": "strong (fixed batch of 8 split by image)"}
 
 
+def bench_elementwise_roofline(torch, hip, reps=10):
+    """Per-kernel HBM roofline of the elementwise path at YOLOv3 batch-8
+    shapes (the ops of scripts/elementwise_traffic.py): durations live with
+    HIP events on the kernel's stream; achieved = algorithmic bytes /
+    duration against 8 TB/s; `traffic` = the counter-measured bytes per
+    launch (FETCH_SIZE / WRITE_SIZE, calibrated per access width) from the
+    committed PMC pass, profiles/*_elementwise_traffic.json."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    cands = sorted(ROOT.glob("profiles/*_elementwise_traffic.json"))
+    pmc = json.loads(cands[-1].read_text())["ops"] if cands else {}
+    s = yolov3_conv_table()[3]
+    batch = 8
+    x = torch.rand(batch * s.c * s.h * s.h, device="cuda")
+    col = torch.empty(batch * s.col_elems, device="cuda")
+    img = batch * s.c * s.h * s.h
+    out = torch.rand(batch * s.filters * s.out_h * s.out_h, device="cuda")
+    bias = torch.rand(s.filters, device="cuda")
+    no = out.numel()
+    G, N, bs = batch, 32, 416 * 416
+    ne = G * N * bs
+    y, d = torch.rand(ne, device="cuda"), torch.rand(ne, device="cuda")
+    m, v = torch.zeros(N, device="cuda"), torch.ones(N, device="cuda")
+    md, vd, dsc = (torch.zeros(N, device="cuda") for _ in range(3))
+    ops = {
+        "im2col": (lambda: hip.im2colStridedBatched(
+            s.c, s.h, s.h, s.size, s.size, s.pad, s.pad, s.stride, s.stride, 1, 1, x,
+            s.c * s.h * s.h, 0, col, s.col_elems, 0, batch), 4 * (img + batch * s.col_elems)),
+        "col2im": (lambda: hip.col2imStridedBatched(
+            s.c, s.h, s.h, s.size, s.size, s.pad, s.pad, s.stride, s.stride, 1, 1, col,
+            s.col_elems, 0, x, s.c * s.h * s.h, 0, batch), 4 * (2 * img + batch * s.col_elems)),
+        "forward_bias": (lambda: hip.forwardBias(no, out, 0, s.filters, bias, 1, batch), 8 * no),
+        "activate_leaky": (lambda: hip.ActivateArray(no, out, 0, 9), 8 * no),
+        "means_and_vars": (lambda: hip.meansAndVars(ne, N, G, y, 0, m, v), 8 * ne),
+        "means_and_vars_delta": (lambda: hip.meansAndVarsDelta(ne, N, G, d, y, 0, m, v, md, vd),
+                                 8 * ne),
+        "add_dots": (lambda: hip.addDots(ne, N, G, y, d, 0, dsc), 8 * ne),
+        "normalize_delta": (lambda: hip.normalizeDelta(ne, N, G, d, y, 0, m, v, md, vd), 12 * ne),
+    }
+    res = {}
+    for name, (fn, nbytes) in ops.items():
+        fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        p = pmc.get(name, {})
+        tr = (p.get("traffic_read_bytes") or 0) + (p.get("traffic_write_bytes") or 0) or None
+        res[name] = {"bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+                     "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4),
+                     "traffic": tr, "algorithmic_bytes": nbytes, "ms": round(ms, 4)}
+    res["_note"] = ("YOLOv3 batch 8: im2col/col2im/bias/activation on layer 3 (32x208x208 k3), "
+                    "batch-norm reductions on 8x32x173056; traffic from " +
+                    (str(cands[-1].relative_to(ROOT)) if cands else "none"))
+    del x, col, out, y, d
+    torch.cuda.empty_cache()
+    return res
+
+
 def bench_config1(steps=20):
     """BASELINE config 1: TSingleTensor.matMul 256x256x256 (beta = One,
     ntensors.pas:8059-8140) through the op-table drop-in (host pointers, HIP
@@ -576,6 +639,7 @@ def main():
     conv_bwd = None
     if not args.no_yolo and args.yolo_steps > 0:
         conv_bwd = bench_conv_backward(torch, hip, ctx, rank)
+    ew = None if args.no_yolo else bench_elementwise_roofline(torch, hip)
     yolo_dp = None
     if not args.no_yolo and args.yolo_steps > 0:
         yolo_dp = bench_yolo_dp(torch, hip, ctx, args.yolo_steps)
@@ -620,6 +684,7 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel_ms_mean": round(kern_ms, 4), "kernel_ms_min": round(kern_min, 4),
                          "algorithmic_flop_per_launch": flop},
+            "elementwise_roofline": ew,
             "cpu_baseline": cpu,
             "yolo": yolo,
             "yolo_network": yolo_net,
