@@ -439,6 +439,9 @@ enum { TNS_OP_GEMM = 0, TNS_OP_IM2COL = 1, TNS_OP_COL2IM = 2, TNS_OP_BIAS = 3,
  * these force one, for sweeps).  variant < 0 = heuristic.  Some shapes are
  * NN-with-aligned-operands only and return TNS_ERR_UNSUPPORTED otherwise. */
 int         tns_gemm_variant_count(void);
+/* VALU chain variants of the sdot-order NT product (TNS_OPT_SDOT_FORM = 1 + v) */
+int         tns_sdot_chains_variant_count(void);
+const char* tns_sdot_chains_variant_name(int32_t variant);
 const char* tns_gemm_variant_name(int32_t variant);
 int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t transB,
                          int64_t M, int64_t N, int64_t K, float ALPHA,
@@ -461,9 +464,14 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * (ntensors.pas:1493-1523, meansAndVars with blockSize % 8 == 0).
  * TNS_OPT_TT_EXACT (default 1): gemm(Trans, Trans) sums in the reference's
  * scalar s_tt order (mul, mul, add each rounded; ntensors.pas:2159-2182) on
- * the VALU, bit for bit; 0 = the fp32 MFMA kernel (faster, within 1e-4). */
+ * the VALU, bit for bit; 0 = the fp32 MFMA kernel (faster, within 1e-4).
+ * TNS_OPT_SDOT_FORM (default -1 = by shape): kernel of the sdot-order NT
+ * product (tuning / tests; same result bit for bit): 0 = the MFMA kernel
+ * (one wave per residue class), 1 + v = VALU chain kernel variant v (one
+ * lane per few residue chains, for few outputs over a long k). */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
-       TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5 };
+       TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
+       TNS_OPT_SDOT_FORM = 6 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

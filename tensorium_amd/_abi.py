@@ -30,6 +30,7 @@ TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM, TNS_OP_BIAS, TNS_OP_ACTIVATE = range(
 TNS_OPT_STRICT_BETA0 = 0
 TNS_OPT_CONV_VARIANT, TNS_OPT_CONV_PAD, TNS_OPT_NT_SDOT, TNS_OPT_SRSS_QUIRK = 1, 2, 3, 4
 TNS_OPT_TT_EXACT = 5
+TNS_OPT_SDOT_FORM = 6
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 
@@ -95,6 +96,8 @@ PROTOTYPES: dict[str, tuple] = {
                                            fptr, fptr, fptr, fptr, fptr, fptr, fptr]),
     "tns_hip_set_telemetry": (C.c_int, [vp, i32]),
     "tns_gemm_variant_count": (C.c_int, []),
+    "tns_sdot_chains_variant_count": (C.c_int, []),
+    "tns_sdot_chains_variant_name": (C.c_char_p, [C.c_int32]),
     "tns_gemm_variant_name": (C.c_char_p, [i32]),
     "tns_hip_gemm_variant": (C.c_int, [vp, i32, u8, u8, i64, i64, i64, f32, fptr, i64, i64, i64,
                                        fptr, i64, i64, i64, f32, fptr, i64, i64, i64, i64]),

@@ -204,9 +204,23 @@ bool k_vec4(const float* p, int64_t ld, int64_t stride, int64_t batch, int64_t K
 
 }  // namespace
 
-// 32x64 tiles when they still give >= 4 blocks per CU, else 32x32
+static int g_sdot_form = -1;
+void set_sdot_form(int form) { g_sdot_form = form < 0 ? -1 : form; }
+
+// MFMA: 32x64 tiles when they still give >= 4 blocks per CU, else 32x32;
+// few outputs over a long k go to the VALU chain kernel
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.batch <= 0) return hipSuccess;
+  if (g_sdot_form > 0) return launch_sdot_chains(a, g_sdot_form - 1, s);
+  // few outputs over a long k (conv dW of the 416/208/104-pixel YOLOv3
+  // layers): the VALU chain kernel, tile by output count (scripts/
+  // sdot_forms.py, profiles/r02_sdot_forms.json: YOLOv3 layer 0 dW at batch
+  // 8 1.44 -> 0.28 ms, layer 2 0.35 -> 0.10 ms, layer 5 0.089 -> 0.056 ms)
+  const int64_t t32 = ((a.M + 31) / 32) * ((a.N + 31) / 32) * a.batch;
+  if (g_sdot_form < 0 && a.K >= 4096 && t32 <= 64) {
+    const int64_t outs = a.M * a.N * a.batch;
+    return launch_sdot_chains(a, outs <= 8192 ? 1 : (outs <= 32768 ? 2 : 4), s);
+  }
   const bool v = k_vec4(a.A, a.lda, a.strideA, a.batch, a.K) &&
                  k_vec4(a.B, a.ldb, a.strideB, a.batch, a.K);
   const int64_t b64 = ((a.M + 31) / 32) * ((a.N + 63) / 64) * a.batch;

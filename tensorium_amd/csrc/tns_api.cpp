@@ -508,6 +508,11 @@ int tns_set_option(int32_t opt, int64_t value) {
     case TNS_OPT_TT_EXACT:
       g_tt_exact = value ? 1 : 0;
       return TNS_OK;
+    case TNS_OPT_SDOT_FORM:
+      if (value > sdot_chains_variant_count())
+        return set_error(TNS_ERR_ARG, "sdot form %lld out of range", (long long)value);
+      set_sdot_form((int)value);
+      return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
   }
@@ -1458,6 +1463,8 @@ int tns_hip_conv_backward_bn(tns_ctx* c, int64_t batch, int64_t C, int64_t H, in
 }
 
 int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
+int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
+const char* tns_sdot_chains_variant_name(int32_t v) { return sdot_chains_variant_name(v); }
 const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }
 
 int tns_hip_gemm_variant(tns_ctx* c, int32_t variant, uint8_t transA, uint8_t transB, int64_t M,

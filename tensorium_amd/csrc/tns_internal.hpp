@@ -79,6 +79,13 @@ hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t
 // gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
 // plain epilogue only
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
+// the same product on the VALU, one lane per few residue chains
+// (sgemm_sdot_chains.hip): for few outputs over a long k
+hipError_t launch_sdot_chains(const GemmArgs& a, int variant, hipStream_t s);
+int sdot_chains_variant_count();
+const char* sdot_chains_variant_name(int v);
+// TNS_OPT_SDOT_FORM: -1 heuristic, 0 the MFMA kernel, 1 + v chains variant v
+void set_sdot_form(int form);
 // gemm(Trans, Trans) in the reference's scalar s_tt order (sgemm_tt.hip);
 // plain epilogue only
 hipError_t launch_sgemm_tt(const GemmArgs& a, hipStream_t s);

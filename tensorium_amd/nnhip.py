@@ -294,6 +294,14 @@ class TNNHip:
         one ascending-k chain per element; process-wide."""
         check(self.lib.tns_set_option(3, 1 if on else 0))
 
+    def setSdotForm(self, form: int = -1):
+        """Kernel of the sdot-order NT product: -1 by shape, 0 the MFMA
+        kernel, 1 + v VALU chain variant v (bit-identical); process-wide."""
+        check(self.lib.tns_set_option(6, int(form)))
+
+    def sdotChainsVariants(self) -> int:
+        return int(self.lib.tns_sdot_chains_variant_count())
+
     def setTtExact(self, on: bool = True):
         """gemm(Trans, Trans) in the reference's scalar s_tt order on the VALU
         (default) or on the fp32 MFMA kernel; process-wide."""

@@ -130,6 +130,54 @@ def test_nt_sdot_batched_offsets_and_plain_order(hip, torch_cuda, ora):
     assert np.all(np.abs(got.astype(np.float64) - ref) <= TOL * bnd + 1e-30)
 
 
+CHAIN_SHAPES = [(1, 1, 1), (3, 5, 9), (33, 65, 15), (37, 53, 61), (32, 27, 2704), (17, 40, 1029),
+                (64, 288, 4100), (70, 90, 2304), (5, 7, 0)]
+
+
+@pytest.mark.parametrize("M,N,K", CHAIN_SHAPES)
+def test_nt_sdot_every_form_bit_exact(hip, torch_cuda, ora, M, N, K):
+    """Every kernel of the sdot-order NT product (TNS_OPT_SDOT_FORM: the MFMA
+    kernel and each VALU chain variant, sgemm_sdot_chains.hip) gives the
+    reference's s_nt/sdot_avx2 result bit for bit: K mod 8 tails, K not a
+    multiple of 4 (scalar staging), ragged tiles, every beta mode."""
+    rng = np.random.default_rng(M * 5 + N * 7 + K + 1)
+    A, B, C0 = operands(rng, 0, 1, M, N, K)
+    refs = {ab: run_ref(ora, 0, 1, A, B, C0, *ab) for ab in [(1.0, 0.0), (0.5, 2.0), (1.0, 1.0)]}
+    try:
+        for form in range(hip.sdotChainsVariants() + 1):
+            hip.setSdotForm(form)
+            for (alpha, beta), ref in refs.items():
+                got = run_dev(hip, torch_cuda, 0, 1, A, B, C0, alpha, beta)
+                assert np.array_equal(got, ref), (form, M, N, K, alpha, beta,
+                                                  float(np.abs(got - ref).max()))
+    finally:
+        hip.setSdotForm(-1)
+
+
+def test_nt_sdot_chains_batched_offsets(hip, torch_cuda, ora):
+    """Strided-batched NT with offsets / padded leading dims on every chain
+    variant (the conv dW call shape: batch of images, BETA via the driver)."""
+    rng = np.random.default_rng(21)
+    batch, M, N, K, lda, ldb, off = 3, 45, 70, 1037, 1041, 1039, 5
+    A = rng.uniform(-1, 1, off + batch * M * lda).astype(np.float32)
+    B = rng.uniform(-1, 1, off + batch * N * ldb).astype(np.float32)
+    C = rng.uniform(-1, 1, off + batch * M * N).astype(np.float32)
+    ref = C.copy()
+    ora.sgemm_batch_strided(False, True, M, N, K, 0.5, A[off:], lda, M * lda, B[off:], ldb,
+                            N * ldb, 1.0, ref[off:], N, M * N, batch)
+    dA, dB = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B))
+    try:
+        for form in range(1, hip.sdotChainsVariants() + 1):
+            hip.setSdotForm(form)
+            dC = torch_cuda.from_numpy(C.copy()).cuda()
+            hip.gemmStridedBatched(False, True, M, N, K, 0.5, dA, off, lda, M * lda, dB, off, ldb,
+                                   N * ldb, 1.0, dC, off, N, M * N, batch)
+            hip.finish()
+            assert np.array_equal(dC.cpu().numpy(), ref), form
+    finally:
+        hip.setSdotForm(-1)
+
+
 @pytest.mark.parametrize("M,N,K", SHAPES + [(2945, 2945, 37)])
 def test_tt_bit_exact(hip, torch_cuda, ora, M, N, K):
     """gemm(Trans, Trans) = s_tt (ntensors.pas:2159-2182): both tile sizes
