@@ -678,7 +678,7 @@ def main():
                        "alpha": 1.0, "beta": 0.0, "gemms_per_gpu_per_step": 1,
                        "parallelism": f"{world} independent replicas, one process per GPU, "
                                       "no data-path collective"},
-            "roofline": {"bound": "mfma", "kernel": "sgemm_mfma_kernel<NN>",
+            "roofline": {"bound": "mfma", "kernel": "sgemm_nn_big_kernel<256x256x32, 8 waves>",
                          "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,

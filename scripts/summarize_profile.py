@@ -45,7 +45,8 @@ def main():
 
     # the dominant kernel: the 4096^3 launches (grid of 256 blocks x 512 thr)
     def is_main(name):
-        return "sgemm_mfma_kernel" in name and "Shape<256, 256, 32, 2, 4" in name
+        return ("sgemm_nn_big_kernel" in name and "Geo<256, 256, 2, 4" in name) or \
+            ("sgemm_mfma_kernel" in name and "Shape<256, 256, 32, 2, 4" in name)
 
     # kernel duration from the trace (same command, not profiled with PMC)
     durs = []

@@ -99,8 +99,12 @@ hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s) {
   return launch_sgemm_conv_variant(-1, a, s);
 }
 
-int sgemm_variant_count() { return kNumVariants; }
-const char* sgemm_variant_name(int v) { return (v >= 0 && v < kNumVariants) ? kVariants[v].name : ""; }
+// the last variant indices are the dedicated large-NN kernels (sgemm_nn_big.hip)
+int sgemm_variant_count() { return kNumVariants + sgemm_nn_big_count(); }
+const char* sgemm_variant_name(int v) {
+  if (v >= kNumVariants) return sgemm_nn_big_name(v - kNumVariants);
+  return (v >= 0 && v < kNumVariants) ? kVariants[v].name : "";
+}
 
 hipError_t launch_sgemm_variant(int variant, const GemmArgs& a_in, bool transA, bool transB,
                                 hipStream_t s) {
@@ -110,6 +114,14 @@ hipError_t launch_sgemm_variant(int variant, const GemmArgs& a_in, bool transA, 
   // A is k-contiguous unless transposed; B is n-contiguous unless transposed
   const bool av = vec4_ok(a.A, a.lda, a.strideA, a.batch, transA ? a.M : a.K);
   const bool bv = vec4_ok(a.B, a.ldb, a.strideB, a.batch, transB ? a.K : a.N);
+  if (variant >= kNumVariants) {
+    if (transA || transB) return hipErrorInvalidValue;
+    return launch_sgemm_nn_big(variant - kNumVariants, a, s);
+  }
+  if (variant < 0 && !transA && !transB) {
+    const int nb = sgemm_nn_big_pick(a);
+    if (nb >= 0) return launch_sgemm_nn_big(nb, a, s);
+  }
   const int v = variant < 0 ? pick_variant(a, av, bv) : variant;
   if (v >= kNumVariants) return hipErrorInvalidValue;
   return kVariants[v].fn(a, transA, transB, av, bv, s);

@@ -76,6 +76,12 @@ struct GemmArgs {
 };
 
 hipError_t launch_sgemm(const GemmArgs& a, bool transA, bool transB, hipStream_t s);
+// large aligned NN (M, N multiples of the tile, K of 32; sgemm_nn_big.hip):
+// form v of sgemm_nn_big_count(); pick = -1 when none applies by heuristic
+int sgemm_nn_big_count();
+const char* sgemm_nn_big_name(int v);
+int sgemm_nn_big_pick(const GemmArgs& a);
+hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s);
 // gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
 // plain epilogue only
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);

@@ -344,3 +344,43 @@ def test_every_tile_variant_bit_exact(hip, torch_cuda, ora):
                 hip.finish()
                 ref = run_ref(ora, ta, 0, A, B, C0, 0.5, 2.0)
                 assert np.array_equal(dC.cpu().numpy(), ref), (name, M, N, K, ta)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 256, 32), (512, 768, 96), (256, 512, 2080)])
+def test_nn_big_kernel_bit_exact(hip, torch_cuda, ora, M, N, K):
+    """The dedicated large-NN kernel (sgemm_nn_big.hip: LDS-DMA B, permuted /
+    swizzled transposed A), forced at small multiples of its 256x256x32 tile:
+    every beta mode and alpha != 1 (the A_PART pre-multiply), bit-exact."""
+    forms = [v for v, n in enumerate(hip.gemmVariants()) if n.endswith("nn_big")]
+    assert len(forms) == 3
+    rng = np.random.default_rng(M + N + K)
+    A, B, C0 = operands(rng, 0, 0, M, N, K)
+    C0[0, 0] = np.nan  # strict beta = 0 keeps 0*NaN (ntensors.pas:2259)
+    for alpha, beta in [(1.0, 0.0), (0.5, 2.0), (1.0, 1.0), (-1.5, 0.25)]:
+        ref = run_ref(ora, 0, 0, A, B, C0, alpha, beta)
+        for v in forms:
+            dA, dB, dC = (torch_cuda.from_numpy(x).cuda() for x in (A, B, C0.copy()))
+            hip.gemmVariant(v, False, False, M, N, K, alpha, dA, 0, K, 0, dB, 0, N, 0, beta, dC,
+                            0, N, 0, 1)
+            hip.finish()
+            got = dC.cpu().numpy()
+            assert np.array_equal(got, ref, equal_nan=True), (v, alpha, beta)
+
+
+def test_nn_big_kernel_batched(hip, torch_cuda, ora):
+    """Strided-batched through the large-NN kernels (blockIdx.y = batch)."""
+    forms = [v for v, n in enumerate(hip.gemmVariants()) if n.endswith("nn_big")]
+    rng = np.random.default_rng(5)
+    batch, M, N, K = 3, 256, 256, 64
+    A = rng.uniform(-1, 1, (batch, M, K)).astype(np.float32)
+    B = rng.uniform(-1, 1, (batch, K, N)).astype(np.float32)
+    C = rng.uniform(-1, 1, (batch, M, N)).astype(np.float32)
+    ref = C.copy()
+    ora.sgemm_batch_strided(False, False, M, N, K, 1.0, A.reshape(-1), K, M * K, B.reshape(-1), N,
+                            K * N, 1.0, ref.reshape(-1), N, M * N, batch)
+    for v in forms:
+        dA, dB, dC = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B, C))
+        hip.gemmVariant(v, False, False, M, N, K, 1.0, dA, 0, K, M * K, dB, 0, N, K * N, 1.0, dC,
+                        0, N, M * N, batch)
+        hip.finish()
+        assert np.array_equal(dC.cpu().numpy(), ref), v
