@@ -67,7 +67,7 @@ def main():
     flop = 2.0 * size ** 3
     alg = 3 * size * size * 4
     out = {
-        "tag": tag, "size": size, "kernel": "sgemm_mfma_kernel<Shape<256,256,32,2,4,2>, NN, 4, 4>",
+        "tag": tag, "size": size, "kernel": "sgemm_nn_big_kernel<Geo<256,256,2,4,1>> (NN, 256x256x32, 8 waves)",
         "launches_traced": len(durs),
         "kernel_ms_mean": round(st.mean(durs), 4), "kernel_ms_min": round(min(durs), 4),
         # bench.py's timed launches are the last --steps of the warm-up+steps
