@@ -439,6 +439,9 @@ enum { TNS_OP_GEMM = 0, TNS_OP_IM2COL = 1, TNS_OP_COL2IM = 2, TNS_OP_BIAS = 3,
  * these force one, for sweeps).  variant < 0 = heuristic.  Some shapes are
  * NN-with-aligned-operands only and return TNS_ERR_UNSUPPORTED otherwise. */
 int         tns_gemm_variant_count(void);
+/* plane-sized implicit-conv tiles (TNS_OPT_CONV_VARIANT = 100 + v) */
+int         tns_conv_tile_variant_count(void);
+const char* tns_conv_tile_variant_name(int32_t variant);
 /* VALU chain variants of the sdot-order NT product (TNS_OPT_SDOT_FORM = 1 + v) */
 int         tns_sdot_chains_variant_count(void);
 const char* tns_sdot_chains_variant_name(int32_t variant);
@@ -453,7 +456,8 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
 /* TNS_OPT_STRICT_BETA0 (default 1): beta==0 computes 0*C like the reference
  * (NaN/Inf in C propagate).  0 = BLAS convention (C not read).
  * TNS_OPT_CONV_VARIANT (default -1 = heuristic): forces the tile shape of the
- * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name).
+ * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name, or
+ * 100 + v for plane-sized tile v of tns_conv_tile_variant_name).
  * TNS_OPT_CONV_PAD (default -1 = by cost): 1 gathers from a zero-padded copy
  * of the images, 0 bounds-checks the window inside the GEMM.
  * TNS_OPT_NT_SDOT (default 1): gemm(NoTrans, Trans) sums in the reference's

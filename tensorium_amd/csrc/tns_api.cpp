@@ -1164,6 +1164,53 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
     // implicit GEMM: batch folded into N, B gathered from zero-padded images
     if (!input || !weights || !out || (bias_act && !biases))
       return set_error(TNS_ERR_ARG, "conv_forward: null operand");
+    // plane-sized tiles with a bounds-checked gather from the unpadded
+    // images (conv_tile.hip) where they apply; TNS_OPT_CONV_VARIANT >= 100
+    // forces tile 100 + v, 0..99 the sgemm_kernel.hpp shapes
+    {
+      int tv = -1;
+      const int64_t img0 = C * H * W;
+      if ((kSize == 1 || kSize == 3) && k % 32 == 0 && img0 * 4 <= 0x7fffffffLL &&
+          (g_conv_variant < 0 || g_conv_variant >= 100)) {
+        GemmArgs probe{};
+        probe.M = filters; probe.N = batch * outImg; probe.K = k;
+        probe.conv_sY = (int)stride;
+        probe.A = weights; probe.lda = k;
+        tv = g_conv_variant >= 100 ? (int)(g_conv_variant - 100) : conv_tile_pick(probe, (int)kSize);
+      }
+      if (tv >= 0) {
+        const int64_t chunk = std::max<int64_t>(
+            1, std::min<int64_t>(0x7fffffffLL / (4 * img0),
+                                 0x7fffffffLL / std::max<int64_t>(outImg, 1)));
+        for (int64_t b0 = 0; b0 < batch; b0 += chunk) {
+          const int64_t nb = std::min(chunk, batch - b0);
+          GemmArgs a{};
+          a.M = filters; a.N = nb * outImg; a.K = k;
+          a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_ZERO;
+          a.A = weights; a.lda = k; a.strideA = 0;
+          a.B = input + b0 * img0; a.ldb = outImg; a.strideB = img0;
+          a.C = out + b0 * outImg * filters; a.ldc = outImg; a.strideC = outImg * filters;
+          a.batch = 1; a.epi = bias_act ? EPI_BIAS_ACT : EPI_NONE; a.bias = biases;
+          a.act = act_transcendental(activation) ? 4 : activation;
+          a.conv = 2;
+          a.conv_H = (int)H; a.conv_W = (int)W; a.conv_ow = (int)ow; a.conv_ohw = (int)outImg;
+          a.conv_sY = (int)stride; a.conv_sX = (int)stride;
+          a.conv_pH = (int)padding; a.conv_pW = (int)padding;
+          a.conv_bytes = (int)(4 * nb * img0);
+          OpTimer t(c, TNS_OP_GEMM);
+          hipError_t e = launch_conv_tile(tv, a, (int)kSize, (int)dilation, c->stream);
+          if (e == hipErrorInvalidValue)
+            return set_error(TNS_ERR_UNSUPPORTED, "conv tile %d does not fit this layer", tv);
+          if (int r = hip_status(e, "conv tile launch")) return r;
+        }
+        if (bias_act && act_transcendental(activation)) {
+          OpTimer t(c, TNS_OP_ACTIVATE);
+          return hip_status(launch_activate(out, batch * filters * outImg, activation, c->stream),
+                            "activate launch");
+        }
+        return TNS_OK;
+      }
+    }
     // Materialise the zero border (padded images, no bounds checks in the
     // GEMM) when that copy costs under ~5% of the GEMM: copy time
     // ~bytes/4 TB/s vs GEMM ~flops/80 TF/s.
@@ -1209,7 +1256,9 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
       a.conv_pH = padded ? 0 : (int)padding; a.conv_pW = a.conv_pH;
       a.conv_bytes = (int)(4 * nb * img);
       OpTimer t(c, TNS_OP_GEMM);
-      hipError_t e = launch_sgemm_conv_variant((int)g_conv_variant, a, c->stream);
+      // (99: the sgemm_kernel.hpp shape heuristic, bypassing conv_tile)
+      hipError_t e = launch_sgemm_conv_variant(g_conv_variant == 99 ? -1 : (int)g_conv_variant,
+                                               a, c->stream);
       if (e == hipErrorInvalidValue)
         return set_error(TNS_ERR_UNSUPPORTED, "conv variant %lld unsupported",
                          (long long)g_conv_variant);
@@ -1464,6 +1513,8 @@ int tns_hip_conv_backward_bn(tns_ctx* c, int64_t batch, int64_t C, int64_t H, in
 
 int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
+int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
+const char* tns_conv_tile_variant_name(int32_t v) { return conv_tile_name(v); }
 const char* tns_sdot_chains_variant_name(int32_t v) { return sdot_chains_variant_name(v); }
 const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }
 

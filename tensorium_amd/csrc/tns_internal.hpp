@@ -101,6 +101,13 @@ hipError_t launch_add_in_order(float* C, const float* part, int64_t n, int64_t b
 // implicit-GEMM convolution: NN, B generated from the image (a.conv must be set)
 hipError_t launch_sgemm_conv(const GemmArgs& a, hipStream_t s);
 hipError_t launch_sgemm_conv_variant(int variant, const GemmArgs& a, hipStream_t s);
+// implicit-GEMM convolution on plane-sized tiles (conv_tile.hip): unpadded
+// images (a.conv == 2 fields, a.conv_pH/pW = padding), kernel size ks 1 or
+// 3, K % 32 == 0, M % tile rows == 0; variant v of conv_tile_count()
+int conv_tile_count();
+const char* conv_tile_name(int v);
+int conv_tile_pick(const GemmArgs& a, int ks);
+hipError_t launch_conv_tile(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
 // k-table of an implicit-GEMM convolution over stored Hs x Ws images (padded
 // or not): K = C*kH*kW entries plus KTAB_PAD sentinels
 constexpr int KTAB_PAD = 256;

@@ -299,6 +299,10 @@ class TNNHip:
         kernel, 1 + v VALU chain variant v (bit-identical); process-wide."""
         check(self.lib.tns_set_option(6, int(form)))
 
+    def convTileVariants(self) -> int:
+        """Plane-sized implicit-conv tiles (setConvVariant(100 + v))."""
+        return int(self.lib.tns_conv_tile_variant_count())
+
     def sdotChainsVariants(self) -> int:
         return int(self.lib.tns_sdot_chains_variant_count())
 

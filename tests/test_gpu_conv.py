@@ -314,3 +314,35 @@ def test_conv_backward_rejects_dilation(hip, torch_cuda):
     z = torch_cuda.zeros(4096, device="cuda")
     with pytest.raises(TnsError):
         hip.convBackward(1, 1, 9, 9, z, z, 1, 3, 1, 2, 2, 9, z, z, z, z, None, None)
+
+
+TILE_CASES = [
+    (2, 32, 17, 128, 3, 1, 1, 9, 1), (3, 32, 12, 64, 3, 2, 1, 9, 1), (2, 64, 9, 32, 1, 1, 0, 4, 1),
+    (1, 96, 26, 128, 3, 2, 1, 1, 1), (2, 32, 13, 256, 3, 1, 1, 0, 1), (2, 32, 21, 64, 3, 1, 2, 9, 2),
+    (1, 32, 40, 32, 3, 1, 1, 9, 1)]
+
+
+def test_conv_tile_variants_bit_exact(hip, torch_cuda, ora):
+    """Every plane-sized conv tile (conv_tile.hip, TNS_OPT_CONV_VARIANT =
+    100 + v): bounds-checked gather from unpadded images, 1x1 and 3x3,
+    strides 1/2, dilation 2, ragged N, fused bias + leaky/linear/relu and the
+    separate logistic pass; tiles whose rows do not divide the filter count
+    report UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    ntiles = hip.convTileVariants()
+    assert ntiles >= 4
+    ran = 0
+    try:
+        for v in range(ntiles):
+            hip.setConvVariant(100 + v)
+            for i, (batch, C, H, F, k, s, p, act, d) in enumerate(TILE_CASES):
+                try:
+                    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, 3,
+                                         seed=i, dil=d)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, batch, C, H, F, k, s, p, act, d)
+    finally:
+        hip.setConvVariant(-1)
+    assert ran >= 2 * ntiles
