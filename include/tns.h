@@ -324,7 +324,7 @@ int tns_hip_sum(tns_ctx* ctx, int64_t N, const float* src, int64_t offset, float
  * the packed parameters and state (layout: oracle/tns_oracle.h
  * ora_mlp_train_step), sized tns_mlp_buffer_floats().  *cost (device) gets
  * the softmax layer's loss.Sum().  Limits: nlayers <= 32,
- * 8*batch*max(widths[1..]) <= 40960. */
+ * 9*batch*max(widths[1..]) <= 40960 (one CU's LDS). */
 int64_t tns_mlp_buffer_floats(int32_t nlayers, const int64_t* widths, int32_t bn, int64_t batch);
 int tns_hip_mlp_train_step(tns_ctx* ctx, int32_t nlayers, const int64_t* widths,
                            const int32_t* acts, int32_t bn, int64_t batch, const float* X,

@@ -29,22 +29,36 @@ cost = torch.zeros(1, device="cuda")
 for _ in range(20):
     hip.mlpTrainStep(widths, acts, True, B, X, T, 1e-3, 0.9, 1e-4, buf, cost)
 torch.cuda.synchronize()
-st = buf[n:n + 128].cpu().numpy().view(np.uint32).astype(np.uint64)
+st = buf[n:n + 256].cpu().numpy().view(np.uint32).astype(np.uint64)
 t = st[0::2] | (st[1::2] << 32)
 names = {0: "start"}
 names.update({1 + l: f"fwd{l}" for l in range(6)})
 names[20] = "softmax"
 names.update({21 + l: f"bwd{l}" for l in range(6)})
-names.update({40 + l: f"upd{l}" for l in range(6)})
+names[40] = "update"
 names.update({50 + 2 * l: f"bwd{l}.stage" for l in range(6)})
 names.update({51 + 2 * l: f"bwd{l}.chan" for l in range(6)})
 order = [0] + [1 + l for l in range(6)] + [20]
 for l in reversed(range(6)):
     order += [50 + 2 * l, 51 + 2 * l, 21 + l]  # stage, column pass, gemms
-order += [40 + l for l in range(6)]
+order += [40]
 prev = None
 for i in order:
     if prev is not None:
         print(f"{names[i]:8s} {int(t[i]) - int(t[prev]):8d} cycles")
     prev = i
 print(f"total    {int(t[order[-1]]) - int(t[0]):8d} cycles (s_memtime ticks)")
+
+m = t[64:128]
+def mk(i): return int(m[i])
+fw = ["prefetch issued", "gemm done", "after barrier", "fold done", "after barrier",
+      "chains done", "after barrier", "element pass done", "after barrier"]
+print("forward layer 1 (wave 0 marks, cycles since the previous mark):")
+for i in range(1, 9):
+    print(f"  {fw[i]:20s} {mk(i) - mk(i - 1):8d}")
+bw = {11: "B1 done", 12: "after barrier", 13: "chains done", 14: "after barrier",
+      15: "normalizeDelta done", 16: "after barrier", 17: "dW task done",
+      18: "(dX) loop done", 19: "after barrier"}
+print("backward stage 2:")
+for i in range(11, 20):
+    print(f"  {bw[i]:20s} {mk(i) - mk(i - 1):8d}")

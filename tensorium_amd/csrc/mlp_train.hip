@@ -4,9 +4,14 @@
 // followed by TSoftmaxLayer (nsoftmaxlayer.pas:139-181), nnet.pas:275-450.
 //
 // The whole step is ~9 MFLOP at batch 32, far too small to fill 256 CUs and
-// dominated by ~60 dependent stages; as separate launches it is launch-bound.
+// dominated by dependent stages; as separate launches it is launch-bound.
 // Here one 1024-thread workgroup runs every stage back to back with
-// workgroup barriers in between (all traffic stays in one CU's L1/L2 slice).
+// workgroup barriers in between (all traffic stays in one CU's L1/L2 slice),
+// laid out for latency: the per-channel sequential sums are the only
+// single-thread chains (the element-wise parts of BN, softmax and the update
+// run on all 1024 threads), every stage issues its loads together, operands
+// the next stage needs stay in LDS or registers, and the weight update of
+// layer 0 is applied in its dW epilogue.
 //
 // Numerics mirror oracle/tns_oracle_train.c:
 //  * forward gemm(NoTrans, Trans) = the reference's sdot_avx2 8-lane order:
@@ -14,7 +19,8 @@
 //    8 partial tiles are folded (l, l+4) then ((0+1)+(2+3)) — bit-exact;
 //  * dW (TN) and dX (NN, beta = 1) are ascending-k FMA chains = f32 MFMA;
 //  * per-channel BN / bias sums walk the reference's sequential order in one
-//    thread; exp / ln / pow in double, rounded once.
+//    thread; exp / ln / pow in double, rounded once;
+//  * the cost is vssum_avx2's 8 lane chains (one lane each) and its fold.
 #include "tns_act.hpp"
 #include "tns_internal.hpp"
 
@@ -40,12 +46,48 @@ constexpr int KC = 128;  // largest k-chunk of the LDS-staged forward gemm
       st_[1] = (unsigned)(t_ >> 32);                                              \
     }                                                                             \
   } while (0)
+// MLP_MARK: thread 0's clock without a barrier (wave 0's own timeline)
+#define MLP_MARK(i)                                                               \
+  do {                                                                            \
+    if (threadIdx.x == 0) {                                                       \
+      const unsigned long long t_ = __builtin_amdgcn_s_memtime();                 \
+      unsigned* st_ = reinterpret_cast<unsigned*>(a.buf + a.stamp_off) + 2 * (64 + (i)); \
+      st_[0] = (unsigned)t_;                                                      \
+      st_[1] = (unsigned)(t_ >> 32);                                              \
+    }                                                                             \
+  } while (0)
 #else
 #define MLP_STAMP(i) \
   do {               \
   } while (0)
+#define MLP_MARK(i) \
+  do {              \
+  } while (0)
 #endif
 __device__ constexpr float SEPS = 0.000001f;
+
+// Workgroup barrier for LDS traffic only: waits for this wave's LDS
+// operations, not for its global loads (prefetches stay in flight across it)
+// or stores (nothing after it reads them from memory).  __syncthreads()
+// drains every memory counter, so it is kept only where another thread reads
+// global data written before it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Column blocks for the per-channel sequential sums: 8 LDS reads of rows
+// b0..b0+7 (clamped to the last row; the caller skips the extra terms),
+// issued back to back and held by one empty asm, so a chain waits once per
+// block instead of once per term (hipcc otherwise placed each read right
+// before the add that consumes it, with an lgkmcnt(0) wait each time).
+__device__ __forceinline__ void col8(float (&v)[8], const float* col, int b0, int B, int stride) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) v[u] = col[(b0 + u < B ? b0 + u : B - 1) * stride];
+}
+__device__ __forceinline__ void hold8(float (&v)[8]) {
+  asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
+               "+v"(v[6]), "+v"(v[7]));
+}
 
 // Per-layer views into the packed buffer.  The element offsets are computed
 // on the host (MlpArgs::off) and read from the kernel arguments on each use,
@@ -105,33 +147,38 @@ __device__ __forceinline__ void mfma_chain(floatx16& acc, int steps, const float
 }
 
 // element (row, col) held by accumulator register e of this lane
-__device__ __forceinline__ int acc_row(int e) {
-  return (e & 3) + 8 * (e >> 2) + 4 * ((threadIdx.x & 63) >> 5);
+__device__ __forceinline__ int acc_row(int e, int lane) {
+  return (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
 }
 
-__device__ __forceinline__ float vssum8(const float* a, int64_t n) {
-  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const int64_t blocks = n >> 3;
-  for (int64_t t = 0; t < blocks; ++t)
-    for (int l = 0; l < 8; ++l) acc[l] = acc[l] + a[8 * t + l];
-  const float s0 = acc[0] + acc[4], s1 = acc[1] + acc[5], s2 = acc[2] + acc[6],
-              s3 = acc[3] + acc[7];
-  float r = (s0 + s1) + (s2 + s3);
-  for (int64_t i = blocks * 8; i < n; ++i) r = r + a[i];
-  return r;
+// threadIdx.x behind an empty asm: values derived from it are recomputed in
+// each stage instead of being hoisted out of the layer loops as invariants
+// (at 1024 threads a thread has 128 VGPRs, and the hoisted addresses of
+// every stage spilled to scratch)
+__device__ __forceinline__ int stage_tid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
 }
+
+// Element slots per thread in the [B][O] passes (kernel template argument):
+// 2 when B*max(O) <= 2048 (the MNIST net), else 5 (B*O <= 40960/8).
 
 // Forward gemm of one layer, out[B][O] partials per residue class r = k mod 8
 // into lds[(r*B + m)*O + n], with wave w = (tile, r) and both operands staged
 // through LDS in k-chunks of KCH by coalesced loads; each chain continues
-// across chunks in ascending k (bit-identical to the direct chain).  The
-// chunks alias the partial-sum region: every wave has passed the barrier
-// after the last chunk before any partial is written.
+// across chunks in ascending k (bit-identical to the direct chain).  With
+// 16-byte rows the chunks are loaded as float4, two chunks ahead into
+// registers, so a chunk's global latency overlaps the MFMAs of the previous
+// two.  The chunks alias the partial-sum region: every wave has passed the
+// barrier after the last chunk before any partial is written.
 template <int KCH>
 __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const float* W, int64_t B,
-                                             int64_t O, int64_t I, int tm, int tn) {
+                                             int64_t O, int64_t I, int tm, int tn, int tid) {
   constexpr int KP = KCH + 1;  // LDS row: an odd stride for the lanes' row reads
-  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+  constexpr int QR = KCH / 4;  // float4 units per staged row
+  constexpr int UV = (3 * 32 * QR + NT - 1) / NT;  // units per thread (tm + tn <= 3)
+  const int wid = tid >> 6, lane = tid & 63;
   float* Xs = lds;
   float* Ws = Xs + tm * 32 * KP;
   const int rowsX = tm * 32, rows = (tm + tn) * 32;
@@ -141,19 +188,7 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
   const int l31 = lane & 31, h = lane >> 5;
   floatx16 acc;
   for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-  for (int64_t kc0 = 0; kc0 < I; kc0 += KCH) {
-#pragma unroll 4
-    for (int i = tid; i < rows * KCH; i += NT) {
-      const int row = i / KCH, kk = i % KCH;
-      const int64_t k = kc0 + kk;
-      const bool isx = row < rowsX;
-      const int64_t rr = isx ? row : row - rowsX;
-      const bool ok = k < I && rr < (isx ? B : O);
-      const float* src = isx ? in : W;
-      const float v = src[ok ? rr * I + k : 0];
-      lds[row * KP + kk] = ok ? v : 0.0f;
-    }
-    __syncthreads();
+  auto compute = [&]() {
     if (active) {
 #pragma unroll
       for (int st = 0; st < KCH / 16; ++st) {  // k = kc0 + r + 8*(2*st + h)
@@ -162,38 +197,237 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
                                                    Ws[(n0 + l31) * KP + kk], acc, 0, 0, 0);
       }
     }
-    __syncthreads();
+  };
+  const bool vec = (I & 3) == 0 && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
+  const int64_t nch = (I + KCH - 1) / KCH;
+  if (vec) {
+    const int units = rows * QR;
+    auto load = [&](int64_t kc0, float4 (&v)[UV]) {
+#pragma unroll
+      for (int u = 0; u < UV; ++u) {
+        const int idx = tid + u * NT;
+        const int row = idx / QR, kq = idx % QR;
+        const int64_t k = kc0 + 4 * kq;
+        const bool isx = row < rowsX;
+        const int64_t rr = isx ? row : row - rowsX;
+        const bool ok = idx < units && k < I && rr < (isx ? B : O);
+        const float* src = isx ? in : W;
+        const float4 x = *reinterpret_cast<const float4*>(src + (ok ? rr * I + k : 0));
+        v[u] = ok ? x : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+    };
+    auto store = [&](const float4 (&v)[UV]) {
+#pragma unroll
+      for (int u = 0; u < UV; ++u) {
+        const int idx = tid + u * NT;
+        if (idx < units) {
+          float* d = lds + (idx / QR) * KP + 4 * (idx % QR);
+          d[0] = v[u].x; d[1] = v[u].y; d[2] = v[u].z; d[3] = v[u].w;
+        }
+      }
+    };
+    float4 r0[UV], r1[UV];
+    load(0, r0);
+    if (nch > 1) load(KCH, r1);
+    for (int64_t c = 0; c < nch; c += 2) {
+      store(r0);
+      lds_barrier();
+      if (c + 2 < nch) load((c + 2) * KCH, r0);
+      compute();
+      lds_barrier();
+      if (c + 1 < nch) {
+        store(r1);
+        lds_barrier();
+        if (c + 3 < nch) load((c + 3) * KCH, r1);
+        compute();
+        lds_barrier();
+      }
+    }
+  } else {
+    for (int64_t kc0 = 0; kc0 < I; kc0 += KCH) {
+#pragma unroll 4
+      for (int i = tid; i < rows * KCH; i += NT) {
+        const int row = i / KCH, kk = i % KCH;
+        const int64_t k = kc0 + kk;
+        const bool isx = row < rowsX;
+        const int64_t rr = isx ? row : row - rowsX;
+        const bool ok = k < I && rr < (isx ? B : O);
+        const float* src = isx ? in : W;
+        const float v = src[ok ? rr * I + k : 0];
+        lds[row * KP + kk] = ok ? v : 0.0f;
+      }
+      lds_barrier();
+      compute();
+      lds_barrier();
+    }
   }
   if (active)
     for (int e = 0; e < 16; ++e) {
-      const int64_t m = m0 + acc_row(e), n = n0 + l31;
+      const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
       if (m < B && n < O) lds[(r * B + m) * O + n] = acc[e];
     }
 }
 
+// Backward gemm tasks of one wave (32x32 output tiles, ascending FMA chains
+// over k, the loads of 16 steps issued together).  delta is read from its
+// LDS copy sdel[B][O].
+//  * dW tile (TN: dW += delta^T . in, k over the batch): acc starts from the
+//    stored dW; with `upd` the tile's weights are loaded alongside (wv) for
+//    TConnectedLayer.update, which the caller applies once no dX task of the
+//    layer reads W any more;
+//  * dX tile (NN: prev_delta += delta . W, k over the outputs): prev_delta
+//    is the forward pass's zeroed delta, so the chain starts from +0; the
+//    result goes to memory and to the LDS block `nxt` the next stage reads.
+__device__ __forceinline__ void dw_task(const float* sdel, int64_t m0, int64_t n0, int64_t B,
+                                        int64_t O, int64_t I, const float* lin, const float* dW,
+                                        const float* W, bool upd, floatx16& acc, float (&wv)[16],
+                                        int lane) {
+  const int l31 = lane & 31, h = lane >> 5;
+  for (int e = 0; e < 16; ++e) {
+    const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
+    const bool ok = m < O && n < I;
+    const int64_t ix = ok ? m * I + n : 0;
+    const float c = dW[ix];
+    acc[e] = ok ? c : 0.0f;
+    wv[e] = upd ? W[ix] : 0.0f;
+  }
+  const int64_t m = m0 + l31, n = n0 + l31;
+  const bool vm = m < O, vn = n < I;
+  const int64_t mc = vm ? m : 0, nc = vn ? n : 0;
+  const int steps = (int)((B + 1) / 2);
+  constexpr int U = 16;
+  for (int s = 0; s < steps; s += U) {
+    float av[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = 2 * (int64_t)(s + u) + h;
+      const bool ok = s + u < steps && k < B;
+      const int64_t kc = ok ? k : 0;
+      const float x = sdel[kc * O + mc], y = lin[kc * I + nc];
+      av[u] = (ok && vm) ? x : 0.0f;
+      bv[u] = (ok && vn) ? y : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (s + u < steps) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  }
+}
+
+// weight update of one dW tile (ora_sgd_update's weight part) or its plain store
+__device__ __forceinline__ void dw_store(int64_t m0, int64_t n0, int64_t O, int64_t I, float* dW,
+                                         float* W, bool upd, const floatx16& acc,
+                                         const float (&wv)[16], float lrb, float wdec,
+                                         float momentum, int lane) {
+  const int l31 = lane & 31;
+  for (int e = 0; e < 16; ++e) {
+    const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
+    if (m < O && n < I) {
+      if (upd) {
+        const float dw = fmaf(wdec, wv[e], acc[e]);  // weight_updates.axpy(-decay*batch, W)
+        W[m * I + n] = fmaf(lrb, dw, wv[e]);          // weights.axpy(lr/batch, dW)
+        dW[m * I + n] = momentum * dw;                // weight_updates.Multiply(momentum)
+      } else {
+        dW[m * I + n] = acc[e];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void dx_task(const float* sdel, int64_t m0, int64_t n0, int64_t B,
+                                        int64_t O, int64_t I, const float* W, float* prev,
+                                        float* nxt, int lane) {
+  const int l31 = lane & 31, h = lane >> 5;
+  floatx16 acc;
+  for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+  const int64_t m = m0 + l31, n = n0 + l31;
+  const bool vm = m < B, vn = n < I;
+  const int64_t mc = vm ? m : 0, nc = vn ? n : 0;
+  const int steps = (int)((O + 1) / 2);
+  constexpr int U = 16;
+  for (int s = 0; s < steps; s += U) {
+    float av[U], bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t k = 2 * (int64_t)(s + u) + h;
+      const bool ok = s + u < steps && k < O;
+      const int64_t kc = ok ? k : 0;
+      const float x = sdel[mc * O + kc], y = W[kc * I + nc];
+      av[u] = (ok && vm) ? x : 0.0f;
+      bv[u] = (ok && vn) ? y : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (s + u < steps) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
+  }
+  for (int e = 0; e < 16; ++e) {
+    const int64_t mm = m0 + acc_row(e, lane), nn = n0 + l31;
+    if (mm < B && nn < I) {
+      prev[mm * I + nn] = acc[e];
+      nxt[mm * I + nn] = acc[e];
+    }
+  }
+}
+
+// every layer's dW/dX tasks fit one per wave: the weight update of layer l
+// is applied by its dW waves right after the stage's dX tasks are done
+__device__ __forceinline__ bool defer_update(int64_t B, int64_t O, int64_t I) {
+  const int64_t tmo = (O + 31) / 32, tni = (I + 31) / 32, tmb = (B + 31) / 32;
+  return tmo * tni + tmb * tni <= NWAVES;
+}
+
+template <int EPT>
 __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
-  // 8 * B * O_max floats: partial sums of the forward gemm; between gemms,
-  // up to three [B][O] blocks staged for the per-channel (column) passes, so
-  // their sequential sums read LDS instead of waiting on memory per row
+  // [0, act_off): partial sums of the forward gemm (8 * B * O_max) or its
+  // staged k-chunks; between gemms the [B][O] blocks and per-channel
+  // statistics of the column passes.  [act_off, + B * max width): the block
+  // handed from one stage to the next (forward activations, then the softmax
+  // delta and each dX result), so no stage reads another thread's output
+  // back from memory.
   extern __shared__ float lds[];
-  const int tid = threadIdx.x;
-  const int wid = tid >> 6;
-  const int lane = tid & 63;
+  float* act = lds + a.act_off;
   const int64_t B = a.batch;
   const int L = a.nlayers;
   const int64_t C = a.widths[L];
+  const int Bi = (int)B, Ci = (int)C;  // LDS-resident sizes: 9*B*max(O) <= 40960
   float* smx = a.buf + a.softmax_off;
   float* sm_out = smx;
   float* sm_delta = smx + B * C;
   float* sm_loss = smx + 2 * B * C;
+  const float lrb = a.lr / (float)B;
+  const float wdec = -a.decay * (float)B;
+  const float mom = a.momentum;
 
   // ---- forward ------------------------------------------------------------
   MLP_STAMP(0);
   const float* in = a.X;
   for (int l = 0; l < L; ++l) {
+    const int tid = stage_tid(), wid = tid >> 6, lane = tid & 63;
     const Layer lay(a, l);
     const int64_t I = lay.I, O = lay.O, BO = B * O;
-    for (int64_t e = tid; e < BO; e += NT) lay.delta()[e] = 0.0f;  // nnet.pas:287-296
+    const int Oi = (int)O;
+    float* out = lay.out();
+    // ahead of the gemm: per element slot the stored C (beta = 0 still reads
+    // it: 0*C), bias and BN scale; per channel (first slot) the rolling
+    // statistics; delta zeroed (nnet.pas:287-296)
+    float pc[EPT], pb[EPT], ps[EPT], yv[EPT];
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      pc[q] = pb[q] = ps[q] = yv[q] = 0.0f;
+      if (e < BO) {
+        const int o = e % Oi;
+        pc[q] = out[e];
+        pb[q] = lay.b()[o];
+        if (a.bn) ps[q] = lay.scales()[o];
+        lay.delta()[e] = 0.0f;
+      }
+    }
+    if (l == 1) MLP_MARK(0);
+    float rm_pre = 0.0f, rv_pre = 0.0f;
+    if (a.bn && tid < Oi) {
+      rm_pre = lay.rmean()[tid];
+      rv_pre = lay.rvar()[tid];
+    }
 
     // gemm(RowMajor, NoTrans, Trans, B, O, I, 1, in, I, W, I, 0, out, O):
     // sdot_avx2 residue classes r = k mod 8, each an ascending MFMA chain
@@ -201,13 +435,10 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     const int64_t kr = (I + 7) / 8;            // k values per residue class
     const int steps = (int)((kr + 1) / 2);
     if (tm * tn * 8 <= NWAVES && a.lds_chunks) {
-      // One (tile, residue) task per wave; both operands are k-contiguous
-      // rows (an MFMA lane per row), so they are staged through LDS in
-      // k-chunks by coalesced loads (gemm_chunked)
       if (I > 64)
-        gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn);
+        gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn, tid);
       else
-        gemm_chunked<64>(lds, in, lay.W(), B, O, I, tm, tn);
+        gemm_chunked<64>(lds, in, lay.W(), B, O, I, tm, tn, tid);
     } else
     for (int w = wid; w < tm * tn * 8; w += NWAVES) {
       const int r = w & 7, tile = w >> 3;
@@ -222,95 +453,160 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
                    lay.W() + (n < O ? n : 0) * I + k0, 16, n < O, k0, 16, I);
       }
       for (int e = 0; e < 16; ++e) {
-        const int64_t m = m0 + acc_row(e), n = n0 + (lane & 31);
+        const int64_t m = m0 + acc_row(e, lane), n = n0 + (lane & 31);
         if (m < B && n < O) lds[(r * B + m) * O + n] = acc[e];
       }
     }
-    __syncthreads();
-    for (int64_t e = tid; e < BO; e += NT) {
-      float p[8];
-      for (int q = 0; q < 8; ++q) p[q] = lds[q * BO + e];
-      const float s0 = p[0] + p[4], s1 = p[1] + p[5], s2 = p[2] + p[6], s3 = p[3] + p[7];
-      const float dot = (s0 + s1) + (s2 + s3);
-      const float c0 = 0.0f * lay.out()[e];  // beta = 0 => 0*C (mulvs)
-      const float y = c0 + 1.0f * dot;       // C := C + ALPHA*sdot
-      lay.out()[e] = y;
-      lds[e] = y;  // (this thread's own partial slot, already read)
+    if (l == 1) MLP_MARK(1);
+    lds_barrier();
+    if (l == 1) MLP_MARK(2);
+    // fold the 8 residue partials (vextractf128 / vhaddps order), C := 0*C +
+    // 1*sdot; without BN the bias and activation follow in the same pass
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      if (e < BO) {
+        float p[8];
+        for (int j = 0; j < 8; ++j) p[j] = lds[j * BO + e];
+        const float s0 = p[0] + p[4], s1 = p[1] + p[5], s2 = p[2] + p[6], s3 = p[3] + p[7];
+        const float dot = (s0 + s1) + (s2 + s3);
+        const float y = 0.0f * pc[q] + 1.0f * dot;  // beta = 0 => 0*C (mulvs); C + ALPHA*sdot
+        if (a.bn) {
+          yv[q] = y;
+          lay.x()[e] = y;  // x := out before normalize
+          lds[e] = y;      // (this thread's own partial slot, already read)
+        } else {
+          const float z = act_apply(y + pb[q], lay.act);  // forwardBias, activate
+          out[e] = z;
+          act[e] = z;
+        }
+      }
     }
-    __syncthreads();
+    if (l == 1) MLP_MARK(3);
     if (a.bn) {
-      // per channel: MeansAndVars, rolling stats, x, normalize, x_norm, scale
-      const float* col = lds;  // the layer output, [B][O]
-      for (int64_t o = tid; o < O; o += NT) {
-        // this channel's parameters, all loaded before any store: one memory
-        // round trip instead of one per use
-        const float rm0 = lay.rmean()[o], rv0 = lay.rvar()[o], sc = lay.scales()[o];
+      lds_barrier();
+      if (l == 1) MLP_MARK(4);
+      // per channel: MeansAndVars (sequential over the batch), rolling stats;
+      // mean and sd to LDS for the element pass
+      float* st_m = lds + BO;
+      float* st_sd = lds + BO + O;
+      auto chain = [&](int o, float rm0, float rv0) {
         float m = 0.0f;
-#pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) m = m + col[b * O + o];
+        for (int b0 = 0; b0 < Bi; b0 += 8) {
+          float c[8];
+          col8(c, lds + o, b0, Bi, Oi);
+          hold8(c);
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (b0 + u < Bi) m = m + c[u];
+        }
         m = m / (float)B;
         float v = 0.0f;
-#pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) {
-          const float t = col[b * O + o] - m;
-          v = v + t * t;
+        for (int b0 = 0; b0 < Bi; b0 += 8) {
+          float c[8];
+          col8(c, lds + o, b0, Bi, Oi);
+          hold8(c);
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (b0 + u < Bi) {
+              const float t = c[u] - m;
+              v = v + t * t;
+            }
         }
         v = v / (float)(B - 1);
         lay.mean()[o] = m;
         lay.var()[o] = v;
-        const float mom = 0.05f;  // bnMomentum, nconnectedlayer.pas:67
-        lay.rmean()[o] = fmaf(mom, m, rm0 * (1.0f - mom));
-        lay.rvar()[o] = fmaf(mom, v, rv0 * (1.0f - mom));
-        const float sd = sqrtf(v > SEPS ? v : SEPS);
-#pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) {
-          const float xv = col[b * O + o];
-          lay.x()[b * O + o] = xv;
-          const float xn = (xv - m) / sd;
-          lay.xnorm()[b * O + o] = xn;
-          lay.out()[b * O + o] = xn * sc;
+        const float bmom = 0.05f;  // bnMomentum, nconnectedlayer.pas:67
+        lay.rmean()[o] = fmaf(bmom, m, rm0 * (1.0f - bmom));
+        lay.rvar()[o] = fmaf(bmom, v, rv0 * (1.0f - bmom));
+        st_m[o] = m;
+        st_sd[o] = sqrtf(v > SEPS ? v : SEPS);
+      };
+      if (tid < Oi) chain(tid, rm_pre, rv_pre);  // statistics prefetched
+      for (int o = tid + NT; o < Oi; o += NT) chain(o, lay.rmean()[o], lay.rvar()[o]);
+      if (l == 1) MLP_MARK(5);
+      lds_barrier();
+      if (l == 1) MLP_MARK(6);
+      // per element: normalize, x_norm, scale, bias, activation
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        const int e = tid + q * NT;
+        if (e < BO) {
+          const int o = e % Oi;
+          const float xn = (yv[q] - st_m[o]) / st_sd[o];
+          lay.xnorm()[e] = xn;
+          const float z = act_apply(xn * ps[q] + pb[q], lay.act);
+          out[e] = z;
+          act[e] = z;
         }
       }
-      __syncthreads();
     }
-    for (int64_t e = tid; e < BO; e += NT) {
-      const int64_t o = e % O;
-      lay.out()[e] = act_apply(lay.out()[e] + lay.b()[o], lay.act);  // forwardBias, activate
-    }
-    __syncthreads();
-    in = lay.out();
+    if (l == 1) MLP_MARK(7);
+    lds_barrier();
+    if (l == 1) MLP_MARK(8);
+    in = act;
     MLP_STAMP(1 + l);
   }
 
   // ---- softmax + cross-entropy (groups 1, temperature 1) ----------------------
-  for (int64_t b = tid; b < B; b += NT) {
-    const float* ip = in + b * C;
-    float* op = sm_out + b * C;
-    float largest = ip[0];
-    for (int64_t i = 1; i < C; ++i)
-      if (ip[i] > largest) largest = ip[i];
-    float sum = 0.0f;
-    for (int64_t i = 0; i < C; ++i) {
-      const float e = (float)exp((double)((ip[i] - largest) / 1.0f));
-      sum = sum + e;
-      op[i] = e;
+  {
+    const int tid = stage_tid();
+    const int BC = Bi * Ci;
+    float* sx = act;             // logits (the last layer's output)
+    float* sex = lds;            // exp(x - largest)
+    float* smax = lds + BC;      // per row
+    float* ssum = smax + B;
+    float pt[EPT];
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      pt[q] = e < BC ? a.truth[e] : 0.0f;
     }
-    for (int64_t i = 0; i < C; ++i) op[i] = op[i] / sum;
+    for (int b = tid; b < Bi; b += NT) {
+      const float* ip = sx + b * Ci;
+      float largest = ip[0];
+      for (int i = 1; i < Ci; ++i)
+        if (ip[i] > largest) largest = ip[i];
+      smax[b] = largest;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      if (e < BC) sex[e] = (float)exp((double)((sx[e] - smax[e / Ci]) / 1.0f));
+    }
+    lds_barrier();
+    for (int b = tid; b < Bi; b += NT) {
+      const float* ep = sex + b * Ci;
+      float sum = 0.0f;
+      for (int i = 0; i < Ci; ++i) sum = sum + ep[i];
+      ssum[b] = sum;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      if (e < BC) {
+        const float p = sex[e] / ssum[e / Ci];
+        sm_out[e] = p;
+        sm_loss[e] = pt[q] != 0.0f ? (float)(-log((double)(p > SEPS ? p : SEPS))) : 0.0f;
+        const float d = pt[q] - p;
+        sm_delta[e] = d;
+        act[e] = d;  // (the logits are no longer read)
+      }
+    }
+    // the global writes of the forward pass (layer outputs) are read by other
+    // threads as dW operands below: one full barrier
+    __syncthreads();
   }
-  __syncthreads();
-  for (int64_t i = tid; i < B * C; i += NT) {
-    const float t = a.truth[i], p = sm_out[i];
-    sm_loss[i] = t != 0.0f ? (float)(-log((double)(p > SEPS ? p : SEPS))) : 0.0f;
-    sm_delta[i] = t - p;
-  }
-  __syncthreads();
-  if (tid == 0) *a.cost = vssum8(sm_loss, B * C);
   MLP_STAMP(20);
 
   // ---- backward ---------------------------------------------------------------
   for (int l = L - 1; l >= 0; --l) {
+    const int tid = stage_tid(), wid = tid >> 6, lane = tid & 63;
     const Layer lay(a, l);
     const int64_t I = lay.I, O = lay.O, BO = B * O;
+    const int Oi = (int)O;
     const float* lin = a.X;
     float* prev_delta = nullptr;
     if (l > 0) {
@@ -318,143 +614,231 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       lin = prev.out();
       prev_delta = prev.delta();  // state.delta = nil for layer 0 (nnet.pas:332-335)
     }
-    // softmax backward: prev.delta() += delta; then clamp + activation gradient.
-    // Stage delta (and x, x_norm for batch norm) in LDS for the column passes.
+    const int tmo = (int)((O + 31) / 32), tni = (int)((I + 31) / 32), tmb = (int)((B + 31) / 32);
+    const int nw_dw = tmo * tni, nw_dx = prev_delta ? tmb * tni : 0;
+    const bool defer = l > 0 && defer_update(B, O, I);
+    // ahead of the stage: per element out / x / x_norm; per channel (first
+    // slot) the parameters of the column pass and of the update
+    float dv[EPT], xv[EPT], yo[EPT], xnv[EPT];
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      dv[q] = xv[q] = yo[q] = xnv[q] = 0.0f;
+      if (e < BO) {
+        yo[q] = lay.out()[e];
+        if (a.bn) {
+          xv[q] = lay.x()[e];
+          xnv[q] = lay.xnorm()[e];
+        }
+      }
+    }
+    float db_pre = 0.0f, b_pre = 0.0f, ds_pre = 0.0f, sc_pre = 0.0f, mu_pre = 0.0f,
+          var_pre = 0.0f;
+    if (tid < Oi) {
+      db_pre = lay.db()[tid];
+      b_pre = lay.b()[tid];
+      if (a.bn) {
+        ds_pre = lay.dscales()[tid];
+        sc_pre = lay.scales()[tid];
+        mu_pre = lay.mean()[tid];
+        var_pre = lay.var()[tid];
+      }
+    }
+    // delta (the softmax delta added into the zeroed one for the last layer,
+    // else the dX result of the previous stage, both in `act`): clamp, times
+    // the activation gradient; staged with x, x_norm for the column passes
+    if (l == 2) MLP_MARK(10);
     float* sdel = lds;
     float* sx = lds + BO;
     float* sxn = lds + 2 * BO;
-    for (int64_t e = tid; e < BO; e += NT) {
-      float d = lay.delta()[e];
-      if (l == L - 1) d = d + sm_delta[e];
-      d = d < -1.0f ? -1.0f : (d > 1.0f ? 1.0f : d);  // delta.Clamp(-1, 1)
-      d = d * grad_apply(lay.out()[e], lay.act);
-      lay.delta()[e] = d;
-      sdel[e] = d;
-      if (a.bn) {
-        sx[e] = lay.x()[e];
-        sxn[e] = lay.xnorm()[e];
+    float* st = lds + 3 * BO;  // per channel: scale, mean, sd, mean_delta/B, 2*var_delta/B
+#pragma unroll
+    for (int q = 0; q < EPT; ++q) {
+      const int e = tid + q * NT;
+      if (e < BO) {
+        float d = act[e];
+        if (l == L - 1) d = 0.0f + d;  // delta (zeroed in the forward pass) + softmax delta
+        d = d < -1.0f ? -1.0f : (d > 1.0f ? 1.0f : d);  // delta.Clamp(-1, 1)
+        d = d * grad_apply(yo[q], lay.act);
+        sdel[e] = d;
+        dv[q] = d;
+        if (a.bn) {
+          sx[e] = xv[q];
+          sxn[e] = xnv[q];
+        } else {
+          lay.delta()[e] = d;
+        }
       }
     }
-    __syncthreads();
+    if (l == 2) MLP_MARK(11);
+    lds_barrier();
+    if (l == 2) MLP_MARK(12);
     MLP_STAMP(50 + 2 * l);
-    // per channel: bias_updates.addSums, then the BN backward chain
-    for (int64_t o = tid; o < O; o += NT) {
-      // this channel's parameters, all loaded before any store (one memory
-      // round trip instead of one per use)
-      const float db0 = lay.db()[o];
-      float ds0 = 0.0f, sc = 0.0f, mu = 0.0f, var = 0.0f;
-      if (a.bn) {
-        ds0 = lay.dscales()[o];
-        sc = lay.scales()[o];
-        mu = lay.mean()[o];
-        var = lay.var()[o];
-      }
-      float r = 0.0f;
-#pragma unroll 8
-      for (int64_t b = 0; b < B; ++b) r = r + sdel[b * O + o];
-      lay.db()[o] = db0 + r;
-      if (a.bn) {
-        float dd = 0.0f;  // addDots (strided sdot: mul then add)
-#pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) dd = dd + sxn[b * O + o] * sdel[b * O + o];
-        lay.dscales()[o] = ds0 + dd;
-        float m = 0.0f, v = 0.0f;
-#pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) {
-          const float d = sdel[b * O + o] * sc;  // forwardScale
-          sdel[b * O + o] = d;                   // (own column only)
-          m = m + d;
-          v = v + (sx[b * O + o] - mu) * d;
+    // per channel: bias_updates.addSums and, with BN, addDots (strided sdot:
+    // mul then add), forwardScale and meansAndVarsDelta — four independent
+    // sequential chains over the batch, interleaved in one loop; then this
+    // layer's bias / scale update (TConnectedLayer.update: nothing later in
+    // the step reads b, db, dscales, and scales only from LDS)
+    auto chain = [&](int o, float db0, float b0, float ds0, float sc, float mu, float var) {
+      float r = 0.0f, dd = 0.0f, m = 0.0f, v = 0.0f;
+      for (int b0r = 0; b0r < Bi; b0r += 8) {
+        float cs[8], cn[8], cx[8];
+        col8(cs, sdel + o, b0r, Bi, Oi);
+        if (a.bn) {
+          col8(cn, sxn + o, b0r, Bi, Oi);
+          col8(cx, sx + o, b0r, Bi, Oi);
+          hold8(cn);
+          hold8(cx);
         }
+        hold8(cs);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (b0r + u < Bi) {
+            const float sv = cs[u];
+            r = r + sv;
+            if (a.bn) {
+              dd = dd + cn[u] * sv;
+              const float d = sv * sc;  // forwardScale
+              m = m + d;
+              v = v + (cx[u] - mu) * d;
+            }
+          }
+        }
+      }
+      const float dbn = db0 + r;
+      lay.b()[o] = fmaf(lrb, dbn, b0);  // biases.axpy(lr/batch, bias_updates)
+      lay.db()[o] = mom * dbn;          // bias_updates.Multiply(momentum)
+      if (a.bn) {
+        const float dsn = ds0 + dd;
+        lay.scales()[o] = fmaf(lrb, dsn, sc);  // scales.axpy(lr/batch, scale_updates)
+        lay.dscales()[o] = mom * dsn;          // scale_updates.Multiply(momentum)
         const float ve = var > SEPS ? var : SEPS;
         const float md = m * (-1.0f / sqrtf(ve));
         const float vd = (float)((double)v * -0.5 * pow((double)ve, -1.5));
         lay.mdelta()[o] = md;
         lay.vdelta()[o] = vd;
-        const float mdb = md / (float)B, vdb = 2.0f * vd / (float)B, sd = sqrtf(ve);
-#pragma unroll 8
-        for (int64_t b = 0; b < B; ++b) {
-          const float q = sdel[b * O + o] / sd;
-          const float t = (sx[b * O + o] - mu) * vdb + mdb;
-          lay.delta()[b * O + o] = q + t;
+        st[o] = sc;
+        st[O + o] = mu;
+        st[2 * O + o] = sqrtf(ve);
+        st[3 * O + o] = md / (float)B;
+        st[4 * O + o] = 2.0f * vd / (float)B;
+      }
+    };
+    if (tid < Oi) chain(tid, db_pre, b_pre, ds_pre, sc_pre, mu_pre, var_pre);  // prefetched
+    for (int o = tid + NT; o < Oi; o += NT)
+      chain(o, lay.db()[o], lay.b()[o], a.bn ? lay.dscales()[o] : 0.0f,
+            a.bn ? lay.scales()[o] : 0.0f, a.bn ? lay.mean()[o] : 0.0f,
+            a.bn ? lay.var()[o] : 0.0f);
+    if (l == 2) MLP_MARK(13);
+    if (a.bn) {
+      lds_barrier();
+      if (l == 2) MLP_MARK(14);
+      // per element: normalizeDelta of the scaled delta
+#pragma unroll
+      for (int q = 0; q < EPT; ++q) {
+        const int e = tid + q * NT;
+        if (e < BO) {
+          const int o = e % Oi;
+          const float d = dv[q] * st[o];
+          const float qd = d / st[2 * O + o];
+          const float t = (xv[q] - st[O + o]) * st[4 * O + o] + st[3 * O + o];
+          const float nd = qd + t;
+          lay.delta()[e] = nd;
+          sdel[e] = nd;
         }
       }
     }
-    __syncthreads();
+    if (l == 2) MLP_MARK(15);
+    lds_barrier();
+    if (l == 2) MLP_MARK(16);
     MLP_STAMP(51 + 2 * l);
     // dW += delta^T . in   (TN: M=O, N=I, K=B, beta 1)   and
-    // prev_delta += delta . W (NN: M=B, N=I, K=O, beta 1), both ascending chains
-    const int tmo = (int)((O + 31) / 32), tni = (int)((I + 31) / 32), tmb = (int)((B + 31) / 32);
-    const int nw_dw = tmo * tni, nw_dx = prev_delta ? tmb * tni : 0;
+    // prev_delta += delta . W (NN: M=B, N=I, K=O, beta 1), both ascending
+    // chains; layer 0 (no dX) updates its weights in the dW epilogue, other
+    // layers after the stage's dX tasks (or in the pass after the backward)
+    bool have = false;
+    int64_t hm0 = 0, hn0 = 0;
+    floatx16 hacc;
+    float hw[16];
     for (int w = wid; w < nw_dw + nw_dx; w += NWAVES) {
-      floatx16 acc;
-      const bool is_dw = w < nw_dw;
-      const int t = is_dw ? w : w - nw_dw;
-      const int64_t m0 = (int64_t)(t / tni) * 32, n0 = (int64_t)(t % tni) * 32;
-      const int64_t Mx = is_dw ? O : B;
-      float* Cp = is_dw ? lay.dW() : prev_delta;
-      for (int e = 0; e < 16; ++e) {
-        const int64_t m = m0 + acc_row(e), n = n0 + (lane & 31);
-        acc[e] = (m < Mx && n < I) ? Cp[m * I + n] : 0.0f;
-      }
-      const int l31 = lane & 31, h = lane >> 5;
-      const int64_t m = m0 + l31, n = n0 + l31, nc = n < I ? n : 0;
-      if (is_dw) {  // a = delta[k][m], b = in[k][n], k = 2s + h over the batch
-        const int64_t mc = m < O ? m : 0;
-        mfma_chain(acc, (int)((B + 1) / 2), lay.delta() + h * O + mc, 2 * O, m < O,
-                   lin + h * I + nc, 2 * I, n < I, h, 2, B);
-      } else {      // a = delta[m][k], b = W[k][n], k = 2s + h over the outputs
-        const int64_t mc = m < B ? m : 0;
-        mfma_chain(acc, (int)((O + 1) / 2), lay.delta() + mc * O + h, 2, m < B,
-                   lay.W() + h * I + nc, 2 * I, n < I, h, 2, O);
-      }
-      for (int e = 0; e < 16; ++e) {
-        const int64_t m = m0 + acc_row(e), n = n0 + (lane & 31);
-        if (m < Mx && n < I) Cp[m * I + n] = acc[e];
+      if (w < nw_dw) {
+        const int64_t m0 = (int64_t)(w / tni) * 32, n0 = (int64_t)(w % tni) * 32;
+        dw_task(sdel, m0, n0, B, O, I, lin, lay.dW(), lay.W(), l == 0 || defer, hacc, hw, lane);
+        if (l == 2) MLP_MARK(17);
+        if (defer) {
+          have = true;
+          hm0 = m0;
+          hn0 = n0;
+        } else {
+          dw_store(m0, n0, O, I, lay.dW(), lay.W(), l == 0, hacc, hw, lrb, wdec, mom, lane);
+        }
+      } else {
+        const int t = w - nw_dw;
+        const int64_t m0 = (int64_t)(t / tni) * 32, n0 = (int64_t)(t % tni) * 32;
+        dx_task(sdel, m0, n0, B, O, I, lay.W(), prev_delta, act, lane);
       }
     }
-    __syncthreads();
+    if (l == 2) MLP_MARK(18);
+    lds_barrier();  // every dX task has read W and written its block to `act`
+    if (l == 2) MLP_MARK(19);
+    if (have) dw_store(hm0, hn0, O, I, lay.dW(), lay.W(), true, hacc, hw, lrb, wdec, mom, lane);
     MLP_STAMP(21 + l);
   }
 
-  // ---- update (TConnectedLayer.update, constant learning rate) ----------------
-  const float lrb = a.lr / (float)B;
-  const float wdec = -a.decay * (float)B;
-  for (int l = 0; l < L; ++l) {
-    const Layer lay(a, l);
-    const int64_t O = lay.O, IO = lay.I * lay.O;
-    for (int64_t o = tid; o < O; o += NT) {
-      lay.b()[o] = fmaf(lrb, lay.db()[o], lay.b()[o]);
-      lay.db()[o] = a.momentum * lay.db()[o];
-      if (a.bn) {
-        lay.scales()[o] = fmaf(lrb, lay.dscales()[o], lay.scales()[o]);
-        lay.dscales()[o] = a.momentum * lay.dscales()[o];
-      }
-    }
-    // UB elements per thread per round, their loads issued together (W and dW
-    // live in one buffer: the compiler cannot move a load past a store)
-    constexpr int UB = 8;
-    float* W = lay.W();
-    float* dW = lay.dW();
-    for (int64_t e0 = tid; e0 < IO; e0 += (int64_t)NT * UB) {
-      float w[UB], g[UB];
+  // ---- weight update of layers whose dW tasks were more than one per wave
+  // (none in the MNIST net), after every dW store is visible ---------------------
+  bool rest = false;
+  for (int l = 1; l < L; ++l) rest = rest || !defer_update(B, a.widths[l + 1], a.widths[l]);
+  if (rest) {
+    const int tid = stage_tid();
+    __syncthreads();
+    for (int l = 1; l < L; ++l) {
+      const Layer lay(a, l);
+      if (defer_update(B, lay.O, lay.I)) continue;
+      const int64_t IO = lay.I * lay.O;
+      float* W = lay.W();
+      float* dW = lay.dW();
+      constexpr int UB = 8;
+      for (int64_t e0 = tid; e0 < IO; e0 += (int64_t)NT * UB) {
+        float w[UB], g[UB];
 #pragma unroll
-      for (int u = 0; u < UB; ++u) {
-        const int64_t e = e0 + (int64_t)u * NT;
-        w[u] = W[e < IO ? e : e0];
-        g[u] = dW[e < IO ? e : e0];
-      }
+        for (int u = 0; u < UB; ++u) {
+          const int64_t e = e0 + (int64_t)u * NT;
+          w[u] = W[e < IO ? e : e0];
+          g[u] = dW[e < IO ? e : e0];
+        }
 #pragma unroll
-      for (int u = 0; u < UB; ++u) {
-        const int64_t e = e0 + (int64_t)u * NT;
-        if (e < IO) {
-          const float dw = fmaf(wdec, w[u], g[u]);  // weight_updates.axpy(-decay*batch, W)
-          W[e] = fmaf(lrb, dw, w[u]);               // weights.axpy(lr/batch, dW)
-          dW[e] = a.momentum * dw;                  // weight_updates.Multiply(momentum)
+        for (int u = 0; u < UB; ++u) {
+          const int64_t e = e0 + (int64_t)u * NT;
+          if (e < IO) {
+            const float dw = fmaf(wdec, w[u], g[u]);  // weight_updates.axpy(-decay*batch, W)
+            W[e] = fmaf(lrb, dw, w[u]);               // weights.axpy(lr/batch, dW)
+            dW[e] = mom * dw;                         // weight_updates.Multiply(momentum)
+          }
         }
       }
     }
-    MLP_STAMP(40 + l);
+  }
+  MLP_STAMP(40);
+
+  // ---- cost: loss.Sum() in the vssum_avx2 order: lane l of wave 0 sums
+  // elements 8t + l in ascending t, lane 0 folds (l, l+4), the pairs and the
+  // tail (sm_loss was written before the full barrier after the softmax) ----
+  const int wid = stage_tid() >> 6, lane = threadIdx.x & 63;
+  if (wid == 0) {
+    const int64_t n = B * C, blocks = n >> 3;
+    float acc = 0.0f;
+    if (lane < 8)
+      for (int64_t t = 0; t < blocks; ++t) acc = acc + sm_loss[8 * t + lane];
+    const float a0 = __shfl(acc, 0), a1 = __shfl(acc, 1), a2 = __shfl(acc, 2),
+                a3 = __shfl(acc, 3), a4 = __shfl(acc, 4), a5 = __shfl(acc, 5),
+                a6 = __shfl(acc, 6), a7 = __shfl(acc, 7);
+    if (lane == 0) {
+      const float s0 = a0 + a4, s1 = a1 + a5, s2 = a2 + a6, s3 = a3 + a7;
+      float r = (s0 + s1) + (s2 + s3);
+      for (int64_t i = blocks * 8; i < n; ++i) r = r + sm_loss[i];
+      *a.cost = r;
+    }
   }
 }
 
@@ -504,22 +888,34 @@ hipError_t launch_mlp_train_step(const MlpArgs& args, hipStream_t s) {
   a.stamp_off = p + 3 * B * a.widths[a.nlayers];
   int64_t omax = 0;
   for (int l = 0; l < a.nlayers; ++l) omax = a.widths[l + 1] > omax ? a.widths[l + 1] : omax;
-  // partial sums (>= 3 [B][O] blocks); the forward gemm's k-chunks of both
-  // operands reuse the same space when one (tile, residue) task per wave
-  // covers every layer
+  // [0, act_off): partial sums (8 [B][O] blocks; >= 3 blocks + statistics in
+  // the backward), or the forward gemm's k-chunks of both operands when one
+  // (tile, residue) task per wave covers every layer; then the [B][O_max]
+  // hand-off block
   const int64_t tmx = (a.batch + 31) / 32, tnx = (omax + 31) / 32;
-  size_t lds = (size_t)(8 * a.batch * omax) * sizeof(float);
-  const size_t lds_chunks = (size_t)((tmx + tnx) * 32 * (KC + 1)) * sizeof(float);
-  a.lds_chunks = tmx * tnx * 8 <= NWAVES && lds_chunks <= 160 * 1024;
-  if (a.lds_chunks && lds_chunks > lds) lds = lds_chunks;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const int64_t part = 8 * a.batch * omax, blk = a.batch * omax;
+  const int64_t chunks = (tmx + tnx) * 32 * (KC + 1);
+  constexpr int64_t LDS_FLOATS = 160 * 1024 / 4;
+  a.lds_chunks = tmx * tnx * 8 <= NWAVES && chunks + blk + 4 <= LDS_FLOATS;
+  int64_t act_off = a.lds_chunks && chunks > part ? chunks : part;
+  act_off = (act_off + 3) & ~(int64_t)3;  // 16-byte aligned hand-off block
+  a.act_off = act_off;
+  const size_t lds = (size_t)(act_off + blk) * sizeof(float);
+  if (act_off + blk > LDS_FLOATS) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds);
-    if (e != hipSuccess) return e;
+    const hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<2>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)lds);
+    const hipError_t e5 = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<5>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)lds);
+    if (e2 != hipSuccess) return e2;
+    if (e5 != hipSuccess) return e5;
   }
-  hipLaunchKernelGGL(mlp_train_kernel, dim3(1), dim3(NT), lds, s, a);
+  if (blk <= 2 * NT)
+    hipLaunchKernelGGL(mlp_train_kernel<2>, dim3(1), dim3(NT), lds, s, a);
+  else
+    hipLaunchKernelGGL(mlp_train_kernel<5>, dim3(1), dim3(NT), lds, s, a);
   return hipGetLastError();
 }
 

@@ -1053,8 +1053,8 @@ int tns_hip_mlp_train_step(tns_ctx* c, int32_t nlayers, const int64_t* widths,
     a.widths[l] = widths[l];
     if (l > 0 && widths[l] > omax) omax = widths[l];
   }
-  if (8 * batch * omax > 40960)
-    return set_error(TNS_ERR_ARG, "mlp_train_step: 8*batch*max(width) exceeds LDS staging");
+  if (9 * batch * omax > 40960)
+    return set_error(TNS_ERR_ARG, "mlp_train_step: 9*batch*max(width) exceeds LDS staging");
   for (int l = 0; l < nlayers; ++l) {
     if (!act_supported(acts[l]))
       return set_error(TNS_ERR_UNSUPPORTED, "mlp_train_step: activation %d", acts[l]);

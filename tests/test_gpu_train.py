@@ -182,6 +182,30 @@ def test_fused_mlp_train_step(hip, torch_cuda, ora, bn, steps):
     assert not bad, bad
 
 
+@pytest.mark.parametrize("widths,acts,B", [
+    ([101, 37, 70, 24, 10], [9, 0, 6, 4], 20),   # odd widths: scalar staging, 3-tile fallback gemm
+    ([64, 48, 33, 10], [1, 13, 4], 40),          # two batch tiles, hardtan
+    ([784, 64, 10], [1, 4], 2),                  # smallest batch
+])
+@pytest.mark.parametrize("bn", [0, 1])
+def test_fused_mlp_irregular_shapes(hip, torch_cuda, ora, widths, acts, B, bn):
+    """The fused step at shapes off the MNIST net: every buffer element and
+    the cost bit-identical to the oracle after 3 steps."""
+    buf = ora.mlp_init(widths, bn, B, seed=11)
+    X, T_ = ora.mnist_batch(B, seed=11, classes=widths[-1], inputs=widths[0])
+    T = torch_cuda
+    dbuf, dX, dT = dev(T, buf), dev(T, X), dev(T, T_)
+    dcost = T.zeros(1, device="cuda")
+    for _ in range(3):
+        cost = ora.mlp_train_step(widths, acts, bn, B, X, T_, 1e-2, 0.9, 1e-4, buf)
+        hip.mlpTrainStep(widths, acts, bn, B, dX, dT, 1e-2, 0.9, 1e-4, dbuf, dcost)
+    hip.finish()
+    got = dbuf.cpu().numpy()
+    assert float(dcost.item()) == np.float32(cost)
+    diff = np.flatnonzero(got != buf)
+    assert diff.size == 0, (diff.size, diff[:10])
+
+
 def test_fused_mlp_no_bn_is_bit_exact_one_step(hip, torch_cuda, ora):
     """Without BN the only transcendental is softmax's exp (in double on both
     sides), so one step should reproduce the oracle exactly."""
