@@ -34,8 +34,17 @@ def main():
         run()
         g, i, c = hip.opMs(TNS_OP_GEMM), hip.opMs(TNS_OP_IM2COL), hip.opMs(TNS_OP_COL2IM)
         hip.setTelemetry(False)
+        # dW alone (no state.delta: no dX GEMM, no col2im)
+        run_dw = lambda: hip.convBackward(batch, s.c, s.h, s.h, x, w, s.filters, s.size,  # noqa
+                                          s.stride, s.pad, 1, s.activation, o, d, bu, wu, None,
+                                          None)
+        run_dw()
+        hip.setTelemetry(True)
+        run_dw()
+        gw = hip.opMs(TNS_OP_GEMM)
+        hip.setTelemetry(False)
         out.append({"layer": s.index, "shape": f"{s.c}x{s.h} k{s.size}s{s.stride}->{s.filters}",
-                    "gemm_ms": round(g, 3), "tf": round(2 * s.flops * batch / g / 1e9, 1),
+                    "gemm_ms": round(g, 3), "dw_ms": round(gw, 3), "dx_ms": round(g - gw, 3), "tf": round(2 * s.flops * batch / g / 1e9, 1),
                     "im2col_ms": round(i, 3), "col2im_ms": round(c, 3)})
     print(json.dumps(out))
 

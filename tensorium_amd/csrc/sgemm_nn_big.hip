@@ -178,6 +178,12 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
   const int b_frag = wn * WTN + lc;         // rows lc + 32j
   auto frag = [&](const float* st, int s, float (&a)[TM], float (&b)[TN]) {
     const int k = 2 * s + h;
+#ifdef TNS_NB_NO_FRAG  // (diagnostic: MFMAs on register operands, no LDS reads)
+    for (int i = 0; i < TM; ++i) a[i] = (float)(lane + i + s);
+    for (int j = 0; j < TN; ++j) b[j] = (float)(lane - j + s);
+    (void)st; (void)k;
+    return;
+#endif
     const float* ap = st + k * LDA + (a_frag ^ (((k >> 2) & 7) << 2));
     if constexpr (TM == 4) {
       const float4 v = *reinterpret_cast<const float4*>(ap);
@@ -268,6 +274,7 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 using G256 = Geo<256, 256, 2, 4, 1>;  // 8 waves, wave tile 128x64, 1 block/CU
 using G128 = Geo<128, 128, 2, 2, 2>;  // 4 waves, wave tile 64x64, 2 blocks/CU
 using G256x128 = Geo<256, 128, 2, 2, 1>;  // 4 waves, wave tile 128x64
+using G256w16 = Geo<256, 256, 4, 4, 1>;   // 16 waves, wave tile 64x64, 4 waves per SIMD
 
 template <class G>
 bool applies(const GemmArgs& a) {
@@ -301,11 +308,11 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 
 // (a 4-wave 256x256 form, wave tile 128x128 at one wave per SIMD, spills 67
 // registers at the 512 cap — not instantiated)
-int sgemm_nn_big_count() { return 3; }
+int sgemm_nn_big_count() { return 4; }
 const char* sgemm_nn_big_name(int v) {
   static const char* names[] = {"256x256x32_w2x4_nn_big", "128x128x32_w2x2_nn_big",
-                                "256x128x32_w2x2_nn_big"};
-  return v >= 0 && v < 3 ? names[v] : "";
+                                "256x128x32_w2x2_nn_big", "256x256x32_w4x4_nn_big"};
+  return v >= 0 && v < 4 ? names[v] : "";
 }
 
 // heuristic: the 256x256 form when it gives about a block per CU
@@ -319,6 +326,7 @@ hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s) {
     case 0: return launch<G256>(a, s);
     case 1: return launch<G128>(a, s);
     case 2: return launch<G256x128>(a, s);
+    case 3: return launch<G256w16>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
