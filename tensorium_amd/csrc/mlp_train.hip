@@ -295,7 +295,7 @@ __device__ __forceinline__ void dw_task(const float* sdel, int64_t m0, int64_t n
   const bool vm = m < O, vn = n < I;
   const int64_t mc = vm ? m : 0, nc = vn ? n : 0;
   const int steps = (int)((B + 1) / 2);
-  constexpr int U = 16;
+  constexpr int U = 8;
   for (int s = 0; s < steps; s += U) {
     float av[U], bv[U];
 #pragma unroll
@@ -343,7 +343,7 @@ __device__ __forceinline__ void dx_task(const float* sdel, int64_t m0, int64_t n
   const bool vm = m < B, vn = n < I;
   const int64_t mc = vm ? m : 0, nc = vn ? n : 0;
   const int steps = (int)((O + 1) / 2);
-  constexpr int U = 16;
+  constexpr int U = 8;
   for (int s = 0; s < steps; s += U) {
     float av[U], bv[U];
 #pragma unroll
@@ -434,7 +434,15 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     const int tm = (int)((B + 31) / 32), tn = (int)((O + 31) / 32);
     const int64_t kr = (I + 7) / 8;            // k values per residue class
     const int steps = (int)((kr + 1) / 2);
-    if (tm * tn * 8 <= NWAVES && a.lds_chunks) {
+    if (l == 0) {
+      // layer 0's partials come from mlp_l0_forward_kernel, in this layout
+      if ((BO & 1) == 0) {  // 8*B*O floats = 2*B*O float4
+        const float4* src = reinterpret_cast<const float4*>(a.l0part);
+        for (int i = tid; i < (int)(2 * BO); i += NT) reinterpret_cast<float4*>(lds)[i] = src[i];
+      } else {
+        for (int i = tid; i < (int)(8 * BO); i += NT) lds[i] = a.l0part[i];
+      }
+    } else if (tm * tn * 8 <= NWAVES && a.lds_chunks) {
       if (I > 64)
         gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn, tid);
       else
@@ -615,25 +623,26 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       prev_delta = prev.delta();  // state.delta = nil for layer 0 (nnet.pas:332-335)
     }
     const int tmo = (int)((O + 31) / 32), tni = (int)((I + 31) / 32), tmb = (int)((B + 31) / 32);
-    const int nw_dw = tmo * tni, nw_dx = prev_delta ? tmb * tni : 0;
+    // (layer 0's dW and weight update: mlp_l0_dw_kernel, after this launch)
+    const int nw_dw = l == 0 ? 0 : tmo * tni, nw_dx = prev_delta ? tmb * tni : 0;
     const bool defer = l > 0 && defer_update(B, O, I);
     // ahead of the stage: per element out / x / x_norm; per channel (first
     // slot) the parameters of the column pass and of the update
-    float dv[EPT], xv[EPT], yo[EPT], xnv[EPT];
+    float dv[EPT], xv[EPT], yo[EPT], xnv[EPT], vv[EPT];
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
-      dv[q] = xv[q] = yo[q] = xnv[q] = 0.0f;
+      dv[q] = xv[q] = yo[q] = xnv[q] = vv[q] = 0.0f;
       if (e < BO) {
         yo[q] = lay.out()[e];
         if (a.bn) {
           xv[q] = lay.x()[e];
           xnv[q] = lay.xnorm()[e];
+          vv[q] = lay.var()[e % Oi];
         }
       }
     }
-    float db_pre = 0.0f, b_pre = 0.0f, ds_pre = 0.0f, sc_pre = 0.0f, mu_pre = 0.0f,
-          var_pre = 0.0f;
+    float db_pre = 0.0f, b_pre = 0.0f, ds_pre = 0.0f, sc_pre = 0.0f, mu_pre = 0.0f;
     if (tid < Oi) {
       db_pre = lay.db()[tid];
       b_pre = lay.b()[tid];
@@ -641,7 +650,6 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         ds_pre = lay.dscales()[tid];
         sc_pre = lay.scales()[tid];
         mu_pre = lay.mean()[tid];
-        var_pre = lay.var()[tid];
       }
     }
     // delta (the softmax delta added into the zeroed one for the last layer,
@@ -651,7 +659,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     float* sdel = lds;
     float* sx = lds + BO;
     float* sxn = lds + 2 * BO;
-    float* st = lds + 3 * BO;  // per channel: scale, mean, sd, mean_delta/B, 2*var_delta/B
+    float* st = lds + 3 * BO;  // per channel: scale, mean, sum m, sum v; then pow (double)
 #pragma unroll
     for (int q = 0; q < EPT; ++q) {
       const int e = tid + q * NT;
@@ -679,7 +687,21 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     // sequential chains over the batch, interleaved in one loop; then this
     // layer's bias / scale update (TConnectedLayer.update: nothing later in
     // the step reads b, db, dscales, and scales only from LDS)
-    auto chain = [&](int o, float db0, float b0, float ds0, float sc, float mu, float var) {
+    // the double pow of meansAndVarsDelta depends on the forward variance
+    // only: the last wave evaluates it for every channel while wave 0 runs
+    // the chains (it was the longest single latency of the chain thread)
+    double* st_pw = reinterpret_cast<double*>(st + ((4 * O + 1) & ~(int64_t)1));
+    if (a.bn && wid == NWAVES - 1)
+      for (int o = lane; o < Oi; o += 64) {
+        const float var = lay.var()[o];
+        const float ve = var > SEPS ? var : SEPS;
+#ifdef TNS_MLP_NOPOW  // (diagnostic timing build: wrong numbers)
+        st_pw[o] = (double)ve;
+#else
+        st_pw[o] = pow((double)ve, -1.5);
+#endif
+      }
+    auto chain = [&](int o, float db0, float b0, float ds0, float sc, float mu) {
       float r = 0.0f, dd = 0.0f, m = 0.0f, v = 0.0f;
       for (int b0r = 0; b0r < Bi; b0r += 8) {
         float cs[8], cn[8], cx[8];
@@ -712,36 +734,39 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         const float dsn = ds0 + dd;
         lay.scales()[o] = fmaf(lrb, dsn, sc);  // scales.axpy(lr/batch, scale_updates)
         lay.dscales()[o] = mom * dsn;          // scale_updates.Multiply(momentum)
-        const float ve = var > SEPS ? var : SEPS;
-        const float md = m * (-1.0f / sqrtf(ve));
-        const float vd = (float)((double)v * -0.5 * pow((double)ve, -1.5));
-        lay.mdelta()[o] = md;
-        lay.vdelta()[o] = vd;
         st[o] = sc;
         st[O + o] = mu;
-        st[2 * O + o] = sqrtf(ve);
-        st[3 * O + o] = md / (float)B;
-        st[4 * O + o] = 2.0f * vd / (float)B;
+        st[2 * O + o] = m;
+        st[3 * O + o] = v;
       }
     };
-    if (tid < Oi) chain(tid, db_pre, b_pre, ds_pre, sc_pre, mu_pre, var_pre);  // prefetched
+    if (tid < Oi) chain(tid, db_pre, b_pre, ds_pre, sc_pre, mu_pre);  // prefetched
     for (int o = tid + NT; o < Oi; o += NT)
       chain(o, lay.db()[o], lay.b()[o], a.bn ? lay.dscales()[o] : 0.0f,
-            a.bn ? lay.scales()[o] : 0.0f, a.bn ? lay.mean()[o] : 0.0f,
-            a.bn ? lay.var()[o] : 0.0f);
+            a.bn ? lay.scales()[o] : 0.0f, a.bn ? lay.mean()[o] : 0.0f);
     if (l == 2) MLP_MARK(13);
     if (a.bn) {
       lds_barrier();
       if (l == 2) MLP_MARK(14);
-      // per element: normalizeDelta of the scaled delta
+      // per element: the channel's mean/variance deltas (the thread of batch
+      // row 0 stores them), then normalizeDelta of the scaled delta
 #pragma unroll
       for (int q = 0; q < EPT; ++q) {
         const int e = tid + q * NT;
         if (e < BO) {
           const int o = e % Oi;
+          const float var = vv[q];
+          const float ve = var > SEPS ? var : SEPS;
+          const float sd = sqrtf(ve);
+          const float md = st[2 * O + o] * (-1.0f / sd);
+          const float vd = (float)((double)st[3 * O + o] * -0.5 * st_pw[o]);
+          if (e < O) {
+            lay.mdelta()[o] = md;
+            lay.vdelta()[o] = vd;
+          }
           const float d = dv[q] * st[o];
-          const float qd = d / st[2 * O + o];
-          const float t = (xv[q] - st[O + o]) * st[4 * O + o] + st[3 * O + o];
+          const float qd = d / sd;
+          const float t = (xv[q] - st[O + o]) * (2.0f * vd / (float)B) + md / (float)B;
           const float nd = qd + t;
           lay.delta()[e] = nd;
           sdel[e] = nd;
@@ -842,6 +867,109 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   }
 }
 
+
+// ---- layer 0 outside the single-CU launch ------------------------------------
+// Layer 0's gemms are the step's only large ones (784 x 64 at batch 32: 1.6 M
+// FMAs each, ~12.5 k MFMA cycles on one CU); they run as their own launches
+// over several CUs, before and after the fused kernel.
+
+// Forward residue partials of layer 0 (the same chains as gemm_chunked):
+// block = one 32x32 output tile x 4 residue classes (one per wave); both
+// operands' tile rows staged through LDS in k-chunks of KCH, float4 loads two
+// chunks ahead; partial r of (m, n) to part[(r*B + m)*O + n].
+template <int KCH, int VEC>
+__global__ __launch_bounds__(256) void mlp_l0_forward_kernel(const float* X, const float* W,
+                                                             int64_t B, int64_t O, int64_t I,
+                                                             float* part) {
+  // VEC = 4: float4 units (16-byte rows); 1: single floats
+  constexpr int KP = KCH + 1, QR = KCH / VEC, UV = (64 * QR + 255) / 256;
+  __shared__ float lds[64 * KP];
+  const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, l31 = lane & 31, h = lane >> 5;
+  const int tn = (int)((O + 31) / 32), tile = blockIdx.x >> 1;
+  const int64_t m0 = (int64_t)(tile / tn) * 32, n0 = (int64_t)(tile % tn) * 32;
+  const int r = 4 * (blockIdx.x & 1) + wid;
+  floatx16 acc;
+  for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+  auto load = [&](int64_t kc0, float4 (&v)[UV]) {
+#pragma unroll
+    for (int u = 0; u < UV; ++u) {
+      const int idx = tid + u * 256;
+      const int row = idx / QR, kq = idx % QR;
+      const int64_t k = kc0 + VEC * kq;
+      const bool isx = row < 32;
+      const int64_t g = isx ? m0 + row : n0 + row - 32;
+      const bool ok = idx < 64 * QR && k < I && g < (isx ? B : O);
+      const float* src = (isx ? X : W) + (ok ? g * I + k : 0);
+      if constexpr (VEC == 4) {
+        const float4 x = *reinterpret_cast<const float4*>(src);
+        v[u] = ok ? x : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      } else {
+        const float x = *src;
+        v[u].x = ok ? x : 0.0f;
+      }
+    }
+  };
+  auto store = [&](const float4 (&v)[UV]) {
+#pragma unroll
+    for (int u = 0; u < UV; ++u) {
+      const int idx = tid + u * 256;
+      if (idx < 64 * QR) {
+        float* d = lds + (idx / QR) * KP + VEC * (idx % QR);
+        d[0] = v[u].x;
+        if constexpr (VEC == 4) {
+          d[1] = v[u].y; d[2] = v[u].z; d[3] = v[u].w;
+        }
+      }
+    }
+  };
+  auto compute = [&]() {
+#pragma unroll
+    for (int st = 0; st < KCH / 16; ++st) {  // k = kc0 + r + 8*(2*st + h)
+      const int kk = r + 8 * (2 * st + h);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[l31 * KP + kk], lds[(32 + l31) * KP + kk],
+                                                 acc, 0, 0, 0);
+    }
+  };
+  const int64_t nch = (I + KCH - 1) / KCH;
+  float4 r0[UV], r1[UV];
+  load(0, r0);
+  if (nch > 1) load(KCH, r1);
+  for (int64_t c = 0; c < nch; c += 2) {
+    store(r0);
+    __syncthreads();
+    if (c + 2 < nch) load((c + 2) * KCH, r0);
+    compute();
+    __syncthreads();
+    if (c + 1 < nch) {
+      store(r1);
+      __syncthreads();
+      if (c + 3 < nch) load((c + 3) * KCH, r1);
+      compute();
+      __syncthreads();
+    }
+  }
+  for (int e = 0; e < 16; ++e) {
+    const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
+    if (m < B && n < O) part[(r * B + m) * O + n] = acc[e];
+  }
+}
+
+// dW0 += delta0^T . X (TN, k over the batch) and TConnectedLayer.update's
+// weight part, one 32x32 tile per wave (delta0 is final once the fused
+// kernel has ended)
+__global__ __launch_bounds__(64) void mlp_l0_dw_kernel(const float* delta, const float* X,
+                                                       float* dW, float* W, int64_t B, int64_t O,
+                                                       int64_t I, float lrb, float wdec,
+                                                       float momentum) {
+  const int lane = threadIdx.x;
+  const int tni = (int)((I + 31) / 32);
+  const int64_t m0 = (int64_t)(blockIdx.x / tni) * 32, n0 = (int64_t)(blockIdx.x % tni) * 32;
+  floatx16 acc;
+  float wv[16];
+  dw_task(delta, m0, n0, B, O, I, X, dW, W, true, acc, wv, lane);
+  dw_store(m0, n0, O, I, dW, W, true, acc, wv, lrb, wdec, momentum, lane);
+}
+
 }  // namespace
 
 int64_t mlp_buffer_floats(int nlayers, const int64_t* widths, int bn, int64_t B) {
@@ -912,10 +1040,31 @@ hipError_t launch_mlp_train_step(const MlpArgs& args, hipStream_t s) {
     if (e2 != hipSuccess) return e2;
     if (e5 != hipSuccess) return e5;
   }
+  // layer 0: forward partials over several CUs, then the fused step, then
+  // layer 0's dW + weight update over several CUs
+  const int64_t B0 = a.batch, I0 = a.widths[0], O0 = a.widths[1];
+  if (!a.l0part) return hipErrorInvalidValue;
+  const float* W0 = a.buf + a.off[0][F_W];
+  const bool vec0 = I0 % 4 == 0 && ((reinterpret_cast<uintptr_t>(a.X) |
+                                     reinterpret_cast<uintptr_t>(W0)) & 15) == 0;
+  const unsigned fblocks = (unsigned)(2 * ((B0 + 31) / 32) * ((O0 + 31) / 32));
+  if (vec0)
+    hipLaunchKernelGGL((mlp_l0_forward_kernel<128, 4>), dim3(fblocks), dim3(256), 0, s, a.X, W0,
+                       B0, O0, I0, a.l0part);
+  else
+    hipLaunchKernelGGL((mlp_l0_forward_kernel<64, 1>), dim3(fblocks), dim3(256), 0, s, a.X, W0,
+                       B0, O0, I0, a.l0part);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   if (blk <= 2 * NT)
     hipLaunchKernelGGL(mlp_train_kernel<2>, dim3(1), dim3(NT), lds, s, a);
   else
     hipLaunchKernelGGL(mlp_train_kernel<5>, dim3(1), dim3(NT), lds, s, a);
+  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  const unsigned dblocks = (unsigned)(((O0 + 31) / 32) * ((I0 + 31) / 32));
+  hipLaunchKernelGGL(mlp_l0_dw_kernel, dim3(dblocks), dim3(64), 0, s,
+                     a.buf + a.off[0][F_DELTA], a.X, a.buf + a.off[0][F_DW],
+                     a.buf + a.off[0][F_W], B0, O0, I0, a.lr / (float)B0,
+                     -a.decay * (float)B0, a.momentum);
   return hipGetLastError();
 }
 

@@ -77,7 +77,8 @@ struct tns_ctx {
 
 namespace {
 
-enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5 };
+enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5,
+       SLOT_MLP = 6 };
 
 int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   if (elems < 1) elems = 1;
@@ -1069,6 +1070,9 @@ int tns_hip_mlp_train_step(tns_ctx* c, int32_t nlayers, const int64_t* widths,
   a.decay = decay;
   a.buf = buf;
   a.cost = cost;
+  // layer 0's residue partials (8 x batch x widths[1]), handed from the
+  // layer-0 forward launch to the fused one
+  if (int r = ensure_scratch(c, SLOT_MLP, 8 * batch * widths[1], &a.l0part)) return r;
   return hip_status(launch_mlp_train_step(a, c->stream), "mlp_train_step");
 }
 

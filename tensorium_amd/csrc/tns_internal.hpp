@@ -228,6 +228,7 @@ struct MlpArgs {
   int64_t stamp_off;  // end of the packed buffer (diagnostic stamp builds only)
   int lds_chunks;     // forward gemm operands staged through LDS in k-chunks
   int64_t act_off;    // LDS float offset of the stage-to-stage [B][O_max] block
+  float* l0part;      // layer 0's residue partials [8][B][O0] (mlp_l0_forward_kernel)
 };
 int64_t mlp_buffer_floats(int nlayers, const int64_t* widths, int bn, int64_t batch);
 hipError_t launch_mlp_train_step(const MlpArgs& a, hipStream_t s);
