@@ -352,7 +352,9 @@ int tns_hip_conv2d(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
  *   TNS_CONV_FUSED    (1) library's choice among the two below
  *   TNS_CONV_IM2COL   (2) im2col into workspace + SGEMM with bias+act epilogue
  *   TNS_CONV_IMPLICIT (3) implicit GEMM: the SGEMM gathers its B tiles from
- *                         the image (no col matrix, workspace unused) */
+ *                         the image (no col matrix, workspace unused); a
+ *                         3-channel 3x3 layer with 16 or 32 filters runs the
+ *                         direct kernel instead (same fmaf chains) */
 enum { TNS_CONV_UNFUSED = 0, TNS_CONV_FUSED = 1, TNS_CONV_IM2COL = 2, TNS_CONV_IMPLICIT = 3 };
 int tns_hip_conv_forward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
                          const float* input, const float* weights, const float* biases,

@@ -18,7 +18,8 @@
 //     — one ds_read_b128 per MFMA step instead of four ds_read_b32 — and
 //     XOR-swizzled by k/4 so the transposing ds_write_b32 are conflict-free
 //     (staging lanes cover rows m, m+32, m+64, m+96 of 8 k-quads);
-//   * fragments of step s+1 are read before step s's MFMAs are issued;
+//   * fragments of step s+1 are read before step s's MFMAs are issued
+//     (pinned there by scheduling fences);
 //   * interior-only addressing: no bounds tests, no zero page in the loop.
 #include <type_traits>
 
@@ -232,13 +233,39 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
       // next to their mid-tile use otherwise, exposing their latency)
       __builtin_amdgcn_sched_barrier(0);
     }
+#ifdef TNS_NB_D2  // (experiment: fragments two steps ahead, ring of three)
+    float fa[3][TM], fb[3][TN];
+    frag(cur, 0, fa[0], fb[0]);
+    frag(cur, 1, fa[1], fb[1]);
+#pragma unroll
+    for (int s = 0; s < BK / 2; ++s) {
+      if (s + 2 < BK / 2) frag(cur, s + 2, fa[(s + 2) % 3], fb[(s + 2) % 3]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (more)
+        if (s == BK / 4 - 1) {
+#ifndef TNS_NB_NO_AST
+          store_a(nxt);
+#endif
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      mma(fa[s % 3], fb[s % 3]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (false)
+#endif
+    {
     float a0[TM], b0[TN], a1[TM], b1[TN];
     frag(cur, 0, a0, b0);
 #pragma unroll
     for (int s = 0; s < BK / 2; s += 2) {
+      // (scheduling fences: hipcc otherwise sinks each fragment read next to
+      // its MFMAs and waits on it there; fenced, a step's reads are in flight
+      // behind the previous step's 8 MFMAs — 4096^3 1.000 -> 0.996 ms)
       frag(cur, s + 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
       mma(a0, b0);
       if (s + 2 < BK / 2) frag(cur, s + 2, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
       if constexpr (more)
         if (s == BK / 4 - 2) {  // mid-tile: A of tile t+1 (its loads' first use)
           __builtin_amdgcn_sched_barrier(0);
@@ -247,6 +274,7 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
 #endif
         }
       mma(a1, b1);
+    }
     }
     if constexpr (more) {
 #ifndef TNS_NB_NO_BAR

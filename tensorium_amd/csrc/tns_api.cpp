@@ -1168,6 +1168,15 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
     // implicit GEMM: batch folded into N, B gathered from zero-padded images
     if (!input || !weights || !out || (bias_act && !biases))
       return set_error(TNS_ERR_ARG, "conv_forward: null operand");
+    // short-k first layers (3-channel 3x3): the direct kernel, one HBM pass
+    // (TNS_OPT_CONV_VARIANT >= 0 forces a GEMM tile instead)
+    if (g_conv_variant < 0 && conv_direct_applies(C, kSize, filters)) {
+      OpTimer t(c, TNS_OP_GEMM);
+      return hip_status(launch_conv_direct(input, weights, bias_act ? biases : nullptr, out, batch,
+                                           C, H, W, filters, kSize, stride, padding, dilation, oh,
+                                           ow, activation, c->stream),
+                        "direct conv launch");
+    }
     // plane-sized tiles with a bounds-checked gather from the unpadded
     // images (conv_tile.hip) where they apply; TNS_OPT_CONV_VARIANT >= 100
     // forces tile 100 + v, 0..99 the sgemm_kernel.hpp shapes

@@ -108,6 +108,13 @@ int conv_tile_count();
 const char* conv_tile_name(int v);
 int conv_tile_pick(const GemmArgs& a, int ks);
 hipError_t launch_conv_tile(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
+// direct convolution (conv_direct.hip) for 3-channel 3x3 layers with 16 or
+// 32 filters: bias (nullable: raw output) + activation fused
+bool conv_direct_applies(int64_t C, int64_t ks, int64_t filters);
+hipError_t launch_conv_direct(const float* in, const float* w, const float* bias, float* out,
+                              int64_t batch, int64_t C, int64_t H, int64_t W, int64_t filters,
+                              int64_t ks, int64_t stride, int64_t pad, int64_t dil, int64_t oh,
+                              int64_t ow, int act, hipStream_t s);
 // k-table of an implicit-GEMM convolution over stored Hs x Ws images (padded
 // or not): K = C*kH*kW entries plus KTAB_PAD sentinels
 constexpr int KTAB_PAD = 256;

@@ -112,6 +112,23 @@ def test_conv_implicit_dilation(hip, torch_cuda, ora, pad):
         hip.setConvPad(-1)
 
 
+# direct kernel (conv_direct.hip): 3-channel 3x3 layers with 16 or 32
+# filters — ragged pixel counts, strides, paddings beyond the window,
+# dilation, every activation form (logistic/tanh evaluated in the kernel)
+DIRECT_CASES = [(2, 3, 17, 32, 3, 1, 1, 9, 1), (3, 3, 12, 16, 3, 2, 1, 0, 1),
+                (1, 3, 30, 32, 3, 1, 2, 6, 2), (2, 3, 9, 16, 3, 1, 0, 1, 1),
+                (1, 3, 40, 32, 3, 2, 0, 4, 1), (1, 3, 33, 32, 3, 1, 3, 13, 2)]
+
+
+@pytest.mark.parametrize("fused", [1, 3])
+@pytest.mark.parametrize("case", DIRECT_CASES)
+def test_conv_direct_bit_exact(hip, torch_cuda, ora, fused, case):
+    batch, C, H, F, k, s, p, act, dil = case
+    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, fused, seed=5,
+                         dil=dil)
+    assert np.array_equal(got, ref), case
+
+
 @pytest.mark.parametrize("idx", [0, 1, 2, 11, 62, 74])
 def test_yolov3_layers_batch8_implicit(hip, torch_cuda, ora, idx):
     from tensorium_amd.yolo import yolov3_conv_table
