@@ -23,8 +23,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--pad", type=int, default=-1, help="TNS_OPT_CONV_PAD (-1: heuristic)")
     a = ap.parse_args()
     hip = TNNHip(0)
+    hip.setConvPad(a.pad)
     rows, total = [], 0.0
     for s in yolov3_conv_table():
         x = torch.rand(a.batch, s.c, s.h, s.h, device="cuda")

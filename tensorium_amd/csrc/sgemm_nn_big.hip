@@ -30,13 +30,13 @@ namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 32;
-
 // BM x BN block tile, WM x WN waves (wave tile WTM x WTN = TM x TN 32x32
-// accumulators), MINB blocks per CU
-template <int BM, int BN, int WM, int WN, int MINB>
+// accumulators), MINB blocks per CU, k-tiles of BK (32, or 16 where two
+// blocks share a CU: two LDS stages of each fit beside the other's)
+template <int BM, int BN, int WM, int WN, int MINB, int BK = 32>
 struct Geo {
-  static constexpr int BM_ = BM, BN_ = BN, WN_ = WN, MINB_ = MINB;
+  static constexpr int BM_ = BM, BN_ = BN, WN_ = WN, MINB_ = MINB, BK_ = BK;
+  static constexpr int KQ = BK / 4;                 // k-quads per tile row
   static constexpr int NT = 64 * WM * WN;
   static constexpr int WTM = BM / WM, WTN = BN / WN;
   static constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -49,6 +49,7 @@ struct Geo {
   static_assert(TM == 2 || TM == 4, "A fragments read as one b64 / b128");
   static_assert(BN == 128 || BN == 256, "B rows of 512 B or 1 KB per DMA");
   static_assert(AU >= 1 && BDMA >= 1 && BM * BK / 4 % NT == 0, "staging split");
+  static_assert(BK == 16 || BK == 32, "k-quad swizzle over at most 8 quads");
 };
 
 template <class G>
@@ -56,7 +57,12 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
   constexpr int BM = G::BM_, BN = G::BN_, NT = G::NT, WN = G::WN_;
   constexpr int WTM = G::WTM, WTN = G::WTN, TM = G::TM, TN = G::TN;
   constexpr int LDA = G::LDA, LDB = G::LDB, A_TILE = G::A_TILE, STAGE = G::STAGE;
-  constexpr int AU = G::AU;
+  constexpr int AU = G::AU, BK = G::BK_, KQ = G::KQ;
+  // column swizzle of k-quad kq: a wave's staging lanes cover 64/KQ
+  // consecutive columns of each of the KQ quads; XOR with kq << SW moves
+  // each quad's columns to their own bank range (KQ = 8: the 4-column
+  // rotation; KQ = 4: 16-column blocks)
+  constexpr int SW = KQ == 8 ? 2 : 4;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int lc = lane & 31, h = lane >> 5;
   const int wm = wid / WN, wn = wid % WN;
@@ -130,10 +136,10 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
 #pragma unroll
   for (int u = 0; u < AU; ++u) {
     const int idx = tid + NT * u;
-    const int kq = idx & 7, mm = idx >> 3;
+    const int kq = idx % KQ, mm = idx / KQ;
     const int m = (mm & ~(WTM - 1)) | ((mm % TM) << 5) | ((mm & (WTM - 1)) / TM);
     a_src[u] = A + (m0 + m) * lda + 4 * kq;
-    a_dst[u] = (4 * kq) * LDA + (mm ^ (kq << 2));  // element c adds c*LDA
+    a_dst[u] = (4 * kq) * LDA + (mm ^ (kq << SW));  // element c adds c*LDA
   }
   float4 ra[AU];
   const float alpha = p.alpha;
@@ -185,7 +191,7 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
     (void)st; (void)k;
     return;
 #endif
-    const float* ap = st + k * LDA + (a_frag ^ (((k >> 2) & 7) << 2));
+    const float* ap = st + k * LDA + (a_frag ^ (((k >> 2) & (KQ - 1)) << SW));
     if constexpr (TM == 4) {
       const float4 v = *reinterpret_cast<const float4*>(ap);
       a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
@@ -233,27 +239,6 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
       // next to their mid-tile use otherwise, exposing their latency)
       __builtin_amdgcn_sched_barrier(0);
     }
-#ifdef TNS_NB_D2  // (experiment: fragments two steps ahead, ring of three)
-    float fa[3][TM], fb[3][TN];
-    frag(cur, 0, fa[0], fb[0]);
-    frag(cur, 1, fa[1], fb[1]);
-#pragma unroll
-    for (int s = 0; s < BK / 2; ++s) {
-      if (s + 2 < BK / 2) frag(cur, s + 2, fa[(s + 2) % 3], fb[(s + 2) % 3]);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (more)
-        if (s == BK / 4 - 1) {
-#ifndef TNS_NB_NO_AST
-          store_a(nxt);
-#endif
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      mma(fa[s % 3], fb[s % 3]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (false)
-#endif
-    {
     float a0[TM], b0[TN], a1[TM], b1[TN];
     frag(cur, 0, a0, b0);
 #pragma unroll
@@ -274,7 +259,6 @@ __global__ __launch_bounds__(G::NT, G::MINB_) void sgemm_nn_big_kernel(GemmArgs 
 #endif
         }
       mma(a1, b1);
-    }
     }
     if constexpr (more) {
 #ifndef TNS_NB_NO_BAR
@@ -303,11 +287,14 @@ using G256 = Geo<256, 256, 2, 4, 1>;  // 8 waves, wave tile 128x64, 1 block/CU
 using G128 = Geo<128, 128, 2, 2, 2>;  // 4 waves, wave tile 64x64, 2 blocks/CU
 using G256x128 = Geo<256, 128, 2, 2, 1>;  // 4 waves, wave tile 128x64
 using G256w16 = Geo<256, 256, 4, 4, 1>;   // 16 waves, wave tile 64x64, 4 waves per SIMD
+// 4 waves, wave tile 128x64, k-tiles of 16: two blocks per CU (2 x 48 KB of
+// LDS), so one block's barrier and staging are covered by the other's MFMAs
+using G256x128k16 = Geo<256, 128, 2, 2, 2, 16>;
 
 template <class G>
 bool applies(const GemmArgs& a) {
   if (a.conv || a.epi != EPI_NONE || a.beta_mode == BETA_STORE) return false;
-  if (a.M % G::BM_ || a.N % G::BN_ || a.K % BK || a.M <= 0 || a.N <= 0) return false;
+  if (a.M % G::BM_ || a.N % G::BN_ || a.K % G::BK_ || a.M <= 0 || a.N <= 0) return false;
   if (a.lda % 4 || a.ldb % 4 || !aligned16(a.A) || !aligned16(a.B)) return false;
   if (a.batch > 1 && (a.strideA % 4 || a.strideB % 4)) return false;
   return (a.M / G::BM_) * (a.N / G::BN_) <= 0x7fffffff;
@@ -336,11 +323,12 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 
 // (a 4-wave 256x256 form, wave tile 128x128 at one wave per SIMD, spills 67
 // registers at the 512 cap — not instantiated)
-int sgemm_nn_big_count() { return 4; }
+int sgemm_nn_big_count() { return 5; }
 const char* sgemm_nn_big_name(int v) {
   static const char* names[] = {"256x256x32_w2x4_nn_big", "128x128x32_w2x2_nn_big",
-                                "256x128x32_w2x2_nn_big", "256x256x32_w4x4_nn_big"};
-  return v >= 0 && v < 4 ? names[v] : "";
+                                "256x128x32_w2x2_nn_big", "256x256x32_w4x4_nn_big",
+                                "256x128x16_w2x2_b2_nn_big"};
+  return v >= 0 && v < 5 ? names[v] : "";
 }
 
 // heuristic: the 256x256 form when it gives about a block per CU
@@ -355,6 +343,7 @@ hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s) {
     case 1: return launch<G128>(a, s);
     case 2: return launch<G256x128>(a, s);
     case 3: return launch<G256w16>(a, s);
+    case 4: return launch<G256x128k16>(a, s);
     default: return hipErrorInvalidValue;
   }
 }
