@@ -43,9 +43,19 @@ def main():
         run_dw()
         gw = hip.opMs(TNS_OP_GEMM)
         hip.setTelemetry(False)
+        # whole backward call (derive, bias sums, im2col, dW incl. any
+        # accumulate pass, dX, col2im) by HIP events
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        call_ms = e0.elapsed_time(e1) / 5
         out.append({"layer": s.index, "shape": f"{s.c}x{s.h} k{s.size}s{s.stride}->{s.filters}",
                     "gemm_ms": round(g, 3), "dw_ms": round(gw, 3), "dx_ms": round(g - gw, 3), "tf": round(2 * s.flops * batch / g / 1e9, 1),
-                    "im2col_ms": round(i, 3), "col2im_ms": round(c, 3)})
+                    "im2col_ms": round(i, 3), "col2im_ms": round(c, 3),
+                    "call_ms": round(call_ms, 4)})
     print(json.dumps(out))
 
 
