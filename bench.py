@@ -524,7 +524,7 @@ def bench_mnist(torch, hip, ctx, steps=200):
     wall = ctx.max((time.perf_counter() - t0) / steps)
     return {"batch": B, "net": "784-64-64-64-64-32-10 relu/linear + BN + softmax",
             "us_per_step": round(wall * 1e6, 2), "steps_per_s_total": round(ctx.world / wall, 1),
-            "kernels_per_step": 1, "cost_after": round(float(cost.item()), 4)}
+            "kernels_per_step": 3, "cost_after": round(float(cost.item()), 4)}
 
 
 def cpu_baseline(n, target_s):
