@@ -474,10 +474,16 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * TNS_OPT_SDOT_FORM (default -1 = by shape): kernel of the sdot-order NT
  * product (tuning / tests; same result bit for bit): 0 = the MFMA kernel
  * (one wave per residue class), 1 + v = VALU chain kernel variant v (one
- * lane per few residue chains, for few outputs over a long k). */
+ * lane per few residue chains, for few outputs over a long k).
+ * TNS_OPT_DX_FUSED (default 1): the conv backward's state.delta of stride-1,
+ * dilation-1 layers with >= 8192 pixels per image by one kernel that runs
+ * each window tap's filter chain and adds it to the image pixel in scol2im's
+ * order (no col matrix); 2 = that kernel on every stride-1 layer it fits;
+ * 0 = the reference's two stages, TN GEMM into the workspace + col2im (same
+ * bits in all three). */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
-       TNS_OPT_SDOT_FORM = 6 };
+       TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

@@ -17,7 +17,12 @@ from tensorium_amd._abi import TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM  # noqa
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dx-fused", type=int, default=1, help="TNS_OPT_DX_FUSED")
+    a = ap.parse_args()
     hip = TNNHip(0)
+    hip.setDxFused(a.dx_fused)
     batch = 8
     out = []
     for s in yolov3_conv_table():

@@ -31,6 +31,7 @@ TNS_OPT_STRICT_BETA0 = 0
 TNS_OPT_CONV_VARIANT, TNS_OPT_CONV_PAD, TNS_OPT_NT_SDOT, TNS_OPT_SRSS_QUIRK = 1, 2, 3, 4
 TNS_OPT_TT_EXACT = 5
 TNS_OPT_SDOT_FORM = 6
+TNS_OPT_DX_FUSED = 7
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 

@@ -30,6 +30,7 @@ static thread_local std::string g_err;
 static tns_error_hook_t g_hook = nullptr;
 static int64_t g_strict_beta0 = 1;
 static int64_t g_nt_sdot = 1;
+static int64_t g_dx_fused = 1;
 static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
@@ -78,7 +79,7 @@ struct tns_ctx {
 namespace {
 
 enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5,
-       SLOT_MLP = 6 };
+       SLOT_MLP = 6, SLOT_WT = 7 };
 
 int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   if (elems < 1) elems = 1;
@@ -513,6 +514,9 @@ int tns_set_option(int32_t opt, int64_t value) {
       if (value > sdot_chains_variant_count())
         return set_error(TNS_ERR_ARG, "sdot form %lld out of range", (long long)value);
       set_sdot_form((int)value);
+      return TNS_OK;
+    case TNS_OPT_DX_FUSED:
+      g_dx_fused = value < 0 ? 1 : (value > 2 ? 2 : value);
       return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
@@ -1444,8 +1448,13 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   }
   // state.input.im2Col(...) — a 1x1/s1/p0 col matrix is the input itself
   const bool needs_col = kSize != 1 || stride != 1 || padding != 0 || dilation != 1;
+  // state.delta of stride-1 layers without the col matrix (conv_dx.hip)
+  const bool fused_dx =
+      state_delta && dilation == 1 &&
+      ((g_dx_fused == 1 && conv_dx_fused_applies(C, H, W, stride, filters, g.oh, g.ow)) ||
+       (g_dx_fused == 2 && conv_dx_fused_fits(C, H, W, stride, filters, g.oh, g.ow)));
   float* ws = workspace;
-  if (!ws && (needs_col || state_delta))
+  if (!ws && (needs_col || (state_delta && !fused_dx)))
     if (int r = ensure_scratch(c, 0, batch * colSize, &ws)) return r;
   const float* col = input;
   if (needs_col) {
@@ -1487,6 +1496,18 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
         return r;
   }
   if (!state_delta) return TNS_OK;
+  if (fused_dx) {
+    // per image pixel: each window tap's ascending-f chain, added to the
+    // pixel in (kr, kc) order for the taps scol2im does not skip — the same
+    // roundings as the two stages below (646-660)
+    float* wt = nullptr;
+    if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
+    OpTimer t(c, TNS_OP_GEMM);
+    return hip_status(launch_conv_dx_col2im(weights, wt, delta, state_delta, batch, C, H, W,
+                                            filters, kSize, padding, dilation, g.oh, g.ow,
+                                            c->stream),
+                      "fused dX + col2im launch");
+  }
   // col_b = W^T . delta_b (TN strided batched, weights shared, beta = 0 into
   // the workspace), then col2im accumulates into state.delta (646-660)
   if (int r = do_gemm(c, true, false, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,

@@ -299,6 +299,13 @@ class TNNHip:
         kernel, 1 + v VALU chain variant v (bit-identical); process-wide."""
         check(self.lib.tns_set_option(6, int(form)))
 
+    def setDxFused(self, mode: int = 1):
+        """Conv backward state.delta of stride-1 layers: 1 one kernel (each
+        tap's filter chain added to the pixel in scol2im's order, no col
+        matrix) on the large planes where it is faster, 2 on every layer it
+        fits, 0 the reference's TN GEMM + col2im (bit-identical); process-wide."""
+        check(self.lib.tns_set_option(7, int(mode)))
+
     def convTileVariants(self) -> int:
         """Plane-sized implicit-conv tiles (setConvVariant(100 + v))."""
         return int(self.lib.tns_conv_tile_variant_count())

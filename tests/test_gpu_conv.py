@@ -192,6 +192,44 @@ def test_conv_backward_yolov3_batch8(hip, torch_cuda, ora, idx):
     assert np.array_equal(dbu.cpu().numpy(), rbu)
 
 
+@pytest.mark.parametrize("fused", [2, 0])
+@pytest.mark.parametrize("batch,C,H,F,k,s,p,act", [
+    (2, 8, 17, 12, 3, 1, 1, 9), (3, 64, 13, 100, 3, 1, 1, 1), (2, 68, 9, 40, 1, 1, 0, 4),
+    (1, 32, 20, 16, 5, 1, 2, 9), (2, 16, 11, 24, 3, 1, 0, 9), (1, 132, 7, 65, 3, 1, 1, 0),
+    (8, 512, 13, 1024, 3, 1, 1, 9), (8, 128, 52, 256, 3, 1, 1, 9), (8, 32, 208, 64, 3, 1, 1, 9)])
+def test_conv_backward_state_delta_fused(hip, torch_cuda, ora, fused, batch, C, H, F, k, s, p,
+                                         act):
+    """state.delta of stride-1 layers: one kernel running each window tap's
+    filter chain and adding it to the pixel in scol2im's order (no col
+    matrix) and the reference's TN GEMM + col2im — both bit-exact: ragged
+    channel / filter / pixel tiles, 1x1, 5x5, padding 0 (taps skipped at
+    the border), YOLOv3 13x13 and 52x52 shapes at batch 8."""
+    rng = np.random.default_rng(C * 7 + F + H)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.3, 0.3, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    sd0 = rng.uniform(-1, 1, x.shape).astype(np.float32)
+    sd0[0, 0, 0, :2] = -0.0  # a pixel whose every skipped tap must stay skipped
+    rd, rbu, rwu, rsd = d0.copy(), bu0.copy(), wu0.copy(), sd0.copy()
+    ora.conv_backward(x, w, F, k, s, p, act, out, rd, rbu, rwu, rsd)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    dx, dw, dout, dd, dbu, dwu, dsd = map(t, (x, w, out, d0, bu0, wu0, sd0))
+    hip.setDxFused(fused)
+    try:
+        hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, act, dout, dd, dbu, dwu, None,
+                         dsd)
+        hip.finish()
+    finally:
+        hip.setDxFused(1)
+    assert np.array_equal(dsd.cpu().numpy(), rsd)
+    assert np.array_equal(dwu.cpu().numpy(), rwu)
+    assert np.array_equal(dd.cpu().numpy(), rd)
+
+
 def _t(torch, a):
     return torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()
 
