@@ -28,8 +28,13 @@ namespace tns {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-constexpr int NT = 1024;
+#ifndef TNS_MLP_NT
+#define TNS_MLP_NT 1024
+#endif
+constexpr int NT = TNS_MLP_NT;  // (512: diagnostic builds, 256 VGPRs per thread)
 constexpr int NWAVES = NT / 64;
+// element slots per thread of the [B][O] passes: the two kernel instances
+constexpr int EPT_S = 2048 / NT, EPT_L = 5120 / NT;
 constexpr int KC = 128;  // largest k-chunk of the LDS-staged forward gemm
 
 // Diagnostic build only (-DTNS_MLP_STAMPS, scripts/mlp_stamps.py): thread 0
@@ -1031,10 +1036,10 @@ hipError_t launch_mlp_train_step(const MlpArgs& args, hipStream_t s) {
   const size_t lds = (size_t)(act_off + blk) * sizeof(float);
   if (act_off + blk > LDS_FLOATS) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
-    const hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<2>),
+    const hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<EPT_S>),
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)lds);
-    const hipError_t e5 = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<5>),
+    const hipError_t e5 = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_train_kernel<EPT_L>),
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)lds);
     if (e2 != hipSuccess) return e2;
@@ -1055,10 +1060,10 @@ hipError_t launch_mlp_train_step(const MlpArgs& args, hipStream_t s) {
     hipLaunchKernelGGL((mlp_l0_forward_kernel<64, 1>), dim3(fblocks), dim3(256), 0, s, a.X, W0,
                        B0, O0, I0, a.l0part);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  if (blk <= 2 * NT)
-    hipLaunchKernelGGL(mlp_train_kernel<2>, dim3(1), dim3(NT), lds, s, a);
+  if (blk <= EPT_S * NT)
+    hipLaunchKernelGGL(mlp_train_kernel<EPT_S>, dim3(1), dim3(NT), lds, s, a);
   else
-    hipLaunchKernelGGL(mlp_train_kernel<5>, dim3(1), dim3(NT), lds, s, a);
+    hipLaunchKernelGGL(mlp_train_kernel<EPT_L>, dim3(1), dim3(NT), lds, s, a);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   const unsigned dblocks = (unsigned)(((O0 + 31) / 32) * ((I0 + 31) / 32));
   hipLaunchKernelGGL(mlp_l0_dw_kernel, dim3(dblocks), dim3(64), 0, s,
