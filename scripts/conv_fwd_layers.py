@@ -24,11 +24,17 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--pad", type=int, default=-1, help="TNS_OPT_CONV_PAD (-1: heuristic)")
+    ap.add_argument("--variant", type=int, default=-1, help="TNS_OPT_CONV_VARIANT (-1: heuristic)")
+    ap.add_argument("--layers", default="", help="comma-separated layer indices (default: all)")
     a = ap.parse_args()
     hip = TNNHip(0)
     hip.setConvPad(a.pad)
+    hip.setConvVariant(a.variant)
+    only = {int(v) for v in a.layers.split(",") if v}
     rows, total = [], 0.0
     for s in yolov3_conv_table():
+        if only and s.index not in only:
+            continue
         x = torch.rand(a.batch, s.c, s.h, s.h, device="cuda")
         w = torch.rand(s.filters, s.K, device="cuda") * 0.2 - 0.1
         b = torch.rand(s.filters, device="cuda") * 0.2 - 0.1
