@@ -521,6 +521,155 @@ __global__ __launch_bounds__(TPB) void bn_apply_k(const float* y,  // may alias 
   }
 }
 
+// ---- row form of the per-channel elementwise passes ------------------------
+// A workgroup owns a segment of one (group, channel) row of bs contiguous
+// elements, so the channel's constants are read once per workgroup and no
+// element pays the 64-bit (e / bs) % N of the grid-stride forms — that integer
+// division, not HBM, bounded them on the conv shapes (normalizeDelta 3.6 TB/s
+// at 8 x 32 x 173056).  Same per-element arithmetic, same order.  V = 4 on
+// 16-byte aligned rows with bs % 4 == 0.
+constexpr int RU = 4;  // vectors per thread
+
+__device__ __forceinline__ void row_of(int bpr, int64_t N, int64_t& row, int64_t& ch, int& seg) {
+  row = (int64_t)(blockIdx.x / (unsigned)bpr);
+  seg = (int)(blockIdx.x - (unsigned)row * (unsigned)bpr);
+  ch = row % N;
+}
+
+template <int V>
+__device__ __forceinline__ void ld(const float* p, float (&v)[V]) {
+  if constexpr (V == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = *p;
+  }
+}
+template <int V>
+__device__ __forceinline__ void st(float* p, const float (&v)[V]) {
+  if constexpr (V == 4)
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  else
+    *p = v[0];
+}
+
+template <int V>
+__global__ __launch_bounds__(TPB) void normalize_delta_rows(
+    const float* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ var,
+    const float* __restrict__ mean_delta, const float* __restrict__ var_delta,
+    float* __restrict__ delta, int64_t N, int64_t bs, int bpr, float B) {
+  int64_t row, i;
+  int seg;
+  row_of(bpr, N, row, i, seg);
+  const float md = mean_delta[i] / B;
+  const float vd = 2.0f * var_delta[i] / B;
+  const float ve = var[i] > SEPS ? var[i] : SEPS;
+  const float sd = sqrtf(ve);
+  const float m = mean[i];
+  const int64_t base = row * bs;
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int64_t j = ((int64_t)seg * RU * TPB + u * TPB + threadIdx.x) * V;
+    if (j >= bs) break;
+    float d[V], xv[V];
+    ld<V>(delta + base + j, d);
+    ld<V>(x + base + j, xv);
+#pragma unroll
+    for (int c = 0; c < V; ++c) {
+      const float a = d[c] / sd;
+      const float t = (xv[c] - m) * vd + md;  // sNormalizeDelta_avx order
+      d[c] = a + t;
+    }
+    st<V>(delta + base + j, d);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(TPB) void scale_add_rows(float* __restrict__ x, int64_t N, int64_t bs,
+                                                      int bpr, const float* __restrict__ scales,
+                                                      const float* __restrict__ biases,
+                                                      int64_t incb) {
+  int64_t row, i;
+  int seg;
+  row_of(bpr, N, row, i, seg);
+  const float sc = scales[i * incb];
+  const float bi = biases ? biases[i * incb] : 0.0f;
+  const int64_t base = row * bs;
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int64_t j = ((int64_t)seg * RU * TPB + u * TPB + threadIdx.x) * V;
+    if (j >= bs) break;
+    float v[V];
+    ld<V>(x + base + j, v);
+#pragma unroll
+    for (int c = 0; c < V; ++c) {
+      v[c] = v[c] * sc;                // forwardScale (vsMulB)
+      if (biases) v[c] = v[c] + bi;    // forwardBias  (vsAddB)
+    }
+    st<V>(x + base + j, v);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(TPB) void normalize_rows(float* __restrict__ x, int64_t N, int64_t bs,
+                                                      int bpr, const float* __restrict__ means,
+                                                      int64_t mstride,
+                                                      const float* __restrict__ vars,
+                                                      int64_t vstride) {
+  int64_t row, i;
+  int seg;
+  row_of(bpr, N, row, i, seg);
+  const float m = means[i * mstride];
+  float sd = sqrtf(vars[i * vstride]);  // (bs > 1) _snormblkvv -> snormvss
+  sd = sd > SEPS ? sd : SEPS;
+  const int64_t base = row * bs;
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int64_t j = ((int64_t)seg * RU * TPB + u * TPB + threadIdx.x) * V;
+    if (j >= bs) break;
+    float v[V];
+    ld<V>(x + base + j, v);
+#pragma unroll
+    for (int c = 0; c < V; ++c) v[c] = (v[c] - m) / sd;
+    st<V>(x + base + j, v);
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(TPB) void bn_apply_rows(const float* y,  // may alias out
+                                                     float* __restrict__ x,
+                                                     float* __restrict__ xn, float* out,
+                                                     int64_t N, int64_t bs, int bpr,
+                                                     const float* __restrict__ means,
+                                                     const float* __restrict__ vars,
+                                                     const float* __restrict__ scales,
+                                                     const float* __restrict__ biases, int act) {
+  int64_t row, i;
+  int seg;
+  row_of(bpr, N, row, i, seg);
+  const float m = means[i], sc = scales[i], bi = biases[i];
+  float sd = sqrtf(vars[i]);
+  sd = sd > SEPS ? sd : SEPS;
+  const int64_t base = row * bs;
+#pragma unroll
+  for (int u = 0; u < RU; ++u) {
+    const int64_t j = ((int64_t)seg * RU * TPB + u * TPB + threadIdx.x) * V;
+    if (j >= bs) break;
+    float v[V], a[V], o[V];
+    ld<V>(y + base + j, v);
+#pragma unroll
+    for (int c = 0; c < V; ++c) {
+      a[c] = (v[c] - m) / sd;
+      float t = a[c] * sc;
+      t = t + bi;
+      o[c] = act_apply(t, act);
+    }
+    if (x) st<V>(x + base + j, v);
+    if (xn) st<V>(xn + base + j, a);
+    st<V>(out + base + j, o);
+  }
+}
+
 // rolling_mean.Multiply(1 - m); rolling_mean.axpy(m, mean) and the same for
 // the variance (nbaselayer.pas:353-356): one multiply, then one FMA
 __global__ void rolling_update_k(int64_t n, float* __restrict__ rm, float* __restrict__ rv,
@@ -534,6 +683,16 @@ __global__ void rolling_update_k(int64_t n, float* __restrict__ rm, float* __res
 
 }  // namespace
 
+// row form for blocks of >= 256 elements (the conv shapes); returns the
+// workgroups per row, 0 when the grid-stride form is used instead
+static int row_bpr(int64_t rows, int64_t bs, int V) {
+  if (bs < 256) return 0;
+  const int64_t span = (int64_t)TPB * RU * V;
+  const int64_t bpr = (bs + span - 1) / span;
+  return rows * bpr <= 0x7fffffffLL ? (int)bpr : 0;
+}
+static bool al16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
 hipError_t launch_bn_apply(const float* y, float* x, float* xn, float* out, int64_t groups,
                            int64_t N, int64_t bs, const float* means, const float* vars,
                            const float* scales, const float* biases, int act, hipStream_t s) {
@@ -541,6 +700,15 @@ hipError_t launch_bn_apply(const float* y, float* x, float* xn, float* out, int6
   if (total <= 0) return hipSuccess;
   const auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   const bool v4 = bs % 4 == 0 && al(y) && al(out) && (!x || al(x)) && (!xn || al(xn));
+  if (const int bpr = row_bpr(groups * N, bs, v4 ? 4 : 1)) {
+    if (v4)
+      hipLaunchKernelGGL(bn_apply_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s, y,
+                         x, xn, out, N, bs, bpr, means, vars, scales, biases, act);
+    else
+      hipLaunchKernelGGL(bn_apply_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s, y,
+                         x, xn, out, N, bs, bpr, means, vars, scales, biases, act);
+    return hipGetLastError();
+  }
   if (v4)
     hipLaunchKernelGGL(bn_apply_k<4>, dim3(nblk(total / 4)), dim3(TPB), 0, s, y, x, xn, out,
                        total / 4, N, bs, means, vars, scales, biases, act);
@@ -585,6 +753,16 @@ hipError_t launch_normalize(float* x, int64_t groups, int64_t N, int64_t bs, con
                             int64_t mstride, const float* vars, int64_t vstride, hipStream_t s) {
   const int64_t total = groups * N * bs;
   if (total <= 0) return hipSuccess;
+  const bool v4 = bs % 4 == 0 && al16(x);
+  if (const int bpr = row_bpr(groups * N, bs, v4 ? 4 : 1)) {
+    if (v4)
+      hipLaunchKernelGGL(normalize_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s, x,
+                         N, bs, bpr, means, mstride, vars, vstride);
+    else
+      hipLaunchKernelGGL(normalize_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s, x,
+                         N, bs, bpr, means, mstride, vars, vstride);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(normalize_k, dim3(nblk(total)), dim3(TPB), 0, s, x, total, N, bs, means,
                      mstride, vars, vstride);
   return hipGetLastError();
@@ -594,6 +772,16 @@ hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, con
                             const float* biases, int64_t incb, hipStream_t s) {
   const int64_t total = groups * N * bs;
   if (total <= 0) return hipSuccess;
+  const bool v4 = bs % 4 == 0 && al16(x);
+  if (const int bpr = row_bpr(groups * N, bs, v4 ? 4 : 1)) {
+    if (v4)
+      hipLaunchKernelGGL(scale_add_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s, x,
+                         N, bs, bpr, scales, biases, incb);
+    else
+      hipLaunchKernelGGL(scale_add_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s, x,
+                         N, bs, bpr, scales, biases, incb);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(scale_add_k, dim3(nblk(total)), dim3(TPB), 0, s, x, total, N, bs, scales,
                      biases, incb);
   return hipGetLastError();
@@ -648,6 +836,18 @@ hipError_t launch_normalize_delta(const float* x, const float* mean, const float
                                   int64_t groups, int64_t N, int64_t bs, hipStream_t s) {
   const int64_t total = groups * N * bs;
   if (total <= 0) return hipSuccess;
+  const bool v4 = bs % 4 == 0 && al16(x) && al16(delta);
+  if (const int bpr = row_bpr(groups * N, bs, v4 ? 4 : 1)) {
+    if (v4)
+      hipLaunchKernelGGL(normalize_delta_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
+                         s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
+                         (float)(groups * bs));
+    else
+      hipLaunchKernelGGL(normalize_delta_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
+                         s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
+                         (float)(groups * bs));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(normalize_delta_k, dim3(nblk(total)), dim3(TPB), 0, s, x, mean, var,
                      mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs));
   return hipGetLastError();

@@ -400,6 +400,42 @@ hipError_t launch_im2col(const ConvGeom& g, const float* im, int64_t imStride, f
   return hipSuccess;
 }
 
+namespace {
+// stride 1, 3x3 window: the nine taps' col entries are loaded together
+// (out-of-plane taps read entry 0 and are skipped below), then added to the
+// pixel in (kr, kc) order — the per-pixel order of col2im_fast_kernel, whose
+// tap loop with its early continues issued one dependent load at a time
+__global__ __launch_bounds__(256) void col2im_s1k3_kernel(C2IArgs a) {
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= (int)a.pixels) return;
+  const int64_t img = blockIdx.y;
+  const int rowi = pix / a.W, x = pix - rowi * a.W;
+  const int c = rowi / a.H, y = rowi - c * a.H;
+  float* __restrict__ im = a.im + img * a.imStride;
+  const float* __restrict__ col = a.col + img * a.colStride;
+  const int64_t ohw = (int64_t)a.oh * a.ow;
+  float v[9];
+  bool ok[9];
+#pragma unroll
+  for (int kr = 0; kr < 3; ++kr) {
+    const int ry = y - (kr - a.padH) * a.dY;  // the reference's dilation formula
+    const bool okr = (unsigned)ry < (unsigned)a.oh;
+#pragma unroll
+    for (int kc = 0; kc < 3; ++kc) {
+      const int rx = x - (kc - a.padW) * a.dX;
+      const int t = kr * 3 + kc;
+      ok[t] = okr && (unsigned)rx < (unsigned)a.ow;
+      v[t] = col[ok[t] ? (int64_t)(c * 9 + t) * ohw + ry * a.ow + rx : 0];
+    }
+  }
+  float acc = im[pix];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+    if (ok[t]) acc = acc + v[t];
+  im[pix] = acc;
+}
+}  // namespace
+
 hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride, float* im,
                          int64_t imStride, int64_t batch, hipStream_t s) {
   if (g.oh <= 0 || g.ow <= 0 || batch <= 0 || g.C <= 0) return hipSuccess;
@@ -416,7 +452,9 @@ hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride,
     sub.im = im + b0 * imStride;
     dim3 grid((unsigned)((a.pixels + 255) / 256), (unsigned)nb);
     if (a.pixels <= 0x7fffff00LL) {
-      if (g.sY == 1 && g.sX == 1)
+      if (g.sY == 1 && g.sX == 1 && g.kH == 3 && g.kW == 3)
+        hipLaunchKernelGGL(col2im_s1k3_kernel, grid, dim3(256), 0, s, sub);
+      else if (g.sY == 1 && g.sX == 1)
         hipLaunchKernelGGL(col2im_fast_kernel<1>, grid, dim3(256), 0, s, sub);
       else if (g.sY == 2 && g.sX == 2)
         hipLaunchKernelGGL(col2im_fast_kernel<2>, grid, dim3(256), 0, s, sub);
