@@ -401,16 +401,26 @@ hipError_t launch_im2col(const ConvGeom& g, const float* im, int64_t imStride, f
 }
 
 namespace {
-// stride 1, 3x3 window: the nine taps' col entries are loaded together
-// (out-of-plane taps read entry 0 and are skipped below), then added to the
-// pixel in (kr, kc) order — the per-pixel order of col2im_fast_kernel, whose
-// tap loop with its early continues issued one dependent load at a time
-__global__ __launch_bounds__(256) void col2im_s1k3_kernel(C2IArgs a) {
+// 3x3 window, stride S (1 or 2): the nine taps' col entries are loaded
+// together (taps outside the plane or off the stride grid read entry 0 and
+// are skipped below), then added to the pixel in (kr, kc) order — the
+// per-pixel order of col2im_fast_kernel, whose tap loop with its early
+// continues issued one dependent load at a time.  Stride 2 keeps that
+// kernel's lane order (the lanes of an image row take one column residue
+// class together, so a tap's valid lanes read consecutive col entries).
+template <int S>
+__global__ __launch_bounds__(256) void col2im_k3_kernel(C2IArgs a) {
   const int pix = blockIdx.x * 256 + threadIdx.x;
   if (pix >= (int)a.pixels) return;
   const int64_t img = blockIdx.y;
-  const int rowi = pix / a.W, x = pix - rowi * a.W;
+  const int rowi = pix / a.W, q = pix - rowi * a.W;
+  int x = q;
+  if constexpr (S == 2) {
+    const int w0 = (a.W + 1) / 2;  // columns of residue 0
+    x = q < w0 ? 2 * q : 1 + 2 * (q - w0);
+  }
   const int c = rowi / a.H, y = rowi - c * a.H;
+  const int at = pix - q + x;
   float* __restrict__ im = a.im + img * a.imStride;
   const float* __restrict__ col = a.col + img * a.colStride;
   const int64_t ohw = (int64_t)a.oh * a.ow;
@@ -419,20 +429,20 @@ __global__ __launch_bounds__(256) void col2im_s1k3_kernel(C2IArgs a) {
 #pragma unroll
   for (int kr = 0; kr < 3; ++kr) {
     const int ry = y - (kr - a.padH) * a.dY;  // the reference's dilation formula
-    const bool okr = (unsigned)ry < (unsigned)a.oh;
+    const bool okr = ry >= 0 && ry % S == 0 && ry / S < a.oh;
 #pragma unroll
     for (int kc = 0; kc < 3; ++kc) {
       const int rx = x - (kc - a.padW) * a.dX;
       const int t = kr * 3 + kc;
-      ok[t] = okr && (unsigned)rx < (unsigned)a.ow;
-      v[t] = col[ok[t] ? (int64_t)(c * 9 + t) * ohw + ry * a.ow + rx : 0];
+      ok[t] = okr && rx >= 0 && rx % S == 0 && rx / S < a.ow;
+      v[t] = col[ok[t] ? (int64_t)(c * 9 + t) * ohw + (ry / S) * a.ow + rx / S : 0];
     }
   }
-  float acc = im[pix];
+  float acc = im[at];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
     if (ok[t]) acc = acc + v[t];
-  im[pix] = acc;
+  im[at] = acc;
 }
 }  // namespace
 
@@ -453,7 +463,9 @@ hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride,
     dim3 grid((unsigned)((a.pixels + 255) / 256), (unsigned)nb);
     if (a.pixels <= 0x7fffff00LL) {
       if (g.sY == 1 && g.sX == 1 && g.kH == 3 && g.kW == 3)
-        hipLaunchKernelGGL(col2im_s1k3_kernel, grid, dim3(256), 0, s, sub);
+        hipLaunchKernelGGL(col2im_k3_kernel<1>, grid, dim3(256), 0, s, sub);
+      else if (g.sY == 2 && g.sX == 2 && g.kH == 3 && g.kW == 3)
+        hipLaunchKernelGGL(col2im_k3_kernel<2>, grid, dim3(256), 0, s, sub);
       else if (g.sY == 1 && g.sX == 1)
         hipLaunchKernelGGL(col2im_fast_kernel<1>, grid, dim3(256), 0, s, sub);
       else if (g.sY == 2 && g.sX == 2)
