@@ -47,6 +47,21 @@ __global__ void ktab_kernel(int* t, int K, int total, int Hs, int Ws, int kH, in
   t[total + k] = (kr * dY) | ((kc * dX) << 16);
 }
 
+// planes whose padded size fits 32-bit indexing: grid x -> pixels of one
+// padded plane, y -> plane (no per-element 64-bit division)
+__global__ void pad_plane_kernel(const float* __restrict__ im, float* __restrict__ out, int H,
+                                 int W, int pH, int pW) {
+  const int Hp = H + 2 * pH, Wp = W + 2 * pW;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= Hp * Wp) return;
+  const int64_t pl = blockIdx.y;
+  const int y = i / Wp, x = i - y * Wp;
+  const int iy = y - pH, ix = x - pW;
+  out[pl * Hp * Wp + i] = ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                              ? im[pl * H * W + iy * W + ix]
+                              : 0.0f;
+}
+
 __global__ void pad_kernel(const float* __restrict__ im, float* __restrict__ out, int64_t planes,
                            int H, int W, int pH, int pW) {
   const int Hp = H + 2 * pH, Wp = W + 2 * pW;
@@ -79,6 +94,17 @@ hipError_t launch_pad_images(const float* im, int64_t batch, int64_t C, int64_t 
                              int64_t pH, int64_t pW, float* out, hipStream_t s) {
   const int64_t total = batch * C * (H + 2 * pH) * (W + 2 * pW);
   if (total <= 0) return hipSuccess;
+  const int64_t plane = (H + 2 * pH) * (W + 2 * pW);
+  if (plane <= 0x7fffff00LL && H * W <= 0x7fffffffLL) {
+    for (int64_t p0 = 0; p0 < batch * C; p0 += 65535) {
+      const int64_t np = std::min<int64_t>(65535, batch * C - p0);
+      hipLaunchKernelGGL(pad_plane_kernel, dim3((unsigned)((plane + 255) / 256), (unsigned)np),
+                         dim3(256), 0, s, im + p0 * H * W, out + p0 * plane, (int)H, (int)W,
+                         (int)pH, (int)pW);
+      if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   int64_t blocks = (total + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(pad_kernel, dim3((unsigned)blocks), dim3(256), 0, s, im, out, batch * C,
