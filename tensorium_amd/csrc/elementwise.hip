@@ -85,6 +85,20 @@ __global__ __launch_bounds__(TPB) void derive_kernel(const float* __restrict__ x
        i += (int64_t)gridDim.x * TPB)
     delta[i] = delta[i] * grad_apply(x[i], act);
 }
+// float4 form (n % 4 == 0, 16-byte aligned): same product per element
+__global__ __launch_bounds__(TPB) void derive4_kernel(const float4* __restrict__ x, int64_t n4,
+                                                      int act, float4* __restrict__ delta) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * TPB) {
+    const float4 o = x[i];
+    float4 d = delta[i];
+    d.x = d.x * grad_apply(o.x, act);
+    d.y = d.y * grad_apply(o.y, act);
+    d.z = d.z * grad_apply(o.z, act);
+    d.w = d.w * grad_apply(o.w, act);
+    delta[i] = d;
+  }
+}
 
 // addSums (ntensors.pas:7729-7781) in the reference's order: for output i,
 // _sum := _sum + sumv(bs, block_j) over groups j ascending, then
@@ -438,6 +452,12 @@ hipError_t launch_activate(float* x, int64_t n, int act, hipStream_t s) {
 
 hipError_t launch_derive(const float* x, int64_t n, int act, float* delta, hipStream_t s) {
   if (n <= 0 || act == TNS_acLINEAR) return hipSuccess;
+  if (n % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(delta)) & 15) == 0) {
+    hipLaunchKernelGGL(derive4_kernel, dim3(grid_for(n / 4)), dim3(TPB), 0, s,
+                       reinterpret_cast<const float4*>(x), n / 4, act,
+                       reinterpret_cast<float4*>(delta));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(derive_kernel, dim3(grid_for(n)), dim3(TPB), 0, s, x, n, act, delta);
   return hipGetLastError();
 }

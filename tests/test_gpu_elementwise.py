@@ -28,9 +28,9 @@ def test_activate(hip, torch_cuda, ora, act, n):
         np.array_equal(got, ref, equal_nan=True), (act, np.abs(got - ref).max())
 
 
+@pytest.mark.parametrize("n", [5001, 5004])  # scalar and float4 forms
 @pytest.mark.parametrize("act", EXACT + TRANSC)
-def test_derive(hip, torch_cuda, ora, act):
-    n = 5001
+def test_derive(hip, torch_cuda, ora, act, n):
     y = ora.activate(ora.uniform(n, 9, act, -3.0, 3.0), act)
     delta = ora.uniform(n, 10, act)
     ref = ora.gradient(y, act, delta.copy())
