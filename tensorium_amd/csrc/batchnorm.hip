@@ -303,8 +303,12 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
                                                    float* __restrict__ part1) {
   constexpr int TILE = NT * E;
   constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;  // two LDS streams
-  __shared__ float U[2][TILE];
-  __shared__ float V[TWO ? 2 : 1][TWO ? TILE : 1];
+  // tiles stored lane-major: element e of the tile at (e & 7) * LDT + e / 8,
+  // so a chain lane's consecutive terms are contiguous (ds_read_b128 reads
+  // four); rows padded by 8 floats (conflict-free staging stores)
+  constexpr int LDT = TILE / 8 + 8;
+  __shared__ __attribute__((aligned(16))) float U[2][8 * LDT];
+  __shared__ __attribute__((aligned(16))) float V[TWO ? 2 : 1][TWO ? 8 * LDT : 1];
   const int tid = threadIdx.x;
   const int l = tid & 7, grp = tid >> 3;  // chain lane, chain set (wave 0)
   const bool chain = grp == 0 || (MODE == CH_VDELTA && grp == 1);
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
     auto store = [&](int buf) {
 #pragma unroll
       for (int u = 0; u < E; ++u) {
-        const int e = tid + NT * u;
+        const int e = ((tid + NT * u) & 7) * LDT + ((tid + NT * u) >> 3);
         if constexpr (MODE == CH_SUM) {
           U[buf][e] = ra[u];
         } else if constexpr (MODE == CH_SRSS) {  // srss: vsubps (mean - a), vmulps
@@ -355,15 +359,20 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
       if (tid < 64 && chain) {
         const int64_t rem = nb8 - (int64_t)t * TILE;
         const int cnt = (int)((rem < TILE ? rem : TILE) >> 3);
-        const float* row = ((MODE == CH_VDELTA && grp == 1) ? &V[t & 1][0] : &U[t & 1][0]) + l;
-        const float* rowb = TWO ? &V[t & 1][0] + l : row;
+        const float* row =
+            ((MODE == CH_VDELTA && grp == 1) ? &V[t & 1][0] : &U[t & 1][0]) + l * LDT;
+        const float* rowb = TWO ? &V[t & 1][0] + l * LDT : row;
         int q = 0;
         for (; q + 16 <= cnt; q += 16) {
           float v[16], w[16];
 #pragma unroll
-          for (int z = 0; z < 16; ++z) {
-            v[z] = row[8 * (q + z)];
-            if constexpr (MODE == CH_DOT) w[z] = rowb[8 * (q + z)];
+          for (int z = 0; z < 16; z += 4) {
+            const float4 x4 = *reinterpret_cast<const float4*>(row + q + z);
+            v[z] = x4.x; v[z + 1] = x4.y; v[z + 2] = x4.z; v[z + 3] = x4.w;
+            if constexpr (MODE == CH_DOT) {
+              const float4 y4 = *reinterpret_cast<const float4*>(rowb + q + z);
+              w[z] = y4.x; w[z + 1] = y4.y; w[z + 2] = y4.z; w[z + 3] = y4.w;
+            }
           }
 #pragma unroll
           for (int z = 0; z < 16; ++z) {
@@ -372,8 +381,8 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
           }
         }
         for (; q < cnt; ++q) {
-          if constexpr (MODE == CH_DOT) acc = fmaf(row[8 * q], rowb[8 * q], acc);
-          else acc = acc + row[8 * q];
+          if constexpr (MODE == CH_DOT) acc = fmaf(row[q], rowb[q], acc);
+          else acc = acc + row[q];
         }
       }
       if (t + 1 < ntile) store((t + 1) & 1);
