@@ -23,7 +23,7 @@ PEAK = 8000.0
 # access width of each op's dominant loads (for the FETCH correction)
 WIDTH = {"im2col": "b32", "col2im": "b32", "forward_bias": "b128", "activate_leaky": "b128",
          "means_and_vars": "b32", "means_and_vars_delta": "b32", "add_dots": "b32",
-         "add_sums": "b32", "normalize": "b32", "normalize_delta": "b32"}
+         "add_sums": "b32", "normalize": "b128", "normalize_delta": "b128"}  # (row forms: float4)
 
 
 def segments(rows, names):
