@@ -113,12 +113,13 @@ def test_upsample_shortcut_yolo_ops(hip, torch_cuda, ora):
             for dx in range(s):
                 ref = (ref + (sc * g4[:, :, dy, :, dx]).reshape(-1)).astype(np.float32)
         assert np.array_equal(dev_in.cpu().numpy(), ref), (zero, scale, s)
-    a, b = ora.uniform(1000, 13, 0), ora.uniform(1000, 13, 1)
-    o = T.empty(1000, device="cuda")
-    for act in (4, 9, 1):
-        hip.shortcut(1000, T.from_numpy(a).cuda(), 0, T.from_numpy(b).cuda(), 0, o, 0, act)
-        hip.finish()
-        assert np.array_equal(o.cpu().numpy(), ora.shortcut(a, b, act))
+    for n in (1000, 1001):  # float4 and scalar forms
+        a, b = ora.uniform(n, 13, 0), ora.uniform(n, 13, 1)
+        o = T.empty(n, device="cuda")
+        for act in (4, 9, 1):
+            hip.shortcut(n, T.from_numpy(a).cuda(), 0, T.from_numpy(b).cuda(), 0, o, 0, act)
+            hip.finish()
+            assert np.array_equal(o.cpu().numpy(), ora.shortcut(a, b, act)), (n, act)
     y = ora.uniform(2 * 3 * 85 * 13, 14, 0, -4.0, 4.0)
     oy = T.empty(y.size, device="cuda")
     hip.yoloForward(2, 3, 80, 13, T.from_numpy(y).cuda(), oy)
