@@ -98,7 +98,7 @@ def bench_sgemm(torch, hip, ctx, rank, n, steps, warmup):
     return wall, float(np.mean(kern_ms)), float(np.min(kern_ms))
 
 
-def bench_yolo(torch, hip, ctx, rank, steps, warmup=1):
+def bench_yolo(torch, hip, ctx, rank, steps, warmup=4):
     from tensorium_amd.yolo import yolov3_conv_table
     specs = yolov3_conv_table()
     batch = 8
