@@ -94,17 +94,19 @@ def init(backend: str | None = None) -> DistCtx:
     return DistCtx(dist, rank, world, local, device, gpu)
 
 
-def pack_flat(torch, tensors, device):
-    """One contiguous fp32 buffer holding `tensors` back to back, and the
-    (offset, shape) list to view them out of it again (unpack_flat)."""
-    total = sum(int(t.numel()) for t in tensors)
-    flat = torch.empty(total, dtype=torch.float32, device=device)
+def pack_flat(torch, tensors, device, align: int = 4):
+    """One contiguous fp32 buffer holding `tensors` back to back, each
+    starting on a multiple of `align` floats (16 bytes: the kernels' float4 /
+    aligned-weight paths apply to the views as to separately allocated
+    tensors), and the (offset, shape) list to view them out of it again
+    (unpack_flat)."""
     meta, off = [], 0
     for t in tensors:
-        n = int(t.numel())
-        flat[off:off + n].copy_(t.reshape(-1))
         meta.append((off, tuple(t.shape)))
-        off += n
+        off += -(-int(t.numel()) // align) * align
+    flat = torch.zeros(max(off, 1), dtype=torch.float32, device=device)
+    for t, (o, _) in zip(tensors, meta):
+        flat[o:o + int(t.numel())].copy_(t.reshape(-1))
     return flat, meta
 
 
