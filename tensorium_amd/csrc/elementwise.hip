@@ -513,11 +513,45 @@ __global__ __launch_bounds__(TPB) void add_in_order_kernel(float* __restrict__ C
     C[i] = acc;
   }
 }
+
+// float4 form (n % 4 == 0, 16-byte aligned): the same per-element order
+// C + part[0] + part[1] + ...; up to 8 partials are loaded before the adds
+// so their HBM reads are in flight together
+__global__ __launch_bounds__(TPB) void add_in_order4_kernel(float4* __restrict__ C,
+                                                            const float4* __restrict__ part,
+                                                            int64_t n4, int64_t batch) {
+  for (int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x; i < n4;
+       i += (int64_t)gridDim.x * TPB) {
+    float4 acc = C[i];
+    for (int64_t b0 = 0; b0 < batch; b0 += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + u < batch) v[u] = part[(b0 + u) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + u < batch) {
+          acc.x = acc.x + v[u].x;
+          acc.y = acc.y + v[u].y;
+          acc.z = acc.z + v[u].z;
+          acc.w = acc.w + v[u].w;
+        }
+    }
+    C[i] = acc;
+  }
+}
 }  // namespace
 
 hipError_t launch_add_in_order(float* C, const float* part, int64_t n, int64_t batch,
                                hipStream_t s) {
   if (n <= 0 || batch <= 0) return hipSuccess;
+  if (n % 4 == 0 && aligned16(C) && aligned16(part)) {
+    const int64_t n4 = n / 4;
+    hipLaunchKernelGGL(add_in_order4_kernel, dim3(grid_for(n4)), dim3(TPB), 0, s,
+                       reinterpret_cast<float4*>(C), reinterpret_cast<const float4*>(part), n4,
+                       batch);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(add_in_order_kernel, dim3(grid_for(n)), dim3(TPB), 0, s, C, part, n, batch);
   return hipGetLastError();
 }

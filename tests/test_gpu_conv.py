@@ -140,10 +140,11 @@ def test_yolov3_layers_batch8_implicit(hip, torch_cuda, ora, idx):
 
 @pytest.mark.parametrize("batch,C,H,F,k,s,p,act", [
     (2, 3, 17, 8, 3, 1, 1, 9), (3, 5, 12, 7, 3, 2, 1, 9), (2, 16, 9, 5, 1, 1, 0, 4),
-    (2, 6, 13, 33, 3, 1, 1, 1), (1, 32, 26, 64, 3, 2, 1, 9)])
+    (2, 6, 13, 33, 3, 1, 1, 1), (1, 32, 26, 64, 3, 2, 1, 9), (10, 4, 9, 8, 3, 1, 1, 9)])
 def test_conv_backward_matches_oracle(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act):
     """delta (derived), state_delta (TN + col2im), weight_updates (NT in the
-    reference's sdot order) and bias_updates (addSums order) bit-exact."""
+    reference's sdot order) and bias_updates (addSums order) bit-exact.  Batch
+    10 takes the dW partials past one 8-image load group of add_in_order."""
     rng = np.random.default_rng(batch * 1000 + C * 10 + H)
     oh = (H + 2 * p - k) // s + 1
     x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
