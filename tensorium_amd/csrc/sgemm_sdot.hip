@@ -15,8 +15,9 @@
 // ([row][k], odd row stride) in k-tiles of 64, double-buffered with one
 // barrier per tile.  Zero-filled k >= K adds fma(0, 0, x) = x (a chain that
 // starts at +0 never holds -0).  The epilogue meets the 8 partial tiles in LDS
-// and applies the reference's pairwise sum, alpha product and C add, each
-// rounded separately (built with -ffp-contract=off).
+// (classes r and r + 4 first, in four tiles of space) and applies the
+// reference's pairwise sum, alpha product and C add, each rounded separately
+// (built with -ffp-contract=off).
 #include "tns_internal.hpp"
 
 namespace tns {
@@ -40,7 +41,12 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
   constexpr int U = ROWS * KV / SD_NT;          // staging units per thread
   static_assert(ROWS * KV % SD_NT == 0, "staging split");
   constexpr int STAGE = ROWS * SD_KP;
-  constexpr int PART = 8 * BM * BN;
+  // float4 staging: the epilogue meets the partials in two halves (4 tiles of
+  // LDS: one more block per CU at 32 x 64, YOLOv3 52^2 / 26^2 dW 0.163 ->
+  // 0.156 ms); the scalar-staged form (short odd k, 13^2 dW 0.278 -> 0.284
+  // with halves) keeps all 8 tiles and one barrier
+  constexpr bool HALVES = VEC == 4;
+  constexpr int PART = (HALVES ? 4 : 8) * BM * BN;
   constexpr int LDS = 2 * STAGE > PART ? 2 * STAGE : PART;
   __shared__ float lds[LDS];
 
@@ -141,24 +147,45 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
     }
   }
 
-  // partial tile of residue class r -> lds[r][row][col] (every wave has
-  // passed the last barrier, so the operand buffers are free)
+  // partial tiles of the residue classes (every wave has passed the last
+  // barrier, so the operand buffers are free).  HALVES: classes 4..7 ->
+  // lds[r - 4][row][col]; class r < 4 then forms s_r = lane_r + lane_{r+4} in
+  // its registers and leaves it in lds[r].  Else class r -> lds[r].
+  auto part_at = [&](int j, int e) {
+    const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+    return ((HALVES ? (r & 3) : r) * BM + row) * BN + 32 * j + l31;
+  };
+  if (!HALVES || r >= 4) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
-      lds[(r * BM + row) * BN + 32 * j + l31] = acc[j][e];
-    }
+      for (int e = 0; e < 16; ++e) lds[part_at(j, e)] = acc[j][e];
+  }
   __syncthreads();
+  if constexpr (HALVES) {
+    if (r < 4) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int i = part_at(j, e);
+          lds[i] = acc[j][e] + lds[i];
+        }
+    }
+    __syncthreads();
+  }
   const float alpha = p.alpha, beta = p.beta;
   for (int o = tid; o < BM * BN; o += SD_NT) {
     const int64_t m = m0 + o / BN, n = n0 + o % BN;
     if (m >= M || n >= N) continue;
-    float q[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) q[c] = lds[c * BM * BN + o];
-    const float s0 = q[0] + q[4], s1 = q[1] + q[5], s2 = q[2] + q[6], s3 = q[3] + q[7];
+    constexpr int T = BM * BN;
+    float s0, s1, s2, s3;
+    if constexpr (HALVES) {
+      s0 = lds[o], s1 = lds[T + o], s2 = lds[2 * T + o], s3 = lds[3 * T + o];
+    } else {
+      s0 = lds[o] + lds[4 * T + o], s1 = lds[T + o] + lds[5 * T + o];
+      s2 = lds[2 * T + o] + lds[6 * T + o], s3 = lds[3 * T + o] + lds[7 * T + o];
+    }
     const float dot = (s0 + s1) + (s2 + s3);
     const float sum = alpha * dot;  // sum := ALPHA * sdot(...)
     float* cp = C + m * p.ldc + n;
