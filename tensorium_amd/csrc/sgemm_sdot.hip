@@ -18,6 +18,8 @@
 // (classes r and r + 4 first, in four tiles of space) and applies the
 // reference's pairwise sum, alpha product and C add, each rounded separately
 // (built with -ffp-contract=off).
+#include <algorithm>
+
 #include "tns_internal.hpp"
 
 namespace tns {
@@ -33,19 +35,21 @@ constexpr int SD_NT = 512;       // 8 waves = 8 residue classes
 
 __device__ __attribute__((aligned(16))) static float4 g_sd_zero;
 
-template <int TN, int VEC, int SD_BK>
-__global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
+template <int TN, int VEC, int SD_BK, bool O32 = false>
+__global__ __launch_bounds__(SD_NT) __attribute__((amdgpu_waves_per_eu(O32 ? 6 : 1)))
+void sgemm_nt_sdot_kernel(GemmArgs p) {
   constexpr int SD_KP = SD_BK + 1;  // LDS row stride
   constexpr int BM = 32, BN = 32 * TN, ROWS = BM + BN;
   constexpr int KV = SD_BK / VEC;               // staging units per row
   constexpr int U = ROWS * KV / SD_NT;          // staging units per thread
   static_assert(ROWS * KV % SD_NT == 0, "staging split");
   constexpr int STAGE = ROWS * SD_KP;
-  // float4 staging: the epilogue meets the partials in two halves (4 tiles of
-  // LDS: one more block per CU at 32 x 64, YOLOv3 52^2 / 26^2 dW 0.163 ->
-  // 0.156 ms); the scalar-staged form (short odd k, 13^2 dW 0.278 -> 0.284
-  // with halves) keeps all 8 tiles and one barrier
-  constexpr bool HALVES = VEC == 4;
+  // float4 and O32 staging: the epilogue meets the partials in two halves (4
+  // tiles of LDS: one more block per CU at 32 x 64, YOLOv3 52^2 / 26^2 dW
+  // 0.163 -> 0.156 ms; with O32's 80 VGPRs, 13^2 dW 0.280 -> 0.226 ms); the
+  // 64-bit-addressed scalar form is held to 2 blocks by its 94 VGPRs and keeps
+  // all 8 tiles and one barrier
+  constexpr bool HALVES = VEC == 4 || O32;
   constexpr int PART = (HALVES ? 4 : 8) * BM * BN;
   constexpr int LDS = 2 * STAGE > PART ? 2 * STAGE : PART;
   __shared__ float lds[LDS];
@@ -62,7 +66,35 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
   const int64_t M = p.M, N = p.N, K = p.K;
 
   float st[U * VEC];
+  // O32 (scalar staging, each image's operands addressable in 32 bits): a
+  // thread's k column tid % KV is the same for every staging unit and unit u
+  // is an A row iff u < UA, so a load is the uniform base plus a 32-bit row
+  // offset and one clamped k per tile.  Rows past M / N read the last row
+  // (their outputs are never stored); k >= K reads zero.
+  constexpr int UA = BM * KV / SD_NT;
+  static_assert(!O32 || (VEC == 1 && SD_NT % KV == 0 && BM % (SD_NT / KV) == 0), "O32 form");
+  const int kcol = tid % KV;
+  int roff[O32 ? U : 1];
+  if constexpr (O32) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = tid / KV + u * (SD_NT / KV);
+      roff[u] = u < UA ? (int)(std::min<int64_t>(m0 + row, M - 1) * p.lda)
+                       : (int)(std::min<int64_t>(n0 + row - BM, N - 1) * p.ldb);
+    }
+  }
   auto load_into = [&](float (&st)[U * VEC], int64_t k0) {
+    if constexpr (O32) {
+      const int kk = (int)k0 + kcol;
+      const bool kin = kk < K;
+      const int kc = kin ? kk : 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float v = (u < UA ? A : B)[roff[u] + kc];
+        st[u] = kin ? v : 0.0f;
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int idx = tid + SD_NT * u;
@@ -204,7 +236,7 @@ __global__ __launch_bounds__(SD_NT) void sgemm_nt_sdot_kernel(GemmArgs p) {
   }
 }
 
-template <int TN, int VEC, int BK = 64>
+template <int TN, int VEC, int BK = 64, bool O32 = false>
 hipError_t launch_tn(const GemmArgs& a, hipStream_t s) {
   const int64_t tiles = ((a.M + 31) / 32) * ((a.N + 32 * TN - 1) / (32 * TN));
   if (tiles > 0x7fffffff) return hipErrorInvalidValue;
@@ -215,7 +247,7 @@ hipError_t launch_tn(const GemmArgs& a, hipStream_t s) {
     sub.B = a.B + b0 * a.strideB;
     sub.C = a.C + b0 * a.strideC;
     sub.batch = nb;
-    hipLaunchKernelGGL((sgemm_nt_sdot_kernel<TN, VEC, BK>), dim3((unsigned)tiles, (unsigned)nb),
+    hipLaunchKernelGGL((sgemm_nt_sdot_kernel<TN, VEC, BK, O32>), dim3((unsigned)tiles, (unsigned)nb),
                        dim3(SD_NT), 0, s, sub);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -251,7 +283,10 @@ hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s) {
   const bool v = k_vec4(a.A, a.lda, a.strideA, a.batch, a.K) &&
                  k_vec4(a.B, a.ldb, a.strideB, a.batch, a.K);
   const int64_t b64 = ((a.M + 31) / 32) * ((a.N + 63) / 64) * a.batch;
-  if (b64 >= 1024) return v ? launch_tn<2, 4>(a, s) : launch_tn<2, 1>(a, s);
+  // scalar staging with 32-bit row offsets when each image's A and B fit them
+  const bool o32 = (a.M - 1) * a.lda + a.K <= 0x7fffffffLL && (a.N - 1) * a.ldb + a.K <= 0x7fffffffLL;
+  if (b64 >= 1024)
+    return v ? launch_tn<2, 4>(a, s) : (o32 ? launch_tn<2, 1, 64, true>(a, s) : launch_tn<2, 1>(a, s));
   // few 32x32 tiles over a long k: 256-deep k-tiles (the 64-row LDS stages
   // take 2 x 65.8 KB of gfx950's 160 KB)
   if (a.K >= 16384 && ((a.M + 31) / 32) * ((a.N + 31) / 32) * a.batch < 512)

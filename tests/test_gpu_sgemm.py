@@ -83,7 +83,7 @@ def test_all_transposes_within_bound(hip, torch_cuda, ora, M, N, K, ta, tb):
 
 NT_SHAPES = SHAPES + [(32, 4096, 4096), (32, 64, 784), (10, 32, 32), (3, 5, 8), (3, 5, 9),
                      (33, 65, 15), (64, 1152, 2704), (70, 90, 2304), (32, 27, 173056),
-                     (64, 288, 20001)]
+                     (64, 288, 20001), (1000, 2100, 169)]
 
 
 @pytest.mark.parametrize("M,N,K", NT_SHAPES)
@@ -128,6 +128,25 @@ def test_nt_sdot_batched_offsets_and_plain_order(hip, torch_cuda, ora):
     ref = run_ref(ora, 0, 1, A2, B2, C2, 1.0, 0.0)
     bnd = bound(0, 1, A2, B2, 1.0, 0.0, C2)
     assert np.all(np.abs(got.astype(np.float64) - ref) <= TOL * bnd + 1e-30)
+
+
+def test_nt_sdot_scalar_offsets_many_tiles(hip, torch_cuda, ora):
+    """Scalar-staged 32 x 64 form with 32-bit row offsets (>= 1024 tiles, odd
+    K): ragged M / N rows clamped to the last row, padded leading dims,
+    element offsets and a strided batch."""
+    rng = np.random.default_rng(21)
+    batch, M, N, K, lda, ldb, off = 2, 500, 2001, 37, 41, 39, 5
+    A = rng.uniform(-1, 1, off + batch * M * lda).astype(np.float32)
+    B = rng.uniform(-1, 1, off + batch * N * ldb).astype(np.float32)
+    C = rng.uniform(-1, 1, off + batch * M * N).astype(np.float32)
+    dA, dB, dC = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B, C))
+    hip.gemmStridedBatched(False, True, M, N, K, 0.5, dA, off, lda, M * lda, dB, off, ldb,
+                           N * ldb, 1.0, dC, off, N, M * N, batch)
+    hip.finish()
+    ref = C.copy()
+    ora.sgemm_batch_strided(False, True, M, N, K, 0.5, A[off:], lda, M * lda, B[off:], ldb,
+                            N * ldb, 1.0, ref[off:], N, M * N, batch)
+    assert np.array_equal(dC.cpu().numpy(), ref)
 
 
 CHAIN_SHAPES = [(1, 1, 1), (3, 5, 9), (33, 65, 15), (37, 53, 61), (32, 27, 2704), (17, 40, 1029),
