@@ -3,6 +3,7 @@
 methodology rule 24).  Writes gpurun_out/sgemm_sweep.json.
 
   python scripts/sgemm_sweep.py [--sizes 4096,2048] [--yolo] [--rounds 5]
+      [--tn "M,N,K,batch;..."]
 """
 import argparse
 import json
@@ -22,7 +23,11 @@ _warned = set()
 
 
 def time_variant(hip, v, prob, reps):
-    M, N, K, batch, A, B, C = prob
+    M, N, K, batch, A, B, C = prob[:7]
+    if len(prob) > 7:  # TN: A stored K x M (conv backward's W^T . delta), shared
+        call = lambda: hip.gemmVariant(v, True, False, M, N, K, 1.0, A, 0, M, 0, B, 0, N,  # noqa
+                                       K * N, 0.0, C, 0, N, M * N, batch)
+        return _time(call, v, reps)
     sA = M * K if A.dim() == 3 else 0  # batched: own A per GEMM; yolo: shared weights
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     try:
@@ -43,6 +48,24 @@ def time_variant(hip, v, prob, reps):
     return ev0.elapsed_time(ev1) / reps
 
 
+def _time(call, v, reps):
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    try:
+        call()
+    except Exception as e:
+        if v not in _warned:
+            _warned.add(v)
+            print(f"variant {v}: {e}", flush=True)
+        return None
+    torch.cuda.synchronize()
+    ev0.record()
+    for _ in range(reps):
+        call()
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / reps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", default="4096")
@@ -51,6 +74,7 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--batched", default="", help="n:batch strided-batched n^3 GEMMs")
     ap.add_argument("--shapes", default="", help="M,N,K[;M,N,K...] plain NN GEMMs")
+    ap.add_argument("--tn", default="", help="M,N,K,batch[;...] TN GEMMs, shared A")
     args = ap.parse_args()
     hip = TNNHip(0)
     names = TNNHip.gemmVariants()
@@ -67,6 +91,12 @@ def main():
         B = torch.rand(K, N, device="cuda") * 2 - 1
         C = torch.zeros(M, N, device="cuda")
         probs[f"g{M}x{N}x{K}"] = (M, N, K, 1, A, B, C)
+    for shp in [x for x in args.tn.split(";") if x]:
+        M, N, K, nb = (int(v) for v in shp.split(","))
+        A = torch.rand(K, M, device="cuda") * 0.2 - 0.1
+        B = torch.rand(nb, K, N, device="cuda") * 2 - 1
+        C = torch.zeros(nb, M, N, device="cuda")
+        probs[f"tn{M}x{N}x{K}b{nb}"] = (M, N, K, nb, A, B, C, "tn")
     if args.batched:
         n, nb = (int(v) for v in args.batched.split(":"))
         A = torch.rand(nb, n, n, device="cuda") * 2 - 1

@@ -39,9 +39,18 @@ bool vec4_ok(const float* p, int64_t ld, int64_t stride, int64_t batch, int64_t 
 
 // Shape heuristic: skinny-M conv GEMMs (filters 32/64) get short, wide tiles;
 // otherwise the largest tile that still gives every CU work.
-int pick_variant(const GemmArgs& a, bool av, bool bv) {
+// TN with k <= 1024 (the conv backward's col = W^T . delta, K = filters)
+// unless 256x256 tiles cover M x N exactly: 64x64 tiles on 16x16 MFMAs, on
+// 32x32 MFMAs at k = 1024, 32x32 tiles below ~2 blocks per CU (scripts/
+// sgemm_sweep.py --tn, YOLOv3 dX shapes at batch 8: 52^2 3x3 70 -> 88 TF,
+// 26^2 83 -> 92, 13^2 68 -> 72, 1x1 layers 38-52 -> 47-60; 4096^2 x 1024
+// stays on 256x256, 121 TF against 106 on 64x64).
+int pick_variant(const GemmArgs& a, bool av, bool bv, bool ta, bool tb) {
   const int64_t M = a.M, N = a.N, batch = a.batch;
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch; };
+  const bool big_exact = M % 256 == 0 && N % 256 == 0 && blocks(256, 256) >= 240 && av && bv;
+  if (ta && !tb && a.K <= 1024 && M > 64 && !big_exact)
+    return blocks(64, 64) < 512 ? V_32x32m16 : (a.K >= 1024 ? V_64x64 : V_64x64m16);
   if (M <= 32) return V_32x256;
   if (M <= 64) return V_64x256;
   if (M >= 256 && blocks(256, 256) >= 240 && av && bv) return V_256x256w8;
@@ -122,7 +131,7 @@ hipError_t launch_sgemm_variant(int variant, const GemmArgs& a_in, bool transA, 
     const int nb = sgemm_nn_big_pick(a);
     if (nb >= 0) return launch_sgemm_nn_big(nb, a, s);
   }
-  const int v = variant < 0 ? pick_variant(a, av, bv) : variant;
+  const int v = variant < 0 ? pick_variant(a, av, bv, transA, transB) : variant;
   if (v >= kNumVariants) return hipErrorInvalidValue;
   return kVariants[v].fn(a, transA, transB, av, bv, s);
 }
