@@ -475,8 +475,8 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * product (tuning / tests; same result bit for bit): 0 = the MFMA kernel
  * (one wave per residue class), 1 + v = VALU chain kernel variant v (one
  * lane per few residue chains, for few outputs over a long k).
- * TNS_OPT_DX_FUSED (default 1): the conv backward's state.delta of stride-1,
- * dilation-1 layers with >= 8192 pixels per image by one kernel that runs
+ * TNS_OPT_DX_FUSED (default 1): the conv backward's state.delta of 1x1
+ * stride-1, dilation-1 layers with >= 8192 pixels per image by one kernel that runs
  * each window tap's filter chain and adds it to the image pixel in scol2im's
  * order (no col matrix); 2 = that kernel on every stride-1 layer it fits;
  * 0 = the reference's two stages, TN GEMM into the workspace + col2im (same

@@ -11,5 +11,5 @@ for pass in 1 2; do
     if [ $L = main ]; then lib=tensorium_amd/libtensorium_hip.so; else lib=ab/$L/libtensorium_hip.so; fi
     TNS_LIB=$lib timeout -k 10 200 python -u scripts/conv_bwd_layers.py > gpurun_out/bwd_${L}_$pass.json 2> gpurun_out/bwd_${L}_$pass.err || exit 1
   done
-  python scripts/cmp_bwd_layers.py gpurun_out/bwd_base_$pass.json gpurun_out/bwd_main_$pass.json
+  python scripts/cmp_bwd_layers.py gpurun_out/bwd_${REF:-base}_$pass.json gpurun_out/bwd_main_$pass.json
 done

@@ -153,15 +153,15 @@ __global__ __launch_bounds__(256) void transpose_taps_kernel(const float* w, flo
 }  // namespace
 
 // Measured on the YOLOv3 layers at batch 8 (scripts/conv_bwd_layers.py
-// --dx-fused 0/1, whole backward calls): ahead on every layer with >= 104^2
-// pixels (208^2 3x3 1.054 -> 1.004 ms, 104^2 3x3 0.574 -> 0.536, 1x1 at
-// 208^2 / 104^2 0.284 -> 0.225 / 0.147 -> 0.131), behind below (52^2 3x3
-// 0.398 -> 0.454, 26^2 0.364 -> 0.612, 13^2 0.53 -> 1.0: a block runs all
-// k^2 * F chain steps of its tile in sequence, and small planes give too few
-// tiles to fill the chip), where the GEMM + col2im stages stay.
-bool conv_dx_fused_applies(int64_t C, int64_t H, int64_t W, int64_t stride, int64_t F,
+// --dx-fused 0/1, whole backward calls): ahead of TN GEMM + col2im on the 1x1
+// layers with >= 104^2 pixels (208^2 0.279 -> 0.224 ms, 104^2 0.138 ->
+// 0.128); behind on every 3x3 layer once the TN GEMM took 64x64 16x16-MFMA
+// tiles (208^2 0.88 vs 0.99, 104^2 0.48 vs 0.53; before that it led there
+// too) and on small planes (a block runs all k^2 * F chain steps of its tile
+// in sequence, and small planes give too few tiles to fill the chip).
+bool conv_dx_fused_applies(int64_t C, int64_t H, int64_t W, int64_t ks, int64_t stride, int64_t F,
                            int64_t oh, int64_t ow) {
-  return stride == 1 && C % 4 == 0 && H * W >= 8192 && C * H * W <= 0x7fffffffLL &&
+  return ks == 1 && stride == 1 && C % 4 == 0 && H * W >= 8192 && C * H * W <= 0x7fffffffLL &&
          F * oh * ow <= 0x7fffffffLL && (int64_t)F * C <= 0x7fffffffLL;
 }
 bool conv_dx_fused_fits(int64_t C, int64_t H, int64_t W, int64_t stride, int64_t F, int64_t oh,

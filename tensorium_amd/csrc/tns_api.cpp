@@ -1451,7 +1451,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // state.delta of stride-1 layers without the col matrix (conv_dx.hip)
   const bool fused_dx =
       state_delta && dilation == 1 &&
-      ((g_dx_fused == 1 && conv_dx_fused_applies(C, H, W, stride, filters, g.oh, g.ow)) ||
+      ((g_dx_fused == 1 && conv_dx_fused_applies(C, H, W, kSize, stride, filters, g.oh, g.ow)) ||
        (g_dx_fused == 2 && conv_dx_fused_fits(C, H, W, stride, filters, g.oh, g.ow)));
   float* ws = workspace;
   if (!ws && (needs_col || (state_delta && !fused_dx)))

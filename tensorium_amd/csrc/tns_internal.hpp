@@ -118,7 +118,7 @@ hipError_t launch_conv_direct(const float* in, const float* w, const float* bias
 // conv backward state.delta for stride-1, dilation-1 layers (conv_dx.hip):
 // TN GEMM col = W^T . delta fused with scol2im's accumulation into im; wt is
 // scratch for the [k^2][F][C] copy of the weights (F*C*k^2 floats)
-bool conv_dx_fused_applies(int64_t C, int64_t H, int64_t W, int64_t stride, int64_t F,
+bool conv_dx_fused_applies(int64_t C, int64_t H, int64_t W, int64_t ks, int64_t stride, int64_t F,
                            int64_t oh, int64_t ow);  // where measured faster
 bool conv_dx_fused_fits(int64_t C, int64_t H, int64_t W, int64_t stride, int64_t F, int64_t oh,
                         int64_t ow);  // where the kernel can run (forced: TNS_OPT_DX_FUSED = 2)
