@@ -59,7 +59,83 @@ def parse():
     ap.add_argument("--no-mnist", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU-baseline sample duration")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: start the ranks, rendezvous over gloo, print the "
+                         "JSON line with n_gpus and the ranks seen; no GPU work")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int | None:
+    """One process per GPU.  Returns None when this process is a rank (the
+    caller goes on to benchmark), else the launcher's exit code.
+
+    * WORLD_SIZE set (torchrun / the driver): it must equal --gpus, else exit
+      non-zero — a mismatch would report a world the run did not have.
+    * WORLD_SIZE unset and --gpus N > 1: start N copies of this script as
+      child processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, before
+      this process touches torch or the GPU; wait for them, stop the rest if
+      one fails, and exit with the first non-zero status (rank 0 prints the
+      JSON line).
+    """
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            print(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}; refusing to report a "
+                  f"world the run does not have", file=sys.stderr, flush=True)
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import subprocess
+    port = str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] +
+                                      sys.argv[1:], env=env))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other "
+                      f"ranks", file=sys.stderr, flush=True)
+                for q in alive:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args):
+    """Launcher rehearsal (no GPU): every rank joins a gloo group, the ranks
+    are gathered, rank 0 prints one JSON line."""
+    from tensorium_amd import dist as tdist
+    if os.environ.get("TNS_DRYRUN_FAIL_RANK") == os.environ.get("RANK", "0"):
+        sys.exit(3)   # test hook: a rank that dies before the rendezvous
+    ctx = tdist.init("gloo", use_gpu=False)
+    ranks = ctx.gather_floats([float(ctx.rank), float(os.getpid())])
+    t = ctx.max(float(ctx.rank))
+    ctx.barrier()
+    if ctx.rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": ctx.world, "gpus_arg": args.gpus,
+                          "ranks": [int(r[0]) for r in ranks],
+                          "pids": [int(r[1]) for r in ranks], "max_rank": t}), flush=True)
+    ctx.close()
 
 
 def synthetic(torch, shape, seed, lo=-1.0, hi=1.0):
@@ -611,9 +687,17 @@ def traffic_from_profiles(n):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
+    if args.dry_run:
+        dry_run(args)
+        return
     import torch
     from tensorium_amd import dist as tdist
     ctx = tdist.init("nccl")
+    if ctx.world != args.gpus:
+        raise SystemExit(f"bench.py: {ctx.world} ranks but --gpus {args.gpus}")
     rank, world, local = ctx.rank, ctx.world, ctx.local
     from tensorium_amd.nnhip import TNNHip
     hip = TNNHip(ctx.gpu)

@@ -64,22 +64,30 @@ class DistCtx:
             self.dist = None
 
 
-def init(backend: str | None = None) -> DistCtx:
-    """Initialise from RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* (torchrun).
-    Single process when WORLD_SIZE is unset or 1."""
+def init(backend: str | None = None, use_gpu: bool = True) -> DistCtx:
+    """Initialise from RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* (torchrun or
+    bench.py's own launcher).  Single process when WORLD_SIZE is unset or 1.
+    use_gpu=False (launcher rehearsal) never touches the GPU: gloo only."""
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     # TNS_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share
     # devices round-robin; RCCL needs one device per rank)
-    backend = os.environ.get("TNS_DIST_BACKEND") or backend
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    if use_gpu:
+        backend = os.environ.get("TNS_DIST_BACKEND") or backend
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+    else:
+        backend = "gloo"
     device = "cpu"
     gpu = 0
-    if torch.cuda.is_available():
-        gpu = local % max(torch.cuda.device_count(), 1)
+    if use_gpu and torch.cuda.is_available():
+        ndev = max(torch.cuda.device_count(), 1)
+        if backend == "nccl" and world > ndev:
+            raise RuntimeError(f"{world} ranks over RCCL need {world} GPUs, {ndev} visible "
+                               f"(TNS_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
+        gpu = local % ndev
         torch.cuda.set_device(gpu)
         if backend == "nccl":
             device = f"cuda:{gpu}"
