@@ -278,6 +278,326 @@ def means_and_vars(x, groups, N, bs, quirk):
     return ms, vs
 
 
+# ---------------------------------------------------------------- round 3:
+# batch-norm elementwise passes, softmax / cross-entropy, transcendental
+# activations, the SGD update and one whole connected-layer train step.
+# Decisions shared with the C oracle (stated there too): sEPSILON
+# (ntensors.pas:95) is the single 1e-6; FPC's exp / ln / Power return
+# extended, transcribed here as the C library's double exp / log / pow
+# rounded once to single (math.exp/log/pow are the same libm calls).
+EPS = F(1e-6)
+
+
+def fsqrt(v):
+    """sqrt of a binary32 rounded to binary32: the double sqrt is correctly
+    rounded and 53 >= 2*24 + 2, so rounding it again to 24 bits is exact."""
+    return f32(Fraction(math.sqrt(float(v))))
+
+
+def fdiv(a, b):
+    return f32(a / b)
+
+
+def fsub(a, b):
+    return f32(a - b)
+
+
+def fexp(x):
+    """exp of a single, FPC extended result assigned to a single (+inf when
+    it overflows single)."""
+    try:
+        return f32(Fraction(math.exp(float(x))))
+    except OverflowError:
+        return math.inf
+
+
+def fmax(a, b):
+    return a if a > b else b
+
+
+def block_normalize(x, groups, N, bs, means, var):
+    """TTensor.blockNormalize (ntensors.pas:8693-8718): blockSize 1 ->
+    normvv = _snormvv (4331-4342): (x - m) / sqrt(max(v, eps)); otherwise
+    normblkvv = _snormblkvv (4357-4382) -> snormvss: d := max(sqrt(v), eps),
+    (x - m) / d (the AVX form snormvss_avx uses rcpss: quirk 5, not used)."""
+    x = list(x)
+    for g in range(groups):
+        for i in range(N):
+            o = (g * N + i) * bs
+            if bs == 1:
+                x[o] = fdiv(fsub(x[o], means[i]), fsqrt(fmax(var[i], EPS)))
+            else:
+                d = fmax(fsqrt(var[i]), EPS)
+                for j in range(bs):
+                    x[o + j] = fdiv(fsub(x[o + j], means[i]), d)
+    return x
+
+
+def forward_scale(x, groups, N, bs, s):
+    """TTensor.forwardScale (7687-7707) -> mulblkvv / vsMulB (4112-4139):
+    c[j] := c[j] * s[i], one rounding."""
+    x = list(x)
+    for g in range(groups):
+        for i in range(N):
+            o = (g * N + i) * bs
+            for j in range(bs):
+                x[o + j] = mul(x[o + j], s[i])
+    return x
+
+
+def normalize_delta(x, means, var, md, vd, delta, groups, N, bs):
+    """sNormalizeDelta (8902-8951) with sNormalizeDelta_avx (8761-8818):
+    arguments md/B, 2*vd/B, mean, sqrt(max(v, eps)) (8935, B = groups*bs);
+    per element a := d / std; t := (x - mean) * vdB; t := t + mdB;
+    d := a + t (vdivps, vsubps, vmulps, vaddps, vaddps: each rounded)."""
+    delta = list(delta)
+    B = F(groups * bs)
+    for j in range(groups):
+        for i in range(N):
+            mdb = fdiv(md[i], B)
+            vdb = fdiv(mul(F(2), vd[i]), B)
+            sd = fsqrt(fmax(var[i], EPS))
+            o = (i + j * N) * bs
+            for k in range(bs):
+                a = fdiv(delta[o + k], sd)
+                t = add(mul(fsub(x[o + k], means[i]), vdb), mdb)
+                delta[o + k] = add(a, t)
+    return delta
+
+
+def strided_sum(vals):
+    """vsSumI with stride != 1 (3624-3635): Result := Result + src[i]."""
+    r = Fraction(0)
+    for v in vals:
+        r = add(r, v)
+    return r
+
+
+def add_sums(dst, src, groups, N, bs):
+    """TTensor.addSums (7729-7781): blockSize 1 -> sumv(groups, D2+i, nDst),
+    which is vssum_avx2 when the stride nDst is 1 and the scalar loop
+    otherwise; else per channel the group blocks' vssum in group order."""
+    dst = list(dst)
+    for i in range(N):
+        if bs == 1:
+            vals = [src[g * N + i] for g in range(groups)]
+            dst[i] = add(dst[i], vssum(vals) if N == 1 else strided_sum(vals))
+        else:
+            s = Fraction(0)
+            for g in range(groups):
+                o = (g * N + i) * bs
+                s = add(s, vssum(src[o:o + bs]))
+            dst[i] = add(dst[i], s)
+    return dst
+
+
+def add_dots(dst, a, b, groups, N, bs):
+    """TTensor.addDots (7783-7834): blockSize 1 -> dotvv(groups, stride
+    nDst) = cblas_sdot's strided loop (2217-2219: mul, then add); else per
+    group block sdot (8-lane FMA) summed in group order."""
+    dst = list(dst)
+    for i in range(N):
+        if bs == 1:
+            r = Fraction(0)
+            for g in range(groups):
+                r = add(r, mul(a[g * N + i], b[g * N + i]))
+            dst[i] = add(dst[i], r)
+        else:
+            s = Fraction(0)
+            for g in range(groups):
+                o = (i + g * N) * bs
+                s = add(s, sdot(a[o:o + bs], b[o:o + bs]))
+            dst[i] = add(dst[i], s)
+    return dst
+
+
+def mean_var_delta(delta, x, means, var, groups, N, bs, quirk):
+    """sMeanAndVarianceDelta (8831-8871), final scaling included:
+    mean_delta = m * (-1 / sqrt(max(v, eps))) in single;
+    variance_delta = v * -0.5 * Power(max(v, eps), -1.5) in double."""
+    ms, vs = mean_var_delta_sums(delta, x, means, groups, N, bs, quirk)
+    md, vd = [], []
+    for i in range(N):
+        ve = fmax(var[i], EPS)
+        md.append(mul(ms[i], fdiv(F(-1), fsqrt(ve))))
+        vd.append(f32(Fraction(float(vs[i]) * -0.5 * math.pow(float(ve), -1.5))))
+    return md, vd
+
+
+def logistic(x):
+    """logistic_activate (nactivation.pas:293-297): 1/(1 + exp(-x)) in the
+    extended evaluation (here double), rounded once."""
+    return [f32(Fraction(1.0 / (1.0 + math.exp(-float(v))))) for v in x]
+
+
+def tanh_act(x):
+    """tanh_activate (351-360): px := exp(x); nx := exp(-x) as singles,
+    (px - nx)/(px + nx) in single."""
+    out = []
+    for v in x:
+        px, nx = fexp(v), fexp(-v)
+        if math.inf in (px, nx):   # inf - x over inf + x: NaN (IEEE, exact)
+            out.append(math.nan)
+            continue
+        out.append(fdiv(fsub(px, nx), add(px, nx)))
+    return out
+
+
+def activate(x, act):
+    if act == 0:
+        return logistic(x)
+    if act == 1:
+        return relu(x)
+    if act == 4:
+        return list(x)
+    if act == 6:
+        return tanh_act(x)
+    if act == 9:
+        return leaky(x)
+    raise ValueError(act)
+
+
+def gradient(y, act, delta):
+    """gradient_array (nactivation.pas:624-717): delta *= f'(y) with
+    logistic (1 - y)*y (423-426), relu ord(y > 0), linear 1, tanh 1 - y*y,
+    leaky y > 0 ? 1 : 0.1."""
+    out = []
+    for v, d in zip(y, delta):
+        if act == 0:
+            g = mul(fsub(F(1), v), v)
+        elif act == 1:
+            g = Fraction(1 if v > 0 else 0)
+        elif act == 4:
+            out.append(d)
+            continue
+        elif act == 6:
+            g = fsub(F(1), mul(v, v))
+        elif act == 9:
+            g = Fraction(1) if v > 0 else F(0.1)
+        else:
+            raise ValueError(act)
+        out.append(mul(d, g))
+    return out
+
+
+def softmax(xs, temp):
+    """softmax (nsoftmaxlayer.pas:83-106): largest, e := exp((x - largest) /
+    temp) as a single, sum := sum + e, then o := o / sum."""
+    largest = xs[0]
+    for v in xs[1:]:
+        if v > largest:
+            largest = v
+    es, s = [], Fraction(0)
+    for v in xs:
+        e = fexp(fdiv(fsub(v, largest), temp))
+        s = add(s, e)
+        es.append(e)
+    return [fdiv(e, s) for e in es]
+
+
+def softmax_xent(pred, truth):
+    """softmaxCrossEntropy (123-137): error := -ln(max(p, eps)) where t <> 0,
+    else 0; delta := t - p."""
+    err, dl = [], []
+    for p, t in zip(pred, truth):
+        err.append(f32(Fraction(-math.log(float(fmax(p, EPS))))) if t != 0 else Fraction(0))
+        dl.append(fsub(t, p))
+    return dl, err
+
+
+def sgd_update(W, dW, b, db, scales, dscales, lr, momentum, decay, batch):
+    """TConnectedLayer.update (nconnectedlayer.pas:324-359): lrb :=
+    learningRate / batch, ndb := -decay * batch (singles);
+    biases.axpy(lrb, bias_updates) (saxpy: FMA); bias_updates *= momentum;
+    scales likewise; weight_updates.axpy(ndb, weights);
+    weights.axpy(lrb, weight_updates); weight_updates *= momentum."""
+    lrb = fdiv(lr, F(batch))
+    ndb = mul(-decay, F(batch))
+    b = [fma(lrb, g, v) for v, g in zip(b, db)]
+    db = [mul(momentum, g) for g in db]
+    if scales is not None:
+        scales = [fma(lrb, g, v) for v, g in zip(scales, dscales)]
+        dscales = [mul(momentum, g) for g in dscales]
+    dW = [fma(ndb, w, g) for w, g in zip(W, dW)]
+    W = [fma(lrb, g, w) for w, g in zip(W, dW)]
+    dW = [mul(momentum, g) for g in dW]
+    return W, dW, b, db, scales, dscales
+
+
+def mlp_step(widths, acts, B, X, T, layers, lr, momentum, decay):
+    """One TNNet train step over connected layers with batch norm and a
+    softmax layer (nnet.pas:275-450): per layer forward (nconnectedlayer.pas
+    157-242): out := X . W^T (gemm NT: sdot per element), MeansAndVars
+    (blockSize 1), rolling stats Multiply(1 - 0.05) then axpy(0.05, stat),
+    x := out, blockNormalize, x_norm := out, forwardScale, forwardBias,
+    activate; softmax + cross-entropy, cost = loss.Sum() (vssum_avx2);
+    backward (244-322): the softmax delta added into the last layer's delta
+    (zeroed in forward), Clamp(-1, 1), gradient, addSums, addDots,
+    forwardScale, MeansAndVarsDelta, normalizeDelta, dW += delta^T . X (TN,
+    beta 1), prev delta += delta . W (NN, beta 1; none for layer 0); then
+    update every layer.  `layers` holds each layer's dict of lists."""
+    mom = F(0.05)
+    keep = fsub(F(1), mom)
+    inp = X
+    for li, L in enumerate(layers):
+        I, O = widths[li], widths[li + 1]
+        L["delta"] = [Fraction(0)] * (B * O)
+        out = sgemm(0, 1, B, O, I, Fraction(1), inp, I, L["W"], I, Fraction(0),
+                    [Fraction(0)] * (B * O), O)
+        m, v = means_and_vars(out, B, O, 1, 0)
+        L["mean"], L["var"] = m, v
+        L["rmean"] = [fma(mom, s, mul(r, keep)) for r, s in zip(L["rmean"], m)]
+        L["rvar"] = [fma(mom, s, mul(r, keep)) for r, s in zip(L["rvar"], v)]
+        L["x"] = list(out)
+        out = block_normalize(out, B, O, 1, m, v)
+        L["xnorm"] = list(out)
+        out = forward_scale(out, B, O, 1, L["scales"])
+        out = add_bias(out, L["b"], O, 1, B)
+        L["out"] = activate(out, acts[li])
+        inp = L["out"]
+    C = widths[-1]
+    sm = []
+    for r in range(B):
+        sm += softmax(inp[r * C:(r + 1) * C], Fraction(1))
+    sm_delta, loss = softmax_xent(sm, T)
+    cost = vssum(loss)
+    last = layers[-1]
+    last["delta"] = [add(d, s) for d, s in zip(last["delta"], sm_delta)]
+    for li in range(len(layers) - 1, -1, -1):
+        L = layers[li]
+        I, O = widths[li], widths[li + 1]
+        lin = X if li == 0 else layers[li - 1]["out"]
+        d = [fmax(F(-1), v) if v < -1 else (F(1) if v > 1 else v) for v in L["delta"]]
+        d = gradient(L["out"], acts[li], d)
+        L["db"] = add_sums(L["db"], d, B, O, 1)
+        L["dscales"] = add_dots(L["dscales"], L["xnorm"], d, B, O, 1)
+        d = forward_scale(d, B, O, 1, L["scales"])
+        md, vd = mean_var_delta(d, L["x"], L["mean"], L["var"], B, O, 1, 0)
+        L["mdelta"], L["vdelta"] = md, vd
+        d = normalize_delta(L["x"], L["mean"], L["var"], md, vd, d, B, O, 1)
+        L["delta"] = d
+        L["dW"] = sgemm(1, 0, O, I, B, Fraction(1), d, O, lin, I, Fraction(1), L["dW"], I)
+        if li > 0:
+            P = layers[li - 1]
+            P["delta"] = sgemm(0, 0, B, I, O, Fraction(1), d, O, L["W"], I, Fraction(1),
+                               P["delta"], I)
+    for L in layers:
+        (L["W"], L["dW"], L["b"], L["db"], L["scales"],
+         L["dscales"]) = sgd_update(L["W"], L["dW"], L["b"], L["db"], L["scales"],
+                                    L["dscales"], lr, momentum, decay, B)
+    return cost, sm, sm_delta, loss
+
+
+MLP_ORDER = ["W", "b", "dW", "db", "scales", "rmean", "rvar", "dscales", "out", "delta", "x",
+             "xnorm", "mean", "var", "mdelta", "vdelta"]
+
+
+def mlp_sizes(I, O, B):
+    return {"W": I * O, "b": O, "dW": I * O, "db": O, "scales": O, "rmean": O, "rvar": O,
+            "dscales": O, "out": B * O, "delta": B * O, "x": B * O, "xnorm": B * O, "mean": O,
+            "var": O, "mdelta": O, "vdelta": O}
+
+
 # ---------------------------------------------------------------- cases
 def rnd(rng, n, lo=-1.0, hi=1.0):
     v = rng.uniform(lo, hi, n).astype(np.float32)
@@ -378,6 +698,128 @@ def main() -> None:
             g[f"bnc_{gi}_mean_q{q}"], g[f"bnc_{gi}_var_q{q}"] = to_np(m), to_np(v)
             ms, vs = mean_var_delta_sums(dq, xq, m, groups, N, bs, q)
             g[f"bnc_{gi}_msum_q{q}"], g[f"bnc_{gi}_vsum_q{q}"] = to_np(ms), to_np(vs)
+
+    # ---- round 3 cases
+    # blockNormalize, both epsilon forms; forwardScale; sNormalizeDelta
+    for gi, (groups, N, bs) in enumerate([(4, 3, 1), (3, 2, 16), (2, 3, 13), (5, 1, 1)]):
+        n = groups * N * bs
+        x, xq = rnd(rng, n, -2.0, 2.0)
+        d, dq = rnd(rng, n)
+        sc, scq = rnd(rng, N, 0.5, 1.5)
+        m, v = means_and_vars(xq, groups, N, bs, 0)
+        if gi == 0:     # one channel with a variance under eps: the max() matters
+            v[1] = F(3e-7)
+        mq, mqs = to_np(m), m
+        g[f"bnn_{gi}_dims"] = np.array([groups, N, bs], np.int64)
+        g[f"bnn_{gi}_x"], g[f"bnn_{gi}_d"], g[f"bnn_{gi}_s"] = x, d, sc
+        g[f"bnn_{gi}_mean"], g[f"bnn_{gi}_var"] = mq, to_np(v)
+        g[f"bnn_{gi}_norm"] = to_np(block_normalize(xq, groups, N, bs, mqs, v))
+        g[f"bnn_{gi}_scaled"] = to_np(forward_scale(xq, groups, N, bs, scq))
+        md, vd = mean_var_delta(dq, xq, mqs, v, groups, N, bs, 0)
+        g[f"bnn_{gi}_md"], g[f"bnn_{gi}_vd"] = to_np(md), to_np(vd)
+        g[f"bnn_{gi}_ndelta"] = to_np(normalize_delta(xq, mqs, v, md, vd, dq, groups, N, bs))
+        acc, accq = rnd(rng, N)
+        g[f"bnn_{gi}_acc"] = acc
+        g[f"bnn_{gi}_dots"] = to_np(add_dots(accq, xq, dq, groups, N, bs))
+        g[f"bnn_{gi}_sums"] = to_np(add_sums(accq, dq, groups, N, bs))
+
+    # logistic / tanh (incl. large |x| where exp overflows single -> NaN tanh)
+    xa = np.concatenate([rng.uniform(-8, 8, 40), [0.0, -0.0, 30.0, -30.0, 88.0, 89.0, -89.0,
+                                                   1e-8, -17.5]]).astype(np.float32)
+    xaq = [F(t) for t in xa]
+    g["act_x"] = xa
+    g["act_logistic"] = to_np(logistic(xaq))
+    g["act_tanh"] = to_np(tanh_act(xaq))
+    dg, dgq = rnd(rng, len(xa))
+    ya = to_np(logistic(xaq))
+    g["grad_d"] = dg
+    g["grad_logistic"] = to_np(gradient([F(t) for t in ya], 0, dgq))
+    yt = np.tanh(xa.astype(np.float64)).astype(np.float32)
+    g["grad_tanh_y"] = yt
+    g["grad_tanh"] = to_np(gradient([F(t) for t in yt], 6, dgq))
+
+    # softmax rows (temperature 1 and 0.5) + cross-entropy with one-hot truth
+    for gi, (rows, n, temp) in enumerate([(3, 10, 1.0), (2, 7, 0.5)]):
+        xs, xsq = rnd(rng, rows * n, -6.0, 6.0)
+        sm = []
+        for r in range(rows):
+            sm += softmax(xsq[r * n:(r + 1) * n], F(temp))
+        tr = np.zeros(rows * n, np.float32)
+        tr[[r * n + (r * 3) % n for r in range(rows)]] = 1.0
+        dl, err = softmax_xent(sm, [F(t) for t in tr])
+        g[f"sm_{gi}_dims"] = np.array([rows, n], np.int64)
+        g[f"sm_{gi}_temp"] = np.array([temp], np.float32)
+        g[f"sm_{gi}_x"], g[f"sm_{gi}_truth"] = xs, tr
+        g[f"sm_{gi}_out"], g[f"sm_{gi}_delta"] = to_np(sm), to_np(dl)
+        g[f"sm_{gi}_err"] = to_np(err)
+        g[f"sm_{gi}_cost"] = to_np([vssum(err)])
+
+    # connected-layer SGD update (with and without scales)
+    nw, no = 23, 5
+    W, Wq = rnd(rng, nw)
+    dW, dWq = rnd(rng, nw, -0.1, 0.1)
+    b, bq = rnd(rng, no)
+    db, dbq = rnd(rng, no)
+    s_, sq_ = rnd(rng, no, 0.5, 1.5)
+    ds, dsq = rnd(rng, no)
+    hyper = np.array([0.01, 0.9, 0.0005], np.float32)
+    hq = [F(t) for t in hyper]
+    g["sgd_W"], g["sgd_dW"], g["sgd_b"], g["sgd_db"] = W, dW, b, db
+    g["sgd_s"], g["sgd_ds"], g["sgd_hyper"] = s_, ds, hyper
+    g["sgd_batch"] = np.array([32], np.int64)
+    for tag, useS in (("bn", True), ("nobn", False)):
+        res = sgd_update(Wq, dWq, bq, dbq, sq_ if useS else None, dsq if useS else None,
+                         hq[0], hq[1], hq[2], 32)
+        for k, arr in zip(("W", "dW", "b", "db", "s", "ds"), res):
+            if arr is not None:
+                g[f"sgd_{tag}_{k}_out"] = to_np(arr)
+
+    # one MNIST-BN train step at batch 32, reduced width (config 5's network
+    # shape: connected layers + BN + softmax), every buffer array checked
+    widths, acts, B = [12, 8, 6, 5], [1, 0, 4], 32
+    layers = []
+    init = []
+    for li in range(len(widths) - 1):
+        I, O = widths[li], widths[li + 1]
+        r = float(np.sqrt(2.0 / I))
+        L = {}
+        for k, n in mlp_sizes(I, O, B).items():
+            if k == "W":
+                arr, q = rnd(rng, n, -r, r)
+            elif k == "scales":
+                arr, q = rnd(rng, n, 0.8, 1.2)
+            elif k in ("rmean", "b"):
+                arr, q = rnd(rng, n, -0.1, 0.1)
+            elif k == "rvar":
+                arr, q = rnd(rng, n, 0.5, 1.5)
+            elif k in ("dW", "db", "dscales"):
+                arr, q = rnd(rng, n, -0.05, 0.05)   # momentum carried over from a step before
+            else:
+                arr, q = np.zeros(n, np.float32), [Fraction(0)] * n
+            L[k] = q
+            init.append(arr)
+        layers.append(L)
+    C = widths[-1]
+    init.append(np.zeros(3 * B * C, np.float32))
+    X, Xq = rnd(rng, B * widths[0], 0.0, 1.0)
+    T = np.zeros(B * C, np.float32)
+    T[[r * C + (r * 7 + 1) % C for r in range(B)]] = 1.0
+    hyper = np.array([0.01, 0.9, 0.0005], np.float32)
+    cost, sm, smd, loss = mlp_step(widths, acts, B, Xq, [F(t) for t in T], layers,
+                                   *(F(t) for t in hyper))
+    final = []
+    for L in layers:
+        for k in MLP_ORDER:
+            final.append(to_np(L[k]))
+    final += [to_np(sm), to_np(smd), to_np(loss)]
+    g["mlp_widths"] = np.array(widths, np.int64)
+    g["mlp_acts"] = np.array(acts, np.int64)
+    g["mlp_B"] = np.array([B], np.int64)
+    g["mlp_hyper"] = hyper
+    g["mlp_X"], g["mlp_T"] = X, T
+    g["mlp_buf_in"] = np.concatenate(init)
+    g["mlp_buf_out"] = np.concatenate(final)
+    g["mlp_cost"] = to_np([cost])
 
     np.savez_compressed(OUT, **g)
     print(f"wrote {OUT} ({len(g)} arrays)")

@@ -134,3 +134,92 @@ def test_bn_channel_statistics_golden(ora, golden, gi, quirk):
     vref = (golden[f"bnc_{gi}_vsum_q{quirk}"].astype(np.float64) * -0.5
             * np.power(ve.astype(np.float64), -1.5)).astype(np.float32)
     assert eq(vd, vref)
+
+
+# ---- round 3: the rest of SURVEY §8(c)'s fixture list ----------------------
+
+@pytest.mark.parametrize("gi", range(4))
+def test_bn_elementwise_golden(ora, golden, gi):
+    """blockNormalize in both epsilon forms (_snormvv at blockSize 1,
+    _snormblkvv otherwise), forwardScale, sMeanAndVarianceDelta with its
+    final scaling, sNormalizeDelta_avx, addDots and addSums."""
+    groups, N, bs = (int(v) for v in golden[f"bnn_{gi}_dims"])
+    x, d, s = golden[f"bnn_{gi}_x"], golden[f"bnn_{gi}_d"], golden[f"bnn_{gi}_s"]
+    m, v = golden[f"bnn_{gi}_mean"].copy(), golden[f"bnn_{gi}_var"].copy()
+    assert eq(ora.normalize(x.copy(), groups, N, bs, m, v), golden[f"bnn_{gi}_norm"])
+    assert eq(ora.forward_scale(x.copy(), groups, N, bs, s.copy()), golden[f"bnn_{gi}_scaled"])
+    md, vd = ora.mean_var_delta(d.copy(), x.copy(), m, v, groups, N, bs)
+    assert eq(md, golden[f"bnn_{gi}_md"]) and eq(vd, golden[f"bnn_{gi}_vd"])
+    nd = ora.normalize_delta(x.copy(), m, v, md, vd, d.copy(), groups, N, bs)
+    assert eq(nd, golden[f"bnn_{gi}_ndelta"])
+    acc = golden[f"bnn_{gi}_acc"]
+    assert eq(ora.add_dots(acc.copy(), x.copy(), d.copy(), groups, N, bs),
+              golden[f"bnn_{gi}_dots"])
+    assert eq(ora.add_sums(acc.copy(), d.copy(), groups, N, bs), golden[f"bnn_{gi}_sums"])
+
+
+def test_bn_eps_forms_differ(golden):
+    """The two epsilon placements give different results on the channel whose
+    variance is under eps (bnn_0, blockSize 1: sqrt(max(v, eps)))."""
+    x, m, v = golden["bnn_0_x"], golden["bnn_0_mean"], golden["bnn_0_var"]
+    assert v[1] < np.float32(1e-6)
+    other = (x[1] - m[1]) / np.maximum(np.sqrt(v[1]), np.float32(1e-6))
+    assert np.float32(other) != golden["bnn_0_norm"][1]
+
+
+def test_transcendental_activations_golden(ora, golden):
+    x = golden["act_x"]
+    assert eq(ora.activate(x.copy(), 0), golden["act_logistic"])
+    t = ora.activate(x.copy(), 6)
+    assert eq(t, golden["act_tanh"])
+    assert np.isnan(golden["act_tanh"]).any()       # exp overflow -> NaN, as the reference
+    d = golden["grad_d"]
+    y = golden["act_logistic"]
+    assert eq(ora.gradient(y.copy(), 0, d.copy()), golden["grad_logistic"])
+    assert eq(ora.gradient(golden["grad_tanh_y"].copy(), 6, d.copy()), golden["grad_tanh"])
+
+
+@pytest.mark.parametrize("gi", range(2))
+def test_softmax_xent_golden(ora, golden, gi):
+    rows, n = (int(v) for v in golden[f"sm_{gi}_dims"])
+    temp = float(golden[f"sm_{gi}_temp"][0])
+    out = ora.softmax_rows(golden[f"sm_{gi}_x"].copy(), n, temp)
+    assert eq(out, golden[f"sm_{gi}_out"])
+    dl, err = ora.softmax_xent(out, golden[f"sm_{gi}_truth"].copy())
+    assert eq(dl, golden[f"sm_{gi}_delta"]) and eq(err, golden[f"sm_{gi}_err"])
+    assert np.float32(ora.vssum(err)) == golden[f"sm_{gi}_cost"][0]
+
+
+@pytest.mark.parametrize("tag", ["bn", "nobn"])
+def test_sgd_update_golden(ora, golden, tag):
+    lr, mom, decay = (np.float32(v) for v in golden["sgd_hyper"])
+    batch = int(golden["sgd_batch"][0])
+    W, dW = golden["sgd_W"].copy(), golden["sgd_dW"].copy()
+    b, db = golden["sgd_b"].copy(), golden["sgd_db"].copy()
+    s = golden["sgd_s"].copy() if tag == "bn" else None
+    ds = golden["sgd_ds"].copy() if tag == "bn" else None
+    lrb = np.float32(lr / np.float32(batch))
+    ndb = np.float32(-decay * np.float32(batch))
+    ora.sgd_update(W, dW, b, db, s, ds, float(lrb), float(ndb), float(mom))
+    assert eq(W, golden[f"sgd_{tag}_W_out"]) and eq(dW, golden[f"sgd_{tag}_dW_out"])
+    assert eq(b, golden[f"sgd_{tag}_b_out"]) and eq(db, golden[f"sgd_{tag}_db_out"])
+    if tag == "bn":
+        assert eq(s, golden["sgd_bn_s_out"]) and eq(ds, golden["sgd_bn_ds_out"])
+
+
+def test_mlp_bn_train_step_golden(ora, golden):
+    """One whole connected-network train step with batch norm and softmax
+    (config 5's structure at batch 32, reduced width): every array of the
+    packed buffer after the step, and the cost, bit for bit."""
+    widths = [int(v) for v in golden["mlp_widths"]]
+    acts = [int(v) for v in golden["mlp_acts"]]
+    B = int(golden["mlp_B"][0])
+    lr, mom, decay = (float(v) for v in golden["mlp_hyper"])
+    buf = golden["mlp_buf_in"].copy()
+    assert buf.size == ora.mlp_buffer_floats(widths, True, B)
+    cost = ora.mlp_train_step(widths, acts, True, B, golden["mlp_X"].copy(),
+                              golden["mlp_T"].copy(), lr, mom, decay, buf)
+    exp = golden["mlp_buf_out"]
+    bad = np.flatnonzero(~((buf == exp) | (np.isnan(buf) & np.isnan(exp))))
+    assert bad.size == 0, f"{bad.size} buffer floats differ, first at {bad[:8]}"
+    assert np.float32(cost) == golden["mlp_cost"][0]
