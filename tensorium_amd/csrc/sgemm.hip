@@ -45,12 +45,35 @@ bool vec4_ok(const float* p, int64_t ld, int64_t stride, int64_t batch, int64_t 
 // sgemm_sweep.py --tn, YOLOv3 dX shapes at batch 8: 52^2 3x3 70 -> 88 TF,
 // 26^2 83 -> 92, 13^2 68 -> 72, 1x1 layers 38-52 -> 47-60; 4096^2 x 1024
 // stays on 256x256, 121 TF against 106 on 64x64).
+//
+// NN with float4 operands (the conv GEMMs of Conv2D and forwardGPU's
+// gemmStridedBatched, strideA = 0; FC dX) by block count, as the implicit
+// conv picks (b64 = blocks a 64x64 tile gives, batch included): skinny M on
+// 32x64 / 64x128 tiles, >= 1200 blocks of a deep K on 128x64, >= 600 on
+// 8-wave 64x64 16x16-MFMA tiles, fewer on 64x32 / 32x32 16x16-MFMA tiles
+// (profiles/r03_sgemm_sweep_yolo.json: every YOLOv3 batch-8 shape within
+// 10 % of the best swept tile; the old N >= 1024 rule was up to 2.4x off).
 int pick_variant(const GemmArgs& a, bool av, bool bv, bool ta, bool tb) {
   const int64_t M = a.M, N = a.N, batch = a.batch;
   auto blocks = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((N + bn - 1) / bn) * batch; };
   const bool big_exact = M % 256 == 0 && N % 256 == 0 && blocks(256, 256) >= 240 && av && bv;
   if (ta && !tb && a.K <= 1024 && M > 64 && !big_exact)
     return blocks(64, 64) < 512 ? V_32x32m16 : (a.K >= 1024 ? V_64x64 : V_64x64m16);
+  if (!ta && !tb && !big_exact) {
+    // the 8-wave and 64x32 / 32x64 shapes are float4-NN only: their
+    // nearest general shape otherwise (N = 169 etc. is not a multiple of 4)
+    const bool v4 = av && bv;
+    const int64_t b64 = blocks(64, 64);
+    if (M <= 32) {
+      if (a.K < 32) return V_32x256;
+      return blocks(32, 64) >= 1024 && v4 ? V_32x64m16 : V_32x32m16;
+    }
+    if (M <= 64) return b64 >= 600 ? (v4 ? V_64x128w8 : V_64x128) : V_32x32m16;
+    if (b64 >= 1200 && M % 128 == 0 && a.K >= 1024) return V_128x64;
+    if (b64 >= 600) return v4 ? V_64x64w8m16 : V_64x64;
+    if (b64 >= 256 && a.K < 2048 && v4) return V_64x32m16;
+    return V_32x32m16;
+  }
   if (M <= 32) return V_32x256;
   if (M <= 64) return V_64x256;
   if (M >= 256 && blocks(256, 256) >= 240 && av && bv) return V_256x256w8;
