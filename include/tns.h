@@ -387,7 +387,17 @@ int tns_hip_conv_forward_train(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H
  * workspace (batch*C*k*k*outH*outW floats) may be NULL (context scratch).
  * The backward im2col / col2im pad with padding*dilation (640, 665); a
  * dilation whose columns differ from the layer's outH x outW (92-100) is
- * refused with TNS_ERR_UNSUPPORTED ("same" paddings work at any dilation). */
+ * refused with TNS_ERR_UNSUPPORTED ("same" paddings work at any dilation).
+ * At dilation > 1 this REPRODUCES THE REFERENCE, not the calculus:
+ *  - state_delta follows scol2im's input_row := (kernel_row - pad)*dil
+ *    (ntensors.pas:11650-11715) with pad = padding*dilation, which is not
+ *    the adjoint of im2col — it is not the true input gradient (reference
+ *    quirk 3);
+ *  - tns_hip_conv_forward(_train) at dilation > 1 writes out_dim(H, padding,
+ *    kSize, dilation, stride) columns per filter, while this backward takes
+ *    delta / output with the layer's (H + 2*padding - kSize)/stride + 1
+ *    (nConvolutionLayer.pas:92-100): the two agree only where those sizes
+ *    coincide ("same" paddings), exactly as in the reference. */
 int tns_hip_conv_backward(tns_ctx* ctx, int64_t batch, int64_t C, int64_t H, int64_t W,
                           const float* input, const float* weights, int64_t filters,
                           int64_t kSize, int64_t stride, int64_t padding, int64_t dilation,
@@ -444,6 +454,9 @@ int         tns_gemm_variant_count(void);
 /* plane-sized implicit-conv tiles (TNS_OPT_CONV_VARIANT = 100 + v) */
 int         tns_conv_tile_variant_count(void);
 const char* tns_conv_tile_variant_name(int32_t variant);
+/* ping-pong implicit-conv tiles (TNS_OPT_CONV_VARIANT = 200 + v) */
+int         tns_conv_pp_variant_count(void);
+const char* tns_conv_pp_variant_name(int32_t variant);
 /* VALU chain variants of the sdot-order NT product (TNS_OPT_SDOT_FORM = 1 + v) */
 int         tns_sdot_chains_variant_count(void);
 const char* tns_sdot_chains_variant_name(int32_t variant);
@@ -458,8 +471,9 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
 /* TNS_OPT_STRICT_BETA0 (default 1): beta==0 computes 0*C like the reference
  * (NaN/Inf in C propagate).  0 = BLAS convention (C not read).
  * TNS_OPT_CONV_VARIANT (default -1 = heuristic): forces the tile shape of the
- * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name, or
- * 100 + v for plane-sized tile v of tns_conv_tile_variant_name).
+ * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name, 100 + v
+ * for plane-sized tile v of tns_conv_tile_variant_name, 200 + v for ping-pong
+ * tile v of tns_conv_pp_variant_name).
  * TNS_OPT_CONV_PAD (default -1 = by cost): 1 gathers from a zero-padded copy
  * of the images, 0 bounds-checks the window inside the GEMM.
  * TNS_OPT_NT_SDOT (default 1): gemm(NoTrans, Trans) sums in the reference's

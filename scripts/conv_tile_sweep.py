@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """YOLOv3 batch-8 conv forward per distinct layer shape: the default choice,
 the previous shape heuristic (TNS_OPT_CONV_VARIANT = 99: sgemm_kernel.hpp
-tiles on zero-padded copies) and every plane-sized conv tile (100 + v),
+tiles on zero-padded copies) and every plane-sized conv tile (100 + v) and ping-pong tile (200 + v),
 interleaved rounds in one process.  One JSON line; per-shape lines on stderr.
 
   python scripts/conv_tile_sweep.py [--rounds 3]
@@ -24,10 +24,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--only", default="", help="comma list of forced variants to time")
     a = ap.parse_args()
     hip = TNNHip(0)
     nt = hip.convTileVariants()
     names = {100 + v: hip.lib.tns_conv_tile_variant_name(v).decode() for v in range(nt)}
+    names.update({200 + v: hip.lib.tns_conv_pp_variant_name(v).decode()
+                  for v in range(hip.convPPVariants())})
+    if a.only:
+        names = {k: v for k, v in names.items() if str(k) in a.only.split(",")}
     forms = [-1, 99] + list(names)
     layers, seen = [], {}
     for s in yolov3_conv_table():

@@ -296,6 +296,10 @@ int ensure_copy_stream(tns_ctx* c, int nev) {
   return TNS_OK;
 }
 
+int host_gemm_pipeline(tns_ctx* c, const HostGemm& g, int64_t R, float* dA, float* dB, float* dC,
+                       const float* dA_pre, const float* dB_pre, int64_t oneA, int64_t oneB,
+                       hipStream_t cs, hipStream_t ks);
+
 // dA_pre / dB_pre: device copies of a shared (stride 0) operand already on this
 // context's device (multi-device broadcast), or nullptr
 int host_gemm(tns_ctx* c, const HostGemm& g, const float* dA_pre, const float* dB_pre) {
@@ -308,7 +312,6 @@ int host_gemm(tns_ctx* c, const HostGemm& g, const float* dA_pre, const float* d
   // one block of A / B serving every chunk: B of a single GEMM (chunked by
   // rows of C, which need all of B) and stride-0 operands of a batch
   const bool sharedA = g.sA == 0 || g.batch == 1, sharedB = g.sB == 0 || g.batch == 1;
-  const bool upfrontA = g.sA == 0 && g.batch > 1;
   const int64_t nA = sharedA ? oneA : (g.batch - 1) * g.sA + oneA;
   const int64_t nB = sharedB ? oneB : (g.batch - 1) * g.sB + oneB;
   const int64_t nC = (g.batch - 1) * g.sC + oneC;
@@ -318,16 +321,35 @@ int host_gemm(tns_ctx* c, const HostGemm& g, const float* dA_pre, const float* d
   if (!dB_pre && oneB)
     if (int r = ensure_scratch(c, SLOT_STAGE2, nB, &dB)) return r;
   if (int r = ensure_scratch(c, SLOT_STAGE3, nC, &dC)) return r;
-  const float* uA = dA_pre ? dA_pre : dA;
-  const float* uB = dB_pre ? dB_pre : dB;
   // chunks: rows of C for one GEMM (>= 512 rows each, at most 4), GEMMs for
   // a batch (at most 16)
   const bool by_rows = g.batch == 1;
-  const int64_t units = by_rows ? g.M : g.batch;
   int64_t R = by_rows ? std::min<int64_t>(4, std::max<int64_t>(1, g.M / 512))
                       : std::min<int64_t>(16, g.batch);
   if (int r = ensure_copy_stream(c, (int)(2 * R))) return r;
   hipStream_t cs = c->copy_stream, ks = c->stream;
+  // every path out after the first copy is enqueued drains both streams: an
+  // error must not leave an upload reading (or a download writing) the
+  // caller's host buffers after the call has returned
+  const int r = host_gemm_pipeline(c, g, R, dA, dB, dC, dA_pre, dB_pre, oneA, oneB, cs, ks);
+  if (r != TNS_OK) {
+    (void)hipStreamSynchronize(cs);
+    (void)hipStreamSynchronize(ks);
+  }
+  return r;
+}
+
+int host_gemm_pipeline(tns_ctx* c, const HostGemm& g, int64_t R, float* dA, float* dB, float* dC,
+                       const float* dA_pre, const float* dB_pre, int64_t oneA, int64_t oneB,
+                       hipStream_t cs, hipStream_t ks) {
+  const float* uA = dA_pre ? dA_pre : dA;
+  const float* uB = dB_pre ? dB_pre : dB;
+  const int64_t a_rows = g.ta ? g.K : g.M, a_cols = g.ta ? g.M : g.K;
+  const int64_t b_rows = g.tb ? g.N : g.K, b_cols = g.tb ? g.K : g.N;
+  const bool sharedA = g.sA == 0 || g.batch == 1, sharedB = g.sB == 0 || g.batch == 1;
+  const bool upfrontA = g.sA == 0 && g.batch > 1;
+  const bool by_rows = g.batch == 1;
+  const int64_t units = by_rows ? g.M : g.batch;
   const bool needC = beta_mode_for(g.beta) != BETA_ZERO;
   const hipMemcpyKind H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
   // shared operands first
@@ -417,7 +439,12 @@ int multi_host_gemm(const int32_t* devices, int n, const HostGemm& g) {
   const int64_t a_rows = g.ta ? g.K : g.M, a_cols = g.ta ? g.M : g.K;
   const int64_t b_rows = g.tb ? g.N : g.K, b_cols = g.tb ? g.K : g.N;
   const int64_t oneA = span_of(a_rows, g.lda, a_cols), oneB = span_of(b_rows, g.ldb, b_cols);
-  // shared operands: host -> slot 0 once, slot 0 -> every other slot by peer copy
+  // shared operands: host -> slot 0 once, slot 0 -> every other slot by peer
+  // copy; only the slots that get GEMMs (the first min(n, batch)) need them,
+  // and with one such slot (a single GEMM: the op-table's plain gemm) there is
+  // nothing to broadcast: slot 0 runs the ordinary pipeline, row-chunked
+  // uploads included
+  const int nwork = (int)std::min<int64_t>(n, g.batch);
   std::vector<const float*> preA(n, nullptr), preB(n, nullptr);
   auto broadcast = [&](const float* host, int64_t rows, int64_t cols, int64_t ld, int64_t elems,
                        int slot, std::vector<const float*>& pre) -> int {
@@ -430,7 +457,7 @@ int multi_host_gemm(const int32_t* devices, int n, const HostGemm& g) {
       TNS_HIP_TRY(hipStreamSynchronize(ctx[0]->stream));
     }
     pre[0] = root;
-    for (int i = 1; i < n; ++i) {
+    for (int i = 1; i < nwork; ++i) {
       std::lock_guard<std::mutex> lk(ctx[i]->mu);
       TNS_HIP_TRY(hipSetDevice(ctx[i]->device));
       float* d;
@@ -446,9 +473,9 @@ int multi_host_gemm(const int32_t* devices, int n, const HostGemm& g) {
     }
     return TNS_OK;
   };
-  if (g.sA == 0 && oneA && n > 1)
+  if (g.sA == 0 && oneA && nwork > 1)
     if (int r = broadcast(g.A, a_rows, a_cols, g.lda, oneA, SLOT_STAGE1, preA)) return r;
-  if (g.sB == 0 && oneB && n > 1)
+  if (g.sB == 0 && oneB && nwork > 1)
     if (int r = broadcast(g.B, b_rows, b_cols, g.ldb, oneB, SLOT_STAGE2, preB)) return r;
   std::vector<int> status(n, TNS_OK);
   std::vector<std::string> errs(n);
@@ -1181,11 +1208,12 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
                                            ow, activation, c->stream),
                         "direct conv launch");
     }
-    // plane-sized tiles with a bounds-checked gather from the unpadded
-    // images (conv_tile.hip) where they apply; TNS_OPT_CONV_VARIANT >= 100
-    // forces tile 100 + v, 0..99 the sgemm_kernel.hpp shapes
+    // tiles with a bounds-checked gather from the unpadded images where they
+    // apply: the ping-pong schedule (conv_pp.hip) or the plane-sized lock-step
+    // tiles (conv_tile.hip); TNS_OPT_CONV_VARIANT 200 + v forces conv_pp tile
+    // v, 100 + v conv_tile tile v, 0..99 the sgemm_kernel.hpp shapes
     {
-      int tv = -1;
+      int tv = -1, pv = -1;
       const int64_t img0 = C * H * W;
       if ((kSize == 1 || kSize == 3) && k % 32 == 0 && img0 * 4 <= 0x7fffffffLL &&
           (g_conv_variant < 0 || g_conv_variant >= 100)) {
@@ -1193,8 +1221,14 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
         probe.M = filters; probe.N = batch * outImg; probe.K = k;
         probe.conv_sY = (int)stride;
         probe.A = weights; probe.lda = k;
-        tv = g_conv_variant >= 100 ? (int)(g_conv_variant - 100) : conv_tile_pick(probe, (int)kSize);
+        if (g_conv_variant >= 200)
+          pv = (int)(g_conv_variant - 200);
+        else if (g_conv_variant >= 100)
+          tv = (int)(g_conv_variant - 100);
+        else if ((pv = conv_pp_pick(probe, (int)kSize)) < 0)
+          tv = conv_tile_pick(probe, (int)kSize);
       }
+      if (pv >= 0) tv = 1000 + pv;
       if (tv >= 0) {
         const int64_t chunk = std::max<int64_t>(
             1, std::min<int64_t>(0x7fffffffLL / (4 * img0),
@@ -1215,7 +1249,8 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
           a.conv_pH = (int)padding; a.conv_pW = (int)padding;
           a.conv_bytes = (int)(4 * nb * img0);
           OpTimer t(c, TNS_OP_GEMM);
-          hipError_t e = launch_conv_tile(tv, a, (int)kSize, (int)dilation, c->stream);
+          hipError_t e = tv >= 1000 ? launch_conv_pp(tv - 1000, a, (int)kSize, (int)dilation, c->stream)
+                                    : launch_conv_tile(tv, a, (int)kSize, (int)dilation, c->stream);
           if (e == hipErrorInvalidValue)
             return set_error(TNS_ERR_UNSUPPORTED, "conv tile %d does not fit this layer", tv);
           if (int r = hip_status(e, "conv tile launch")) return r;
@@ -1548,6 +1583,8 @@ int tns_hip_conv_backward_bn(tns_ctx* c, int64_t batch, int64_t C, int64_t H, in
 int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
+int tns_conv_pp_variant_count(void) { return conv_pp_count(); }
+const char* tns_conv_pp_variant_name(int32_t v) { return conv_pp_name(v); }
 const char* tns_conv_tile_variant_name(int32_t v) { return conv_tile_name(v); }
 const char* tns_sdot_chains_variant_name(int32_t v) { return sdot_chains_variant_name(v); }
 const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }

@@ -82,6 +82,9 @@ int sgemm_nn_big_count();
 const char* sgemm_nn_big_name(int v);
 int sgemm_nn_big_pick(const GemmArgs& a);
 hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s);
+// the 256x256 NN tile on the ping-pong schedule (sgemm_nn_pp.hip; form 5)
+bool sgemm_nn_pp_applies(const GemmArgs& a);
+hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s);
 // gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
 // plain epilogue only
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
@@ -108,6 +111,12 @@ int conv_tile_count();
 const char* conv_tile_name(int v);
 int conv_tile_pick(const GemmArgs& a, int ks);
 hipError_t launch_conv_tile(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
+// implicit-GEMM convolution on the ping-pong schedule (conv_pp.hip): same
+// operands and limits as conv_tile; conv_pp_pick = -1 where not measured faster
+int conv_pp_count();
+const char* conv_pp_name(int v);
+int conv_pp_pick(const GemmArgs& a, int ks);
+hipError_t launch_conv_pp(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
 // direct convolution (conv_direct.hip) for 3-channel 3x3 layers with 16 or
 // 32 filters: bias (nullable: raw output) + activation fused
 bool conv_direct_applies(int64_t C, int64_t ks, int64_t filters);

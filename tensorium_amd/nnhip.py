@@ -310,6 +310,10 @@ class TNNHip:
         """Plane-sized implicit-conv tiles (setConvVariant(100 + v))."""
         return int(self.lib.tns_conv_tile_variant_count())
 
+    def convPPVariants(self) -> int:
+        """Ping-pong implicit-conv tiles (setConvVariant(200 + v))."""
+        return int(self.lib.tns_conv_pp_variant_count())
+
     def sdotChainsVariants(self) -> int:
         return int(self.lib.tns_sdot_chains_variant_count())
 

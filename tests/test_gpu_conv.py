@@ -402,3 +402,33 @@ def test_conv_tile_variants_bit_exact(hip, torch_cuda, ora):
     finally:
         hip.setConvVariant(-1)
     assert ran >= 2 * ntiles
+
+
+PP_CASES = TILE_CASES + [(2, 32, 9, 128, 1, 1, 0, 4, 1), (2, 64, 9, 128, 1, 1, 0, 4, 1),
+                         (2, 64, 26, 512, 3, 1, 1, 9, 1), (1, 64, 13, 1024, 3, 1, 1, 1, 1)]
+
+
+def test_conv_pp_variants_bit_exact(hip, torch_cuda, ora):
+    """Every ping-pong conv tile (conv_pp.hip, TNS_OPT_CONV_VARIANT = 200 + v):
+    two wave groups alternating compute and staging, staging loads issued a
+    phase early; one, two and many k-tiles (the prologue, the peeled last
+    tiles), 1x1 / 3x3, strides 1/2, dilation 2, ragged N, fused epilogues and
+    the separate logistic pass — bit-identical to the oracle."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convPPVariants()
+    assert nv >= 3
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setConvVariant(200 + v)
+            for i, (batch, C, H, F, k, s, p, act, d) in enumerate(PP_CASES):
+                try:
+                    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, 3,
+                                         seed=100 + i, dil=d)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, batch, C, H, F, k, s, p, act, d)
+    finally:
+        hip.setConvVariant(-1)
+    assert ran >= 3 * nv

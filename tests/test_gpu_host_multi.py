@@ -66,6 +66,45 @@ def test_multi_device_strided_batched(hiplib, torch_cuda, ora, devices, ta, tb, 
     assert np.array_equal(single, got)
 
 
+@pytest.mark.parametrize("devices", [[0, 1], [1, 0, 1]])
+def test_multi_device_distinct_gpus(hiplib, torch_cuda, ora, devices):
+    """The real cross-device branch: shards on distinct GPUs, the shared
+    operand peer-copied over xGMI (hipMemcpyPeerAsync) and per-thread
+    hipSetDevice onto the second GPU.  Needs two GPUs (skipped on the 1-GPU
+    box; runs wherever the multi-GPU evidence is gathered)."""
+    if hiplib.tns_device_count() < 2:
+        pytest.skip("needs >= 2 GPUs (the cross-device peer-copy branch)")
+    for shared in (True, False):
+        rng = np.random.default_rng(31 + len(devices) + shared)
+        M, N, K, batch = 96, 80, 72, 9
+        lda, ldb, ldc, sA, sB, sC, A, B, C0 = _case(rng, 0, 0, M, N, K, batch, shared, 1, 3)
+        ref = _ref(ora, 0, 0, M, N, K, 1.0, A, lda, sA, B, ldb, sB, 0.0, C0, ldc, sC, batch)
+        got = C0.copy()
+        dev = (C.c_int32 * len(devices))(*devices)
+        rc = hiplib.tns_hip_sgemm_strided_batched_multi(dev, len(devices), 0, 0, M, N, K, 1.0,
+                                                        _p(A), lda, sA, _p(B), ldb, sB, 0.0,
+                                                        _p(got), ldc, sC, batch)
+        assert rc == 0, hiplib.tns_last_error()
+        assert np.array_equal(got, ref), (devices, shared)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_multi_device_single_gemm_no_broadcast(hiplib, torch_cuda, ora, devices):
+    """A batch-1 call over several slots (the op-table's plain gemm with
+    tns_set_op_devices): only slot 0 has work, nothing is broadcast, and the
+    result is the single-device one."""
+    rng = np.random.default_rng(77)
+    M, N, K = 130, 70, 90
+    lda, ldb, ldc, sA, sB, sC, A, B, C0 = _case(rng, 0, 0, M, N, K, 1, True)
+    ref = _ref(ora, 0, 0, M, N, K, 1.0, A, lda, 0, B, ldb, 0, 0.5, C0, ldc, sC, 1)
+    got = C0.copy()
+    dev = (C.c_int32 * len(devices))(*devices)
+    rc = hiplib.tns_hip_sgemm_strided_batched_multi(dev, len(devices), 0, 0, M, N, K, 1.0, _p(A),
+                                                    lda, 0, _p(B), ldb, 0, 0.5, _p(got), ldc, sC, 1)
+    assert rc == 0, hiplib.tns_last_error()
+    assert np.array_equal(got, ref)
+
+
 def test_op_table_spread_over_devices(hiplib, torch_cuda, ora):
     """tns_set_op_devices makes the unmodified op-table pointer
     (gemmStridedBatched) run sharded; n = 1 restores the default context."""
