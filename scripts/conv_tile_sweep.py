@@ -31,6 +31,8 @@ def main():
     names = {100 + v: hip.lib.tns_conv_tile_variant_name(v).decode() for v in range(nt)}
     names.update({200 + v: hip.lib.tns_conv_pp_variant_name(v).decode()
                   for v in range(hip.convPPVariants())})
+    names.update({300 + v: hip.lib.tns_conv_dma_variant_name(v).decode()
+                  for v in range(hip.convDMAVariants())})
     if a.only:
         names = {k: v for k, v in names.items() if str(k) in a.only.split(",")}
     forms = [-1, 99] + list(names)

@@ -425,6 +425,192 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
   }
 }
 
+// The same lane chains with the waves specialised (blocks of >= 16384
+// elements, the YOLOv3 conv planes at 104^2 and above): wave 0 runs only the
+// chains, waves 1..3 only stage.  A chain's 8-16 terms per LDS row are read
+// a 16-term group ahead of the adds that consume them (the lock-step kernel
+// above waited on each group's reads before its adds: ~12 cycles per
+// dependent add), and the staging waves keep one tile of loads in flight in
+// registers while the chain wave works, three LDS buffers deep (a tile is
+// loaded at the top of tile t, written after the barrier that ends t, read
+// in tile t+2).  The loop bodies of the two roles are separate, so no staging
+// register is carried around a loop edge (hipcc copies such registers right
+// after their loads and waits there).  Same terms, same order: bit-identical.
+template <int MODE>
+__global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__ a,
+                                                       const float* __restrict__ b,
+                                                       const float* __restrict__ mu_arr,
+                                                       int64_t nblocks, int64_t N, int64_t bs,
+                                                       int quirk, float* __restrict__ part0,
+                                                       float* __restrict__ part1) {
+  constexpr int SNT = 192, E = 32, TILE = SNT * E, NBUF = 3;
+  constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;
+  // lane-major rows (a chain's terms contiguous), LDT = 8 mod 32 for
+  // conflict-free staging stores, and 64 floats of slack past a row's last
+  // term: the chain loop reads two 16-term groups ahead without a bound test
+  constexpr int LDT = TILE / 8 + 72;
+  __shared__ __attribute__((aligned(16))) float U[NBUF][8 * LDT];
+  __shared__ __attribute__((aligned(16))) float V[TWO ? NBUF : 1][TWO ? 8 * LDT : 1];
+  const int tid = threadIdx.x;
+  const bool chainwave = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;
+  const int st = tid - 64;  // staging thread index (waves 1..3)
+  const int l = tid & 7, grp = tid >> 3;
+  const bool chain = grp == 0 || (MODE == CH_VDELTA && grp == 1);
+  const int64_t nb8 = (bs >> 3) << 3;
+  const int ntile = (int)((nb8 + TILE - 1) / TILE);
+  const int tail = (int)(bs & 7);
+  for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    const int64_t i = blk % N;
+    const float* pa = a + blk * bs;
+    const float* pb = TWO ? b + blk * bs : nullptr;
+    const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA) ? mu_arr[i] : 0.0f;
+    float acc = 0.0f;
+    if (!chainwave) {
+      // float4 staging where the block is 16-byte aligned (nb8 % 8 == 0: a
+      // float4 is wholly inside or outside the full 8-blocks)
+      const bool v4 = ((reinterpret_cast<uintptr_t>(pa) | (TWO ? reinterpret_cast<uintptr_t>(pb) : 0)) & 15) == 0;
+      float ra[E], rb[TWO ? E : 1];
+      auto load = [&](int t) {
+        const int64_t t0 = (int64_t)t * TILE;
+        if (v4) {
+#pragma unroll
+          for (int u = 0; u < E / 4; ++u) {
+            const int64_t k = t0 + 4 * (st + SNT * u);
+            const bool in = k < nb8;
+            const float4 x = in ? *reinterpret_cast<const float4*>(pa + k) : float4{0, 0, 0, 0};
+            ra[4 * u] = x.x; ra[4 * u + 1] = x.y; ra[4 * u + 2] = x.z; ra[4 * u + 3] = x.w;
+            if constexpr (TWO) {
+              const float4 y = in ? *reinterpret_cast<const float4*>(pb + k) : float4{0, 0, 0, 0};
+              rb[4 * u] = y.x; rb[4 * u + 1] = y.y; rb[4 * u + 2] = y.z; rb[4 * u + 3] = y.w;
+            }
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < E / 4; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              const int64_t k = t0 + 4 * (st + SNT * u) + c;
+              ra[4 * u + c] = k < nb8 ? pa[k] : 0.0f;
+              if constexpr (TWO) rb[4 * u + c] = k < nb8 ? pb[k] : 0.0f;
+            }
+        }
+      };
+      auto store = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < E / 4; ++u)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int ee = 4 * (st + SNT * u) + c;
+            const int e = (ee & 7) * LDT + (ee >> 3);
+            const float va = ra[4 * u + c];
+            if constexpr (MODE == CH_SUM) {
+              U[buf][e] = va;
+            } else if constexpr (MODE == CH_SRSS) {  // srss: vsubps (mean - a), vmulps
+              const float d = mu - va;
+              U[buf][e] = d * d;
+            } else if constexpr (MODE == CH_VDELTA) {  // a = delta, b = x
+              U[buf][e] = va;
+              V[buf][e] = (rb[4 * u + c] - mu) * va;
+            } else {
+              U[buf][e] = va;
+              V[buf][e] = rb[4 * u + c];
+            }
+          }
+      };
+      for (int t = 0; t < 2 && t < ntile; ++t) {
+        load(t);
+        store(t);
+      }
+      __syncthreads();
+      for (int t = 0; t < ntile; ++t) {
+        const bool more = t + 2 < ntile;
+        if (more) load(t + 2);
+        __syncthreads();
+        if (more) store((t + 2) % NBUF);
+      }
+    } else {
+      __syncthreads();
+      for (int t = 0; t < ntile; ++t) {
+        if (chain) {
+          const int64_t rem = nb8 - (int64_t)t * TILE;
+          const int cnt = (int)((rem < TILE ? rem : TILE) >> 3);
+          const int buf = t % NBUF;
+          const float* row =
+              ((MODE == CH_VDELTA && grp == 1) ? &V[buf][0] : &U[buf][0]) + l * LDT;
+          const float* rowb = TWO ? &V[buf][0] + l * LDT : row;
+          float va[16], wa[16], vb[16], wb[16];
+          auto rd = [&](int q, float (&v)[16], float (&w)[16]) {
+#pragma unroll
+            for (int z = 0; z < 16; z += 4) {
+              const float4 x4 = *reinterpret_cast<const float4*>(row + q + z);
+              v[z] = x4.x; v[z + 1] = x4.y; v[z + 2] = x4.z; v[z + 3] = x4.w;
+              if constexpr (MODE == CH_DOT) {
+                const float4 y4 = *reinterpret_cast<const float4*>(rowb + q + z);
+                w[z] = y4.x; w[z + 1] = y4.y; w[z + 2] = y4.z; w[z + 3] = y4.w;
+              }
+            }
+          };
+          auto add16 = [&](const float (&v)[16], const float (&w)[16]) {
+#pragma unroll
+            for (int z = 0; z < 16; ++z) {
+              if constexpr (MODE == CH_DOT) acc = fmaf(v[z], w[z], acc);
+              else acc = acc + v[z];
+            }
+          };
+          // groups of 16 terms, the next two groups' reads always in flight
+          // (unconditional: they may read the row's slack past cnt)
+          const int full = cnt & ~31;
+          rd(0, va, wa);
+          rd(16, vb, wb);
+          for (int q = 0; q < full; q += 32) {
+            add16(va, wa);
+            __builtin_amdgcn_sched_barrier(0);
+            rd(q + 32, va, wa);
+            add16(vb, wb);
+            __builtin_amdgcn_sched_barrier(0);
+            rd(q + 48, vb, wb);
+          }
+          for (int q = full; q < cnt; ++q) {
+            if constexpr (MODE == CH_DOT) acc = fmaf(row[q], rowb[q], acc);
+            else acc = acc + row[q];
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (tid < 64) {  // lane-order epilogues (as block_chains)
+      const bool lanes_form = MODE == CH_SRSS || (MODE == CH_VDELTA && grp == 1);
+      if constexpr (MODE == CH_DOT) {
+        if (tail && grp == 0) {
+          const float xa = l < tail ? pa[nb8 + l] : 0.0f;
+          const float xb = l < tail ? pb[nb8 + l] : 0.0f;
+          acc = fmaf(xa, xb, acc);
+        }
+      }
+      const float up = __shfl_down(acc, 4, 8);
+      float x0 = (lanes_form && tail == 0 && quirk) ? acc : acc + up;
+      if (lanes_form && l == 0)
+        for (int k = 0; k < tail; ++k) {
+          if (MODE == CH_SRSS) {
+            const float d = mu - pa[nb8 + k];
+            x0 = x0 + d * d;
+          } else {
+            x0 = x0 + (pb[nb8 + k] - mu) * pa[nb8 + k];
+          }
+        }
+      const float h = x0 + __shfl_down(x0, 1, 8);
+      float r = h + __shfl_down(h, 2, 8);
+      if (l == 0 && chain) {
+        if (!lanes_form && MODE != CH_DOT)
+          for (int k = 0; k < tail; ++k) r = r + pa[nb8 + k];
+        if (grp == 0) part0[blk] = r;
+        else part1[blk] = r;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // per-channel passes: block results added over the groups in order
 enum FinMode { FIN_MEAN = 0, FIN_VAR = 1, FIN_VDELTA = 2, FIN_ADD = 3 };
 template <int MODE>
@@ -457,7 +643,10 @@ hipError_t run_chains(const float* a, const float* b, const float* mu, int64_t g
                       int64_t bs, int quirk, float* part0, float* part1, hipStream_t s) {
   const int64_t nblocks = groups * N;
   const unsigned grid = (unsigned)(nblocks < (1 << 20) ? nblocks : (1 << 20));
-  if (bs >= 4096)
+  if (bs >= 16384)
+    hipLaunchKernelGGL((block_chains_ws<MODE>), dim3(grid), dim3(256), 0, s, a, b, mu, nblocks,
+                       N, bs, quirk, part0, part1);
+  else if (bs >= 4096)
     hipLaunchKernelGGL((block_chains<MODE, 256, 16>), dim3(grid), dim3(256), 0, s, a, b, mu,
                        nblocks, N, bs, quirk, part0, part1);
   else

@@ -17,11 +17,10 @@
 //     t+1 into the other LDS stage; in phase B group 1 computes tile t while
 //     group 0 writes k 16..31 of tile t+1 — every SIMD's matrix pipe has a
 //     wave with MFMAs to issue while its partner stages;
-//   * the global side of a staging job (the B gathers from the unpadded
-//     images with the window bounds checked, out-of-window taps read as 0
-//     through the buffer resource's range check; the A float4 loads) is
-//     issued into registers at the START of the group's compute phase, a
-//     whole phase ahead of the LDS writes that consume it;
+//   * a staging job (the B gathers from the unpadded images with the window
+//     bounds checked, out-of-window taps read as 0 through the buffer
+//     resource's range check; the A float4 loads; the LDS writes) runs in
+//     the group's memory phase;
 //   * B is gathered for a fixed k per lane (the lanes of a quarter take 16
 //     consecutive output pixels of one k: coalesced), (c, kr, kc) advanced
 //     incrementally by 32 per tile; A (weights, k-contiguous) transposed into
@@ -207,10 +206,6 @@ __global__ __launch_bounds__(NT, 1) void conv_pp_kernel(GemmArgs p, int dil) {
   if (nt > 0) {
     issue(0);
     finish(smem);
-    if (g == 1 && nt > 1) {
-      advance();
-      issue(1);
-    }
     __syncthreads();
     if (g == 0) frag(smem, 0, a0, b0);
   }
@@ -220,26 +215,22 @@ __global__ __launch_bounds__(NT, 1) void conv_pp_kernel(GemmArgs p, int dil) {
     const bool more = t + 1 < nt;
     // phase A: group 0 computes tile t, group 1 writes k 0..15 of tile t+1
     if (g == 0) {
+      compute(cur);
+    } else {
       if (more) {
         advance();
         issue(t + 1);
-        __builtin_amdgcn_sched_barrier(0);
+        finish(nxt);
       }
-      compute(cur);
-    } else {
-      if (more) finish(nxt);
       frag(cur, 0, a0, b0);
     }
     __syncthreads();
     // phase B: group 1 computes tile t, group 0 writes k 16..31 of tile t+1
     if (g == 1) {
-      if (t + 2 < nt) {
-        advance();
-        issue(t + 2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
       compute(cur);
     } else if (more) {
+      advance();
+      issue(t + 1);
       finish(nxt);
       frag(nxt, 0, a0, b0);  // k 0..3 of tile t+1: written in phase A
     }

@@ -125,12 +125,12 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
   const unsigned b_lds0 = __builtin_amdgcn_readfirstlane(
       (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)(smem + A_TILE +
                                                                       4 * wq * LDB));
-  // issue: the half's B DMA (straight into LDS) and A loads (into ra), as
-  // early as the rows they overwrite are free; finish (the group's memory
-  // phase): wait for both, scale A, transposing ds_writes.  Issued all at
-  // once at the start of a memory phase, the 256 CUs' requests queue behind
-  // each other and the wait outlasts the partner's compute phase (diagnostic
-  // builds: either part alone costs the same as both, none -5 %)
+  // issue: the half's B DMA (straight into LDS) and A loads (into ra);
+  // finish: wait for both, scale A, transposing ds_writes.  Both run in the
+  // group's memory phase.  (Issued a phase earlier instead — loads carried in
+  // registers across the partner's compute phase, the DMA into rows the group
+  // had finished reading — hipcc copies the loop-carried registers right
+  // after the loads and waits on them there: 4096^3 0.972 -> 1.137 ms.)
   float4 ra[AU];
   auto issue_half = [&](int64_t k0, int st, int half) {
 #ifndef TNS_PP_NO_B  // (diagnostic builds: timing without this part, wrong results)
@@ -189,9 +189,8 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
   };
   float a0[TM], b0[TN];
   // one k-tile of this wave's MFMAs from stage cur, step 0's fragments
-  // already in a0/b0; with issue, the loads of the half (ik0, ist, 0) are
-  // issued once steps 0..7 (k 0..15) are consumed
-  auto compute = [&](const float* cur, bool issue, int64_t ik0, int ist) {
+  // already in a0/b0
+  auto compute = [&](const float* cur) {
     float a1[TM], b1[TN];
 #pragma unroll
     for (int s = 0; s < BK / 2; s += 2) {
@@ -201,25 +200,15 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
       if (s + 2 < BK / 2) frag(cur, s + 2, a0, b0);
       __builtin_amdgcn_sched_barrier(0);
       mma(a1, b1);
-      if (s == BK / 4 - 2 && issue) {
-        __builtin_amdgcn_sched_barrier(0);
-        issue_half(ik0, ist, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
     }
   };
 
   // Staging jobs: group 1 fills k 0..15 of tile t+1 in phase A(t), group 0
-  // k 16..31 in phase B(t).  Group 0 issues its job's loads at the start of
-  // its compute phase A(t) (rows 16..31 of stage (t+1)&1 were last read in
-  // phase B(t-1)); group 1 issues the loads of its next job (tile t+2, rows
-  // 0..15 of stage t&1) halfway through its compute phase B(t), once it has
-  // consumed those rows itself (group 0 read them in phase A(t)).
+  // k 16..31 in phase B(t); every job's rows were last read in tile t-1.
   const int nt = (int)(p.K / BK);
   if (nt > 0) {
     issue_half(0, 0, 1 - g);  // group 1: k 0..15, group 0: k 16..31
     finish_half(0, 1 - g);
-    if (g == 1 && nt > 1) issue_half(BK, 1, 0);
     __syncthreads();
     if (g == 0) frag(smem, 0, a0, b0);
   }
@@ -229,17 +218,20 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
     const bool more = t + 1 < nt;
     // phase A
     if (g == 0) {
-      if (more) issue_half((int64_t)(t + 1) * BK, nxt, 1);
-      compute(cur, false, 0, 0);
+      compute(cur);
     } else {
-      if (more) finish_half(nxt, 0);
+      if (more) {
+        issue_half((int64_t)(t + 1) * BK, nxt, 0);
+        finish_half(nxt, 0);
+      }
       frag(cur, 0, a0, b0);
     }
     __syncthreads();
     // phase B
     if (g == 1) {
-      compute(cur, t + 2 < nt, (int64_t)(t + 2) * BK, t & 1);
+      compute(cur);
     } else if (more) {
+      issue_half((int64_t)(t + 1) * BK, nxt, 1);
       finish_half(nxt, 1);
       frag(smem + nxt * STAGE, 0, a0, b0);  // k 0..1 of tile t+1: staged in phase A
     }

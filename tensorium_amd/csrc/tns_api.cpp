@@ -1209,11 +1209,12 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
                         "direct conv launch");
     }
     // tiles with a bounds-checked gather from the unpadded images where they
-    // apply: the ping-pong schedule (conv_pp.hip) or the plane-sized lock-step
-    // tiles (conv_tile.hip); TNS_OPT_CONV_VARIANT 200 + v forces conv_pp tile
-    // v, 100 + v conv_tile tile v, 0..99 the sgemm_kernel.hpp shapes
+    // apply: the LDS-DMA ring (conv_dma.hip), the ping-pong schedule
+    // (conv_pp.hip) or the plane-sized lock-step tiles (conv_tile.hip);
+    // TNS_OPT_CONV_VARIANT 300 + v forces conv_dma tile v, 200 + v conv_pp
+    // tile v, 100 + v conv_tile tile v, 0..99 the sgemm_kernel.hpp shapes
     {
-      int tv = -1, pv = -1;
+      int tv = -1, pv = -1, dv = -1;
       const int64_t img0 = C * H * W;
       if ((kSize == 1 || kSize == 3) && k % 32 == 0 && img0 * 4 <= 0x7fffffffLL &&
           (g_conv_variant < 0 || g_conv_variant >= 100)) {
@@ -1221,14 +1222,17 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
         probe.M = filters; probe.N = batch * outImg; probe.K = k;
         probe.conv_sY = (int)stride;
         probe.A = weights; probe.lda = k;
-        if (g_conv_variant >= 200)
+        if (g_conv_variant >= 300)
+          dv = (int)(g_conv_variant - 300);
+        else if (g_conv_variant >= 200)
           pv = (int)(g_conv_variant - 200);
         else if (g_conv_variant >= 100)
           tv = (int)(g_conv_variant - 100);
-        else if ((pv = conv_pp_pick(probe, (int)kSize)) < 0)
+        else if ((dv = conv_dma_pick(probe, (int)kSize)) < 0)
           tv = conv_tile_pick(probe, (int)kSize);
       }
       if (pv >= 0) tv = 1000 + pv;
+      if (dv >= 0) tv = 2000 + dv;
       if (tv >= 0) {
         const int64_t chunk = std::max<int64_t>(
             1, std::min<int64_t>(0x7fffffffLL / (4 * img0),
@@ -1249,8 +1253,10 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
           a.conv_pH = (int)padding; a.conv_pW = (int)padding;
           a.conv_bytes = (int)(4 * nb * img0);
           OpTimer t(c, TNS_OP_GEMM);
-          hipError_t e = tv >= 1000 ? launch_conv_pp(tv - 1000, a, (int)kSize, (int)dilation, c->stream)
-                                    : launch_conv_tile(tv, a, (int)kSize, (int)dilation, c->stream);
+          hipError_t e =
+              tv >= 2000 ? launch_conv_dma(tv - 2000, a, (int)kSize, (int)dilation, c->stream)
+              : tv >= 1000 ? launch_conv_pp(tv - 1000, a, (int)kSize, (int)dilation, c->stream)
+                           : launch_conv_tile(tv, a, (int)kSize, (int)dilation, c->stream);
           if (e == hipErrorInvalidValue)
             return set_error(TNS_ERR_UNSUPPORTED, "conv tile %d does not fit this layer", tv);
           if (int r = hip_status(e, "conv tile launch")) return r;
@@ -1585,6 +1591,8 @@ int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
 int tns_conv_pp_variant_count(void) { return conv_pp_count(); }
 const char* tns_conv_pp_variant_name(int32_t v) { return conv_pp_name(v); }
+int tns_conv_dma_variant_count(void) { return conv_dma_count(); }
+const char* tns_conv_dma_variant_name(int32_t v) { return conv_dma_name(v); }
 const char* tns_conv_tile_variant_name(int32_t v) { return conv_tile_name(v); }
 const char* tns_sdot_chains_variant_name(int32_t v) { return sdot_chains_variant_name(v); }
 const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }

@@ -117,6 +117,12 @@ int conv_pp_count();
 const char* conv_pp_name(int v);
 int conv_pp_pick(const GemmArgs& a, int ks);
 hipError_t launch_conv_pp(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
+// implicit-GEMM convolution fed by an LDS-DMA ring (conv_dma.hip): same
+// operands and limits as conv_tile
+int conv_dma_count();
+const char* conv_dma_name(int v);
+int conv_dma_pick(const GemmArgs& a, int ks);
+hipError_t launch_conv_dma(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
 // direct convolution (conv_direct.hip) for 3-channel 3x3 layers with 16 or
 // 32 filters: bias (nullable: raw output) + activation fused
 bool conv_direct_applies(int64_t C, int64_t ks, int64_t filters);

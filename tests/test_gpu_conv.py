@@ -432,3 +432,31 @@ def test_conv_pp_variants_bit_exact(hip, torch_cuda, ora):
     finally:
         hip.setConvVariant(-1)
     assert ran >= 3 * nv
+
+
+def test_conv_dma_variants_bit_exact(hip, torch_cuda, ora):
+    """Every LDS-DMA-ring conv tile (conv_dma.hip, TNS_OPT_CONV_VARIANT =
+    300 + v): B gathered into LDS by dword LDS-DMA (out-of-window taps land
+    as 0 through the range check), A by 16-byte LDS-DMA into the swizzled
+    slot image, three stages two tiles ahead; one, two, three and many
+    k-tiles, 1x1 / 3x3, strides 1/2, dilation 2, ragged N, fused epilogues
+    and the separate logistic pass — bit-identical to the oracle."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convDMAVariants()
+    assert nv >= 3
+    ran = 0
+    cases = PP_CASES + [(2, 96, 11, 128, 1, 1, 0, 9, 1), (3, 32, 7, 64, 3, 1, 1, 9, 1)]
+    try:
+        for v in range(nv):
+            hip.setConvVariant(300 + v)
+            for i, (batch, C, H, F, k, s, p, act, d) in enumerate(cases):
+                try:
+                    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, 3,
+                                         seed=200 + i, dil=d)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, batch, C, H, F, k, s, p, act, d)
+    finally:
+        hip.setConvVariant(-1)
+    assert ran >= 3 * nv

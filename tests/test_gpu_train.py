@@ -18,7 +18,8 @@ def dev(torch, x):
 
 @pytest.mark.parametrize("groups,N,bs", [(32, 64, 1), (32, 10, 1), (4, 8, 9), (2, 3, 2704),
                                          (8, 16, 2704), (3, 4, 1029), (1100, 2, 9),
-                                         (8, 4, 173056), (8, 5, 169), (6, 3, 64)])
+                                         (8, 4, 173056), (8, 5, 169), (6, 3, 64),
+                                         (2, 3, 20011), (1, 3, 16392)])
 def test_means_vars_normalize_scale(hip, torch_cuda, ora, groups, N, bs):
     x = ora.uniform(groups * N * bs, 21, N, -2.0, 3.0)
     m, v = ora.means_and_vars(x, groups, N, bs)
@@ -62,7 +63,7 @@ def test_means_vars_srss_quirk(hip, torch_cuda, ora, groups, N, bs):
 
 
 BN_BWD = [(32, 64, 1), (4, 8, 9), (8, 16, 2704), (300, 3, 65), (2, 5, 1029), (3, 4, 16),
-          (8, 4, 173056), (2, 3, 43264), (8, 6, 169), (5, 2, 64)]
+          (8, 4, 173056), (2, 3, 43264), (8, 6, 169), (5, 2, 64), (2, 3, 20011), (1, 3, 16392)]
 
 
 @pytest.mark.parametrize("quirk", [0, 1])
