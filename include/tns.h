@@ -460,6 +460,9 @@ const char* tns_conv_pp_variant_name(int32_t variant);
 /* LDS-DMA-ring implicit-conv tiles (TNS_OPT_CONV_VARIANT = 300 + v) */
 int         tns_conv_dma_variant_count(void);
 const char* tns_conv_dma_variant_name(int32_t variant);
+/* input-patch conv tiles, 3x3 stride-1 pad-1 (TNS_OPT_CONV_VARIANT = 400 + v) */
+int         tns_conv_patch_variant_count(void);
+const char* tns_conv_patch_variant_name(int32_t variant);
 /* VALU chain variants of the sdot-order NT product (TNS_OPT_SDOT_FORM = 1 + v) */
 int         tns_sdot_chains_variant_count(void);
 const char* tns_sdot_chains_variant_name(int32_t variant);
@@ -477,7 +480,8 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * implicit-GEMM convolution (tuning; index as tns_gemm_variant_name, 100 + v
  * for plane-sized tile v of tns_conv_tile_variant_name, 200 + v for ping-pong
  * tile v of tns_conv_pp_variant_name, 300 + v for LDS-DMA-ring tile v of
- * tns_conv_dma_variant_name).
+ * tns_conv_dma_variant_name, 400 + v for input-patch tile v of
+ * tns_conv_patch_variant_name).
  * TNS_OPT_CONV_PAD (default -1 = by cost): 1 gathers from a zero-padded copy
  * of the images, 0 bounds-checks the window inside the GEMM.
  * TNS_OPT_NT_SDOT (default 1): gemm(NoTrans, Trans) sums in the reference's

@@ -251,6 +251,8 @@ function tns_conv_pp_variant_count(): longint; cdecl; external libtns;
 function tns_conv_pp_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_conv_dma_variant_count(): longint; cdecl; external libtns;
 function tns_conv_dma_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
+function tns_conv_patch_variant_count(): longint; cdecl; external libtns;
+function tns_conv_patch_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_sdot_chains_variant_count(): longint; cdecl; external libtns;
 function tns_sdot_chains_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_gemm_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;

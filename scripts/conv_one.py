@@ -11,6 +11,7 @@ from pathlib import Path
 import torch
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from tensorium_amd._abi import TnsError  # noqa: E402
 from tensorium_amd.nnhip import TNNHip  # noqa: E402
 from tensorium_amd.yolo import yolov3_conv_table  # noqa: E402
 
@@ -32,7 +33,10 @@ for _ in range(a.rounds):
         hip.setConvVariant(v)
         run = lambda: hip.convForward(8, s.c, s.h, s.h, x, w, b, s.filters, s.size, s.stride,  # noqa
                                       s.pad, 1, s.activation, None, out)
-        run()
+        try:
+            run()
+        except TnsError:
+            continue
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

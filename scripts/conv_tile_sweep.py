@@ -33,6 +33,8 @@ def main():
                   for v in range(hip.convPPVariants())})
     names.update({300 + v: hip.lib.tns_conv_dma_variant_name(v).decode()
                   for v in range(hip.convDMAVariants())})
+    names.update({400 + v: hip.lib.tns_conv_patch_variant_name(v).decode()
+                  for v in range(hip.convPatchVariants())})
     if a.only:
         names = {k: v for k, v in names.items() if str(k) in a.only.split(",")}
     forms = [-1, 99] + list(names)

@@ -150,6 +150,12 @@ __global__ __launch_bounds__(NT, 1) void conv_dma_kernel(GemmArgs p, int dil) {
     return;
 #endif
     const unsigned sbase = lds0 + (unsigned)(st * STAGE) * 4u;
+#ifdef TNS_CD_NO_A
+    if (i < ADMA) return;
+#endif
+#ifdef TNS_CD_NO_B
+    if (i >= ADMA) return;
+#endif
     if (i < ADMA) {
       unsigned keep;
       asm volatile(

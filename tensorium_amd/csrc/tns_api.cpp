@@ -1211,10 +1211,11 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
     // tiles with a bounds-checked gather from the unpadded images where they
     // apply: the LDS-DMA ring (conv_dma.hip), the ping-pong schedule
     // (conv_pp.hip) or the plane-sized lock-step tiles (conv_tile.hip);
-    // TNS_OPT_CONV_VARIANT 300 + v forces conv_dma tile v, 200 + v conv_pp
+    // TNS_OPT_CONV_VARIANT 400 + v forces conv_patch tile v (3x3 stride-1
+    // pad-1 layers), 300 + v conv_dma tile v, 200 + v conv_pp
     // tile v, 100 + v conv_tile tile v, 0..99 the sgemm_kernel.hpp shapes
     {
-      int tv = -1, pv = -1, dv = -1;
+      int tv = -1, pv = -1, dv = -1, ev = -1;
       const int64_t img0 = C * H * W;
       if ((kSize == 1 || kSize == 3) && k % 32 == 0 && img0 * 4 <= 0x7fffffffLL &&
           (g_conv_variant < 0 || g_conv_variant >= 100)) {
@@ -1222,7 +1223,10 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
         probe.M = filters; probe.N = batch * outImg; probe.K = k;
         probe.conv_sY = (int)stride;
         probe.A = weights; probe.lda = k;
-        if (g_conv_variant >= 300)
+        const bool patch_ok = kSize == 3 && stride == 1 && padding == 1 && dilation == 1;
+        if (g_conv_variant >= 400)
+          ev = patch_ok ? (int)(g_conv_variant - 400) : -1;
+        else if (g_conv_variant >= 300)
           dv = (int)(g_conv_variant - 300);
         else if (g_conv_variant >= 200)
           pv = (int)(g_conv_variant - 200);
@@ -1233,6 +1237,9 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
       }
       if (pv >= 0) tv = 1000 + pv;
       if (dv >= 0) tv = 2000 + dv;
+      if (ev >= 0) tv = 3000 + ev;
+      if (g_conv_variant >= 400 && ev < 0)
+        return set_error(TNS_ERR_UNSUPPORTED, "conv_patch needs a 3x3 stride-1 pad-1 layer");
       if (tv >= 0) {
         const int64_t chunk = std::max<int64_t>(
             1, std::min<int64_t>(0x7fffffffLL / (4 * img0),
@@ -1254,7 +1261,8 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
           a.conv_bytes = (int)(4 * nb * img0);
           OpTimer t(c, TNS_OP_GEMM);
           hipError_t e =
-              tv >= 2000 ? launch_conv_dma(tv - 2000, a, (int)kSize, (int)dilation, c->stream)
+              tv >= 3000 ? launch_conv_patch(tv - 3000, a, c->stream)
+              : tv >= 2000 ? launch_conv_dma(tv - 2000, a, (int)kSize, (int)dilation, c->stream)
               : tv >= 1000 ? launch_conv_pp(tv - 1000, a, (int)kSize, (int)dilation, c->stream)
                            : launch_conv_tile(tv, a, (int)kSize, (int)dilation, c->stream);
           if (e == hipErrorInvalidValue)
@@ -1593,6 +1601,8 @@ int tns_conv_pp_variant_count(void) { return conv_pp_count(); }
 const char* tns_conv_pp_variant_name(int32_t v) { return conv_pp_name(v); }
 int tns_conv_dma_variant_count(void) { return conv_dma_count(); }
 const char* tns_conv_dma_variant_name(int32_t v) { return conv_dma_name(v); }
+int tns_conv_patch_variant_count(void) { return conv_patch_count(); }
+const char* tns_conv_patch_variant_name(int32_t v) { return conv_patch_name(v); }
 const char* tns_conv_tile_variant_name(int32_t v) { return conv_tile_name(v); }
 const char* tns_sdot_chains_variant_name(int32_t v) { return sdot_chains_variant_name(v); }
 const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }

@@ -123,6 +123,12 @@ int conv_dma_count();
 const char* conv_dma_name(int v);
 int conv_dma_pick(const GemmArgs& a, int ks);
 hipError_t launch_conv_dma(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
+// 3x3 stride-1 pad-1 convolution reading B from a staged input patch
+// (conv_patch.hip): whole output rows per tile
+int conv_patch_count();
+const char* conv_patch_name(int v);
+int conv_patch_pick(const GemmArgs& a);
+hipError_t launch_conv_patch(int v, const GemmArgs& a, hipStream_t s);
 // direct convolution (conv_direct.hip) for 3-channel 3x3 layers with 16 or
 // 32 filters: bias (nullable: raw output) + activation fused
 bool conv_direct_applies(int64_t C, int64_t ks, int64_t filters);

@@ -314,6 +314,10 @@ class TNNHip:
         """Ping-pong implicit-conv tiles (setConvVariant(200 + v))."""
         return int(self.lib.tns_conv_pp_variant_count())
 
+    def convPatchVariants(self) -> int:
+        """Input-patch 3x3 stride-1 conv tiles (setConvVariant(400 + v))."""
+        return int(self.lib.tns_conv_patch_variant_count())
+
     def convDMAVariants(self) -> int:
         """LDS-DMA-ring implicit-conv tiles (setConvVariant(300 + v))."""
         return int(self.lib.tns_conv_dma_variant_count())

@@ -460,3 +460,35 @@ def test_conv_dma_variants_bit_exact(hip, torch_cuda, ora):
     finally:
         hip.setConvVariant(-1)
     assert ran >= 3 * nv
+
+
+PATCH_CASES = [(2, 32, 17, 128, 3, 1, 1, 9, 1), (2, 32, 13, 256, 3, 1, 1, 0, 1),
+               (1, 64, 26, 128, 3, 1, 1, 1, 1), (3, 32, 52, 128, 3, 1, 1, 9, 1),
+               (2, 64, 13, 1024, 3, 1, 1, 9, 1), (1, 32, 104, 128, 3, 1, 1, 4, 1),
+               (2, 32, 7, 64, 3, 1, 1, 9, 1), (1, 32, 23, 128, 3, 1, 1, 9, 1)]
+
+
+def test_conv_patch_variants_bit_exact(hip, torch_cuda, ora):
+    """Every input-patch conv tile (conv_patch.hip, TNS_OPT_CONV_VARIANT =
+    400 + v): whole output rows per tile (partial last row groups), the
+    5-channel zero-halo patch by dword LDS-DMA, tap offsets from the per-tile
+    table — bit-identical to the oracle; tiles that do not fit a plane
+    report UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convPatchVariants()
+    assert nv >= 3
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setConvVariant(400 + v)
+            for i, (batch, C, H, F, k, s, p, act, d) in enumerate(PATCH_CASES):
+                try:
+                    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, 3,
+                                         seed=300 + i, dil=d)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, batch, C, H, F, k, s, p, act, d)
+    finally:
+        hip.setConvVariant(-1)
+    assert ran >= 2 * nv
