@@ -431,8 +431,10 @@ def bench_conv_backward(torch, hip, ctx, rank, steps=2):
     """Row f-2: TConvolutionalLayer.backward over the 75 YOLOv3-416 conv
     layers at batch 8 (tns_hip_conv_backward: derive, addSums, im2col,
     per-image NT dW in the sdot order, TN dX + col2im), synthetic delta.
-    Work = dW + dX GEMMs = 2x the forward FLOPs (the first layer's dX is
-    computed too)."""
+    Work = dW for every layer + dX for layers 1..74: the first layer gets no
+    state delta, as TNNet.Propagate leaves it (state := Default(TNNetState),
+    nnet.pas:328-337 / 414-426), so its dX and col2im are skipped, as in
+    nConvolutionLayer.pas:642 ("if assigned(state.delta)")."""
     from tensorium_amd.yolo import yolov3_conv_table
     specs = yolov3_conv_table()
     batch = 8
@@ -447,7 +449,7 @@ def bench_conv_backward(torch, hip, ctx, rank, steps=2):
         delta = synthetic(torch, (batch, s.filters, s.out_h, s.out_h), g + 3, -1.0, 1.0)
         bu = torch.zeros(s.filters, device="cuda")
         wu = torch.zeros((s.filters, s.K), device="cuda")
-        sd = torch.zeros((batch, s.c, s.h, s.h), device="cuda")
+        sd = torch.zeros((batch, s.c, s.h, s.h), device="cuda") if s.index > 0 else None
         layers.append((s, x, w, out, delta, bu, wu, sd))
         max_ws = max(max_ws, batch * s.K * s.out_h * s.out_h)
     ws = torch.empty(max(max_ws, 1), device="cuda")
@@ -473,7 +475,7 @@ def bench_conv_backward(torch, hip, ctx, rank, steps=2):
              "im2col_ms": round(hip.opMs(TNS_OP_IM2COL), 3),
              "col2im_ms": round(hip.opMs(TNS_OP_COL2IM), 3)}
     hip.setTelemetry(False)
-    gflop = 2 * sum(s.flops for s in specs) * batch / 1e9
+    gflop = sum(s.flops * (2 if s.index > 0 else 1) for s in specs) * batch / 1e9
     del layers, ws
     torch.cuda.empty_cache()
     return {"layers": len(specs), "batch_per_gpu": batch, "ms_per_batch": round(wall * 1e3, 3),

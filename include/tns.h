@@ -466,6 +466,10 @@ const char* tns_conv_patch_variant_name(int32_t variant);
 /* VALU chain variants of the sdot-order NT product (TNS_OPT_SDOT_FORM = 1 + v) */
 int         tns_sdot_chains_variant_count(void);
 const char* tns_sdot_chains_variant_name(int32_t variant);
+/* residue-register forms of the sdot-order NT product (TNS_OPT_SDOT_FORM =
+ * 64 + v) */
+int         tns_sdot_rc_variant_count(void);
+const char* tns_sdot_rc_variant_name(int32_t variant);
 const char* tns_gemm_variant_name(int32_t variant);
 int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t transB,
                          int64_t M, int64_t N, int64_t K, float ALPHA,
@@ -496,7 +500,9 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * TNS_OPT_SDOT_FORM (default -1 = by shape): kernel of the sdot-order NT
  * product (tuning / tests; same result bit for bit): 0 = the MFMA kernel
  * (one wave per residue class), 1 + v = VALU chain kernel variant v (one
- * lane per few residue chains, for few outputs over a long k).
+ * lane per few residue chains, for few outputs over a long k), 64 + v =
+ * residue-register form v (one or two waves keep an output tile's eight
+ * residue chains in their registers; many tiles over a short k).
  * TNS_OPT_DX_FUSED (default 1): the conv backward's state.delta of 1x1
  * stride-1, dilation-1 layers with >= 8192 pixels per image by one kernel that runs
  * each window tap's filter chain and adds it to the image pixel in scol2im's

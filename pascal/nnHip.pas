@@ -255,6 +255,8 @@ function tns_conv_patch_variant_count(): longint; cdecl; external libtns;
 function tns_conv_patch_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_sdot_chains_variant_count(): longint; cdecl; external libtns;
 function tns_sdot_chains_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
+function tns_sdot_rc_variant_count(): longint; cdecl; external libtns;
+function tns_sdot_rc_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_gemm_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_hip_gemm_variant(ctx: PTnsCtx; variant: longint; transA, transB: boolean;
   M, N, K: int64; ALPHA: single; A: THipMem; aOffset, lda, strideA: int64; B: THipMem; bOffset,

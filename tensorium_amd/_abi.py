@@ -98,6 +98,7 @@ PROTOTYPES: dict[str, tuple] = {
     "tns_hip_set_telemetry": (C.c_int, [vp, i32]),
     "tns_gemm_variant_count": (C.c_int, []),
     "tns_sdot_chains_variant_count": (C.c_int, []),
+    "tns_sdot_rc_variant_count": (C.c_int, []),
     "tns_conv_tile_variant_count": (C.c_int, []),
     "tns_conv_tile_variant_name": (C.c_char_p, [C.c_int32]),
     "tns_conv_pp_variant_count": (C.c_int, []),
@@ -107,6 +108,7 @@ PROTOTYPES: dict[str, tuple] = {
     "tns_conv_patch_variant_count": (C.c_int, []),
     "tns_conv_patch_variant_name": (C.c_char_p, [C.c_int32]),
     "tns_sdot_chains_variant_name": (C.c_char_p, [C.c_int32]),
+    "tns_sdot_rc_variant_name": (C.c_char_p, [C.c_int32]),
     "tns_gemm_variant_name": (C.c_char_p, [i32]),
     "tns_hip_gemm_variant": (C.c_int, [vp, i32, u8, u8, i64, i64, i64, f32, fptr, i64, i64, i64,
                                        fptr, i64, i64, i64, f32, fptr, i64, i64, i64, i64]),

@@ -142,8 +142,16 @@ __global__ __launch_bounds__(G::NT) void conv_tile_kernel(GemmArgs p, int dil) {
       const unsigned x = 4u * (unsigned)(cc_[i] * HW + y * W + z);
 #pragma unroll
       for (int j = 0; j < J; ++j) {
+#if defined(TNS_CT_NOGATHER)  // diagnostic builds only: timing without the gather
+        rb[i][j] = (float)(x + j);
+        continue;
+#endif
+#if defined(TNS_CT_NOCHECK)  // diagnostic: no window check (wrong values at the borders)
+        const bool ok = true;
+#else
         const bool ok = ((unsigned)(ir0[j] + y) < (unsigned)H) &
                         ((unsigned)(ic0[j] + z) < (unsigned)W);
+#endif
         const unsigned off = ok ? vbase[j] + x : 0x80000000u;
         rb[i][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
       }
@@ -170,7 +178,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile_kernel(GemmArgs p, int dil) {
   float4 ra[AU];
   auto load_a = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < AU; ++u) ra[u] = *reinterpret_cast<const float4*>(a_src[u] + k0);
+    for (int u = 0; u < AU; ++u) {
+#if defined(TNS_CT_NOA)  // diagnostic: no A loads
+      ra[u] = make_float4(k0, u, 0, 1);
+      continue;
+#endif
+      ra[u] = *reinterpret_cast<const float4*>(a_src[u] + k0);
+    }
   };
   auto store_a = [&](float* as) {
 #pragma unroll
@@ -240,12 +254,16 @@ __global__ __launch_bounds__(G::NT) void conv_tile_kernel(GemmArgs p, int dil) {
       if constexpr (more)
         if (s == G::SS) {  // tile t+1 into the other stage, after MFMA step SS
           __builtin_amdgcn_sched_barrier(0);
+#if !defined(TNS_CT_NOSTORE)  // diagnostic builds only: timing without the LDS fill
           store_a(nxt);
           store_b(nxt + A_TILE);
+#endif
         }
       mma(a1, b1);
     }
+#if !defined(TNS_CT_NOBAR)  // diagnostic: no per-tile barrier (wrong results)
     if constexpr (more) __syncthreads();
+#endif
   };
   for (int t = 0; t + 1 < nt; ++t) tile(t, std::true_type{});
   if (nt > 0) tile(nt - 1, std::false_type{});

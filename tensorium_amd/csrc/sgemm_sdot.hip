@@ -270,6 +270,7 @@ void set_sdot_form(int form) { g_sdot_form = form < 0 ? -1 : form; }
 // few outputs over a long k go to the VALU chain kernel
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.batch <= 0) return hipSuccess;
+  if (g_sdot_form >= SDOT_FORM_RC) return launch_sdot_rc(g_sdot_form - SDOT_FORM_RC, a, s);
   if (g_sdot_form > 0) return launch_sdot_chains(a, g_sdot_form - 1, s);
   // few outputs over a long k (conv dW of the 416/208/104-pixel YOLOv3
   // layers): the VALU chain kernel, tile by output count (scripts/
@@ -280,6 +281,13 @@ hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s) {
     const int64_t outs = a.M * a.N * a.batch;
     return launch_sdot_chains(a, outs <= 8192 ? 1 : (outs <= 32768 ? 2 : 4), s);
   }
+  // many 64x64 tiles over a short k (conv dW of the 26^2 / 13^2 layers, k =
+  // pixels per image): two waves per 32x32 tile, four residue chains each
+  // (sgemm_sdot_rc.hip; profiles/r03_dw_forms.json: 4-7 % on those layers,
+  // behind this kernel on the 52^2 ones)
+  const int64_t t64 = ((a.M + 63) / 64) * ((a.N + 63) / 64) * a.batch;
+  if (g_sdot_form < 0 && a.K <= 1024 && t64 >= 512 && sdot_rc_applies(a))
+    return launch_sdot_rc(1, a, s);
   const bool v = k_vec4(a.A, a.lda, a.strideA, a.batch, a.K) &&
                  k_vec4(a.B, a.ldb, a.strideB, a.batch, a.K);
   const int64_t b64 = ((a.M + 31) / 32) * ((a.N + 63) / 64) * a.batch;

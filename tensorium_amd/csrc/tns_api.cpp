@@ -538,7 +538,8 @@ int tns_set_option(int32_t opt, int64_t value) {
       g_tt_exact = value ? 1 : 0;
       return TNS_OK;
     case TNS_OPT_SDOT_FORM:
-      if (value > sdot_chains_variant_count())
+      if (value > sdot_chains_variant_count() &&
+          (value < SDOT_FORM_RC || value >= SDOT_FORM_RC + sdot_rc_variant_count()))
         return set_error(TNS_ERR_ARG, "sdot form %lld out of range", (long long)value);
       set_sdot_form((int)value);
       return TNS_OK;
@@ -1605,6 +1606,8 @@ int tns_conv_patch_variant_count(void) { return conv_patch_count(); }
 const char* tns_conv_patch_variant_name(int32_t v) { return conv_patch_name(v); }
 const char* tns_conv_tile_variant_name(int32_t v) { return conv_tile_name(v); }
 const char* tns_sdot_chains_variant_name(int32_t v) { return sdot_chains_variant_name(v); }
+int tns_sdot_rc_variant_count(void) { return sdot_rc_variant_count(); }
+const char* tns_sdot_rc_variant_name(int32_t v) { return sdot_rc_variant_name(v); }
 const char* tns_gemm_variant_name(int32_t v) { return sgemm_variant_name(v); }
 
 int tns_hip_gemm_variant(tns_ctx* c, int32_t variant, uint8_t transA, uint8_t transB, int64_t M,

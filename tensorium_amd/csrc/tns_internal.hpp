@@ -93,7 +93,15 @@ hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
 hipError_t launch_sdot_chains(const GemmArgs& a, int variant, hipStream_t s);
 int sdot_chains_variant_count();
 const char* sdot_chains_variant_name(int v);
-// TNS_OPT_SDOT_FORM: -1 heuristic, 0 the MFMA kernel, 1 + v chains variant v
+// the same product with an output tile's residue chains in one or two
+// waves' registers (sgemm_sdot_rc.hip)
+int sdot_rc_variant_count();
+const char* sdot_rc_variant_name(int v);
+bool sdot_rc_applies(const GemmArgs& a);
+hipError_t launch_sdot_rc(int v, const GemmArgs& a, hipStream_t s);
+// TNS_OPT_SDOT_FORM: -1 heuristic, 0 the MFMA kernel, 1 + v chains variant v,
+// 64 + v residue-register form v
+constexpr int SDOT_FORM_RC = 64;
 void set_sdot_form(int form);
 // gemm(Trans, Trans) in the reference's scalar s_tt order (sgemm_tt.hip);
 // plain epilogue only

@@ -296,7 +296,8 @@ class TNNHip:
 
     def setSdotForm(self, form: int = -1):
         """Kernel of the sdot-order NT product: -1 by shape, 0 the MFMA
-        kernel, 1 + v VALU chain variant v (bit-identical); process-wide."""
+        kernel, 1 + v VALU chain variant v, 64 + v residue-register form v
+        (bit-identical); process-wide."""
         check(self.lib.tns_set_option(6, int(form)))
 
     def setDxFused(self, mode: int = 1):
@@ -324,6 +325,10 @@ class TNNHip:
 
     def sdotChainsVariants(self) -> int:
         return int(self.lib.tns_sdot_chains_variant_count())
+
+    def sdotRcVariants(self) -> int:
+        """Residue-register sdot forms (setSdotForm(64 + v))."""
+        return int(self.lib.tns_sdot_rc_variant_count())
 
     def setTtExact(self, on: bool = True):
         """gemm(Trans, Trans) in the reference's scalar s_tt order on the VALU

@@ -193,6 +193,42 @@ def test_conv_backward_yolov3_batch8(hip, torch_cuda, ora, idx):
     assert np.array_equal(dbu.cpu().numpy(), rbu)
 
 
+@pytest.mark.parametrize("idx", [1, 11, 28, 44, 45, 58])
+def test_conv_backward_dw_rc_forms(hip, torch_cuda, ora, idx):
+    """Every residue-register form of the dW product (sgemm_sdot_rc.hip,
+    TNS_OPT_SDOT_FORM = 64 + v; per-image sums added in image order after
+    the launch) gives the reference's per-image beta = 1 sdot loop bit for
+    bit — 13^2 (K = 169 per image: unaligned rows, ragged k-tile), 255
+    filters, 1x1 and stride-2 layers."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    spec = yolov3_conv_table()[idx]
+    batch, C, H, F, k, s, p = 8, spec.c, spec.h, spec.filters, spec.size, spec.stride, spec.pad
+    rng = np.random.default_rng(100 + idx)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.1, 0.1, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    rd, rbu, rwu = d0.copy(), bu0.copy(), wu0.copy()
+    ora.conv_backward(x, w, F, k, s, p, spec.activation, out, rd, rbu, rwu, None)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    dx, dw, dout = map(t, (x, w, out))
+    try:
+        for v in range(hip.sdotRcVariants()):
+            hip.setSdotForm(64 + v)
+            dd, dbu, dwu = map(t, (d0, bu0, wu0))
+            hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, spec.activation, dout, dd,
+                             dbu, dwu)
+            hip.finish()
+            got = dwu.cpu().numpy()
+            assert np.array_equal(got, rwu), (v, float(np.abs(got - rwu).max()))
+            assert np.array_equal(dd.cpu().numpy(), rd)
+    finally:
+        hip.setSdotForm(-1)
+
+
 @pytest.mark.parametrize("fused", [2, 0])
 @pytest.mark.parametrize("batch,C,H,F,k,s,p,act", [
     (2, 8, 17, 12, 3, 1, 1, 9), (3, 64, 13, 100, 3, 1, 1, 1), (2, 68, 9, 40, 1, 1, 0, 4),

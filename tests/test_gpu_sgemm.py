@@ -156,14 +156,17 @@ CHAIN_SHAPES = [(1, 1, 1), (3, 5, 9), (33, 65, 15), (37, 53, 61), (32, 27, 2704)
 @pytest.mark.parametrize("M,N,K", CHAIN_SHAPES)
 def test_nt_sdot_every_form_bit_exact(hip, torch_cuda, ora, M, N, K):
     """Every kernel of the sdot-order NT product (TNS_OPT_SDOT_FORM: the MFMA
-    kernel and each VALU chain variant, sgemm_sdot_chains.hip) gives the
+    kernel, each VALU chain variant, sgemm_sdot_chains.hip, and each
+    residue-register form, sgemm_sdot_rc.hip) gives the
     reference's s_nt/sdot_avx2 result bit for bit: K mod 8 tails, K not a
     multiple of 4 (scalar staging), ragged tiles, every beta mode."""
     rng = np.random.default_rng(M * 5 + N * 7 + K + 1)
     A, B, C0 = operands(rng, 0, 1, M, N, K)
     refs = {ab: run_ref(ora, 0, 1, A, B, C0, *ab) for ab in [(1.0, 0.0), (0.5, 2.0), (1.0, 1.0)]}
     try:
-        for form in range(hip.sdotChainsVariants() + 1):
+        forms = list(range(hip.sdotChainsVariants() + 1))
+        forms += [64 + v for v in range(hip.sdotRcVariants())]
+        for form in forms:
             hip.setSdotForm(form)
             for (alpha, beta), ref in refs.items():
                 got = run_dev(hip, torch_cuda, 0, 1, A, B, C0, alpha, beta)
@@ -186,7 +189,9 @@ def test_nt_sdot_chains_batched_offsets(hip, torch_cuda, ora):
                             N * ldb, 1.0, ref[off:], N, M * N, batch)
     dA, dB = (torch_cuda.from_numpy(x.copy()).cuda() for x in (A, B))
     try:
-        for form in range(1, hip.sdotChainsVariants() + 1):
+        forms = list(range(1, hip.sdotChainsVariants() + 1))
+        forms += [64 + v for v in range(hip.sdotRcVariants())]
+        for form in forms:
             hip.setSdotForm(form)
             dC = torch_cuda.from_numpy(C.copy()).cuda()
             hip.gemmStridedBatched(False, True, M, N, K, 0.5, dA, off, lda, M * lda, dB, off, ldb,
