@@ -46,13 +46,15 @@ def main():
     # the dominant kernel: the 4096^3 launches (grid of 256 blocks x 512 thr)
     def is_main(name):
         return ("sgemm_nn_big_kernel" in name and "Geo<256, 256, 2, 4" in name) or \
+            "sgemm_nn_pp_kernel" in name or \
             ("sgemm_mfma_kernel" in name and "Shape<256, 256, 32, 2, 4" in name)
 
     # kernel duration from the trace (same command, not profiled with PMC)
-    durs = []
+    durs, names = [], set()
     for r in csv.DictReader(open(src / "trace" / "trace_kernel_trace.csv")):
         if is_main(r["Kernel_Name"]) and int(r["Grid_Size_X"]) == 131072:
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+            names.add(r["Kernel_Name"])
     fetch = rows(src / "fetch" / "fetch_counter_collection.csv", is_main).get("FETCH_SIZE", [])
     write = rows(src / "write" / "write_counter_collection.csv", is_main).get("WRITE_SIZE", [])
     mf = rows(src / "mfma" / "mfma_counter_collection.csv", is_main)
@@ -67,7 +69,7 @@ def main():
     flop = 2.0 * size ** 3
     alg = 3 * size * size * 4
     out = {
-        "tag": tag, "size": size, "kernel": "sgemm_nn_big_kernel<Geo<256,256,2,4,1>> (NN, 256x256x32, 8 waves)",
+        "tag": tag, "size": size, "kernel": sorted(names)[0] if len(names) == 1 else sorted(names),
         "launches_traced": len(durs),
         "kernel_ms_mean": round(st.mean(durs), 4), "kernel_ms_min": round(min(durs), 4),
         # bench.py's timed launches are the last --steps of the warm-up+steps
