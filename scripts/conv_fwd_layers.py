@@ -10,6 +10,7 @@ per layer the shape, ms, TFLOP/s and its share of the sum; run under
 import argparse
 import json
 import sys
+import time
 from pathlib import Path
 
 import torch
@@ -26,6 +27,8 @@ def main():
     ap.add_argument("--pad", type=int, default=-1, help="TNS_OPT_CONV_PAD (-1: heuristic)")
     ap.add_argument("--variant", type=int, default=-1, help="TNS_OPT_CONV_VARIANT (-1: heuristic)")
     ap.add_argument("--layers", default="", help="comma-separated layer indices (default: all)")
+    ap.add_argument("--warm-ms", type=float, default=0.0,
+                    help="run each layer back-to-back this long before timing it")
     a = ap.parse_args()
     hip = TNNHip(0)
     hip.setConvPad(a.pad)
@@ -45,6 +48,12 @@ def main():
         for _ in range(3):
             run()
         torch.cuda.synchronize()
+        if a.warm_ms > 0:  # hold the GPU busy first: the clock ramps over ~20 ms of load
+            t_end = time.perf_counter() + a.warm_ms / 1e3
+            while time.perf_counter() < t_end:
+                for _ in range(10):
+                    run()
+                torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.reps):

@@ -120,6 +120,48 @@ __global__ __launch_bounds__(512, 1) void m32_lds(float* out, float x) {
   out[blockIdx.x * 512 + threadIdx.x] = r;
 }
 
+
+// m16_lds4: conv_tile's wave loop with k-permuted LDS images: one
+// ds_read_b128 per operand fragment feeds 4 MFMA steps (12 reads per 44 MFMAs)
+__global__ __launch_bounds__(512, 1) void m16_lds4(float* out, float x) {
+  __shared__ float lds[32 * 192 + 32 * 144];
+  for (int i = threadIdx.x; i < 32 * 336; i += 512) lds[i] = x * i;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, r16 = lane & 15, q = lane >> 4, wm = threadIdx.x >> 6;
+  floatx4 acc[11];
+  for (int j = 0; j < 11; ++j) acc[j] = floatx4{0, 0, 0, 0};
+  auto frag = [&](int s, float4& a, float4 (&b)[11]) {
+    const int kq = (s & 1) * 4 + q;  // k-quad row
+    a = *reinterpret_cast<const float4*>(lds + kq * 576 + 4 * ((wm * 16 + r16) ^ (s & 1)));
+    const float* bp = lds + 32 * 144 + kq * 768 + 4 * r16;
+#pragma unroll
+    for (int j = 0; j < 11; ++j) b[j] = *reinterpret_cast<const float4*>(bp + 64 * j);
+  };
+  float4 a0, b0[11], a1, b1[11];
+  frag(0, a0, b0);
+  auto mm = [&](const float4& a, const float4 (&b)[11]) {
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[j].x, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[j].y, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[j].z, acc[j], 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[j].w, acc[j], 0, 0, 0);
+  };
+  for (int s = 0; s < STEPS / 4; s += 2) {
+    frag(s + 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a0, b0);
+    frag(s + 2, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a1, b1);
+  }
+  float r = 0;
+  for (int j = 0; j < 11; ++j) r += acc[j][0] + acc[j][3];
+  out[blockIdx.x * 512 + threadIdx.x] = r;
+}
+
 template <class F>
 void run(const char* name, F kernel, double flop_per_wave, float* out) {
   hipEvent_t e0, e1;
@@ -145,6 +187,7 @@ int main() {
   const double f32 = 2.0 * 32 * 32 * 2 * 8 * (STEPS / 2);     // per wave
   run("m16_regs", m16_regs, f16, out);
   run("m16_lds", m16_lds, f16, out);
+  run("m16_lds4", m16_lds4, f16, out);
   run("m32_regs", m32_regs, f32, out);
   run("m32_lds", m32_lds, f32, out);
   (void)hipFree(out);

@@ -320,11 +320,17 @@ const TileInfo kTiles[] = {
 };
 #undef TNS_CT
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+// the conv_tile4.hip forms picked by default
+constexpr int kT4Big = 3;    // 128 x 176 x 64, stores after group 1 and reads interleaved
+constexpr int kT4Small = 8;  // 64 x 96 x 32, reads interleaved
 
 }  // namespace
 
-int conv_tile_count() { return kNumTiles; }
-const char* conv_tile_name(int v) { return v >= 0 && v < kNumTiles ? kTiles[v].name : ""; }
+// variants kNumTiles + v: conv_tile4.hip's form v (k-permuted b128 fragments)
+int conv_tile_count() { return kNumTiles + conv_tile4_count(); }
+const char* conv_tile_name(int v) {
+  return v >= 0 && v < kNumTiles ? kTiles[v].name : conv_tile4_name(v - kNumTiles);
+}
 
 // Measured per YOLOv3 layer shape (scripts/conv_tile_sweep.py, profiles/
 // r02_conv_tile_sweep.json): the 8-wave 128 x 176 tile beats the
@@ -333,15 +339,25 @@ const char* conv_tile_name(int v) { return v >= 0 && v < kNumTiles ? kTiles[v].n
 // 3x3 layers by ~2 %; everywhere else (1x1, the 13^2 / 26^2 layers with 512 /
 // 1024 filters over K = 2304 / 4608) the older shapes stay ahead; stride-2
 // 128/256-filter layers are a tie.  -1: not this kernel.
+//
+// Round 3: the conv_tile4.hip forms (k-permuted ds_read_b128 fragments) of the
+// same tiles, measured at a held clock (scripts/conv_fwd_layers.py --warm-ms,
+// profiles/r03_conv_tile4.json): 128 x 176 x 64 with interleaved stores and
+// reads 10-11 % ahead on the 128 / 256-filter 3x3 layers of either stride
+// (52^2 0.127 -> 0.115 ms, 104^2 0.138 -> 0.123), 64 x 96 x 32 13 % ahead on
+// the 64-filter ones (208^2 0.166 -> 0.145); the 512 / 1024-filter layers
+// keep the multi-block sgemm_kernel.hpp tiles.
 int conv_tile_pick(const GemmArgs& a, int ks) {
   if (ks != 3 || a.K % BK || a.lda % 4 || (reinterpret_cast<uintptr_t>(a.A) & 15)) return -1;
+  if ((a.M == 128 || a.M == 256) && a.K % conv_tile4_bk(kT4Big) == 0) return kNumTiles + kT4Big;
   if ((a.M == 128 || a.M == 256) && a.conv_sY == 1) return 0;  // (stride 2: a tie)
-  if (a.M == 64) return 1;
+  if (a.M == 64) return kNumTiles + kT4Small;
   return -1;
 }
 
 hipError_t launch_conv_tile(int v, const GemmArgs& a, int ks, int dil, hipStream_t s) {
-  if (v < 0 || v >= kNumTiles) return hipErrorInvalidValue;
+  if (v >= kNumTiles) return launch_conv_tile4(v - kNumTiles, a, ks, dil, s);
+  if (v < 0) return hipErrorInvalidValue;
   return kTiles[v].fn(a, ks, dil, s);
 }
 

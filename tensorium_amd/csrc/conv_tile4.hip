@@ -1,0 +1,456 @@
+// conv_tile4.hip — conv_tile.hip's plane-sized implicit-GEMM convolution with
+// k-permuted LDS images: one ds_read_b128 per operand fragment feeds four
+// v_mfma_f32_16x16x4_f32 steps (TConvolutionalLayer.forward → Conv2D +
+// forwardBias + activate after fuseBatchNorm: nConvolutionLayer.pas:457-569,
+// ntensors.pas:8252-8349; sim2Col's column order, 11415-11532).
+//
+// Same arithmetic as conv_tile.hip (each output an ascending-k fma chain over
+// k = (c, kr, kc) from +0 in the 16x16x4 lane-quarter order, then bias add
+// and activation, each rounded once), so bit-identical to it and to sim2Col +
+// the reference GEMM.  What changes is how the operands reach the MFMAs:
+//
+//   * MFMA step s of a k-tile consumes k = 4s + q (lane quarter q).  Steps
+//     4g .. 4g+3 form group g; a lane's four values of one group sit in one
+//     16-byte LDS slot: image row 4g + q, slot = column, component i holds
+//     k = 16g + 4i + q.  A wave reads 1 A slot + J B slots per group (12
+//     ds_read_b128 per 44 MFMAs on the 128x176 tile, against 12 ds_read_b32
+//     per 11 MFMAs): the bare wave loop measured 0.968 of the MFMA peak in
+//     this form against 0.857 with per-step b32 reads (scripts/mfma_probe.hip).
+//     Row strides are multiples of 64 dwords, so the b128 reads are
+//     conflict-free;
+//   * B is gathered as in conv_tile (lanes of a quarter take 16 consecutive
+//     output pixels of one k, out-of-window taps read 0 through the buffer
+//     range check), but a lane quarter takes the component i, not q, so the
+//     transposing ds_write_b32 stores are 2-way (free); each column's window
+//     validity is a 9-bit tap mask computed once, one bfe per element;
+//   * A (weights, k-contiguous) float4 loads are spread into the four slot
+//     rows of their k-quad (2-way stores, no swizzle needed);
+//   * one barrier per k-tile, placed before the last group's MFMAs: the next
+//     tile's first fragments are read right after it, under those MFMAs, so
+//     no LDS latency is exposed at the tile boundary; the next tile's global
+//     loads are issued at the top of a tile and stored after group SG.
+#include <type_traits>
+
+#include "tns_act.hpp"
+#include "tns_internal.hpp"
+
+namespace tns {
+namespace {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
+          int RI_ = 0, bool ST_ = false>
+struct Geo4 {
+  // WM x WN waves, each a 16-row strip of BN / WN columns
+  static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_, SG = SG_;
+  // instruction placement (sched_group_barrier) inside each group's MFMAs:
+  //   IL > 0: the next tile's loads and their address arithmetic in group 0
+  //           (IL VALU per MFMA) instead of a block at the tile top
+  //   SI:     the LDS stores of the next tile in group SG, one per MFMA,
+  //           instead of a block after it
+  //   RI > 0: the next group's fragment reads one per RI MFMAs instead of a
+  //           block in front of them
+  //   ST:     staging staggered by wave half (waves w and w + NW/2 share a
+  //           SIMD): half h issues its loads in front of group h's MFMAs and
+  //           stores after group SG + h, so one wave of a SIMD runs MFMAs
+  //           while the other stages
+  static constexpr int IL = IL_, RI = RI_;
+  static constexpr bool SI = SI_, ST = ST_;
+  static constexpr int NW = WM * WN, NT = 64 * NW;
+  static constexpr int J = BN / 16;             // 16-column fragments of the tile
+  static constexpr int JW = J / WN;             // ... of one wave
+  static constexpr int NG = BK / 16;            // 4-step groups per k-tile
+  static constexpr int ROWS = BK / 4;           // slot rows per image (4g + q)
+  static constexpr int A_TILE = ROWS * BM * 4;  // floats
+  static constexpr int STAGE = ROWS * (BM + BN) * 4;
+  static constexpr int AU = BM * BK / 4 / NT;   // float4 A units per thread
+  static constexpr int KI = BK / 4 / NW;        // B k-slots per thread
+  static_assert(BM == 16 * WM, "one 16-row strip per wave");
+  static_assert(BM % 16 == 0 && BN % 16 == 0, "b128 slot rows: 64-dword multiples");
+  static_assert(BK % 16 == 0 && SG <= NG - 2, "stores precede the barrier");
+  static_assert(!(IL && SI) || SG >= 1, "interleaved stores need a group after the loads");
+  static_assert(!ST || (!IL && !SI && SG + 1 <= NG - 2 && NW % 2 == 0), "staggered staging");
+  static_assert(AU >= 1 && BM * BK / 4 % NT == 0 && KI >= 1 && BK / 4 % NW == 0 && J % WN == 0,
+                "geometry");
+  static_assert(2 * STAGE * 4 <= 163840, "LDS");
+};
+
+template <class G, int KS>
+__global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) {
+  constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, JW = G::JW, NG = G::NG;
+  constexpr int A_TILE = G::A_TILE, STAGE = G::STAGE, AU = G::AU, KI = G::KI;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w % G::WM, wn = w / G::WM;
+  const int half = __builtin_amdgcn_readfirstlane(w >= G::NW / 2 ? 1 : 0);  // (ST)
+  const int r16 = lane & 15, q = lane >> 4;
+  const int tiles_m = (int)(p.M / BM);
+  // XCD-contiguous order, column tiles outer (blocks of one XCD share the
+  // images' rows in its L2); tile rows inner
+  int tm, tn;
+  {
+    const int nb = gridDim.x, bid = blockIdx.x;
+    const int xcd = bid & 7, qq = nb >> 3, rr = nb & 7;
+    const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    tm = wg % tiles_m;
+    tn = wg / tiles_m;
+  }
+  const int64_t m0 = (int64_t)tm * BM;
+  const int n0 = tn * BN;
+  const int N = (int)p.N, K = (int)p.K;
+  const int H = p.conv_H, W = p.conv_W, HW = H * W;
+
+  // ---- per-column state: window origin and the 9-bit tap validity mask ----
+  unsigned vbase[J], tmask[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    int n = n0 + 16 * j + r16;
+    n = n < N ? n : N - 1;  // past N: any valid pixel, never stored
+    const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
+    const int orow = pix / p.conv_ow, ocol = pix - orow * p.conv_ow;
+    const int ir0 = orow * p.conv_sY - p.conv_pH, ic0 = ocol * p.conv_sX - p.conv_pW;
+    vbase[j] = 4u * (unsigned)(img * (int)p.strideB + ir0 * W + ic0);
+    unsigned m = 0;
+#pragma unroll
+    for (int kr = 0; kr < KS; ++kr)
+#pragma unroll
+      for (int kc = 0; kc < KS; ++kc)
+        m |= (unsigned)(((unsigned)(ir0 + kr * dil) < (unsigned)H) &
+                        ((unsigned)(ic0 + kc * dil) < (unsigned)W))
+             << (kr * KS + kc);
+    tmask[j] = m;
+  }
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.B), 0, p.conv_bytes, 0x00020000);
+
+  // ---- B k-slots: slot sl = wm*KI + ii = 4g + r takes k = 16g + 4q + r (the
+  // lane quarter is the slot component), advanced by BK per tile -------------
+  int kc_[KI], kr_[KI], cc_[KI];
+#pragma unroll
+  for (int ii = 0; ii < KI; ++ii) {
+    const int sl = w * KI + ii;
+    const int k = 16 * (sl >> 2) + 4 * q + (sl & 3);
+    cc_[ii] = k / (KS * KS);
+    const int rem = k - cc_[ii] * KS * KS;
+    kr_[ii] = rem / KS;
+    kc_[ii] = rem - kr_[ii] * KS;
+  }
+  auto advance = [&]() {  // k += BK
+#pragma unroll
+    for (int ii = 0; ii < KI; ++ii) {
+      if constexpr (KS == 1) {
+        cc_[ii] += BK;
+      } else {
+        constexpr int DC = BK / (KS * KS), DR = BK % (KS * KS);
+        int rem = kr_[ii] * KS + kc_[ii] + DR;
+        int c = cc_[ii] + DC;
+        if (rem >= KS * KS) { rem -= KS * KS; ++c; }
+        cc_[ii] = c;
+        kr_[ii] = rem >= 2 * KS ? 2 : (rem >= KS ? 1 : 0);
+        kc_[ii] = rem - kr_[ii] * KS;
+      }
+    }
+  };
+  float rb[KI][J];
+  auto gather_b = [&]() {
+#pragma unroll
+    for (int ii = 0; ii < KI; ++ii) {
+      const int y = kr_[ii] * dil, z = kc_[ii] * dil;
+      const unsigned x = 4u * (unsigned)(cc_[ii] * HW + y * W + z);
+      const int tap = kr_[ii] * KS + kc_[ii];
+#pragma unroll
+      for (int j = 0; j < J; ++j) {
+        const bool ok = __builtin_amdgcn_ubfe(tmask[j], tap, 1) != 0;
+        const unsigned off = ok ? vbase[j] + x : 0x80000000u;
+        rb[ii][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+      }
+    }
+  };
+  // slot (row 4g + r, column n), component q
+  int b_dst[KI];
+#pragma unroll
+  for (int ii = 0; ii < KI; ++ii) b_dst[ii] = (w * KI + ii) * BN * 4 + r16 * 4 + q;
+  auto store_b = [&](float* bs) {
+#pragma unroll
+    for (int ii = 0; ii < KI; ++ii)
+#pragma unroll
+      for (int j = 0; j < J; ++j) bs[b_dst[ii] + 64 * j] = rb[ii][j];
+  };
+
+  // ---- A staging (weights [M][K]): unit = k-quad kq4 of row m; its four
+  // values go to rows 4g + 0..3, component i = kq4 & 3 (g = kq4 >> 2) --------
+  const float* a_src[AU];
+  int a_dst[AU];
+#pragma unroll
+  for (int u = 0; u < AU; ++u) {
+    const int idx = tid + G::NT * u;
+    // 8 k-quads of one row per 8 lanes (128 contiguous bytes per row)
+    const int lo = idx & 7, rest = idx >> 3;
+    const int m = rest % BM, kq4 = lo + 8 * (rest / BM);
+    a_src[u] = p.A + (m0 + m) * p.lda + 4 * kq4;
+    a_dst[u] = (4 * (kq4 >> 2)) * BM * 4 + m * 4 + (kq4 & 3);
+  }
+  float4 ra[AU];
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < AU; ++u) ra[u] = *reinterpret_cast<const float4*>(a_src[u] + k0);
+  };
+  auto store_a = [&](float* as) {
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      as[a_dst[u]] = ra[u].x;
+      as[a_dst[u] + BM * 4] = ra[u].y;
+      as[a_dst[u] + 2 * BM * 4] = ra[u].z;
+      as[a_dst[u] + 3 * BM * 4] = ra[u].w;
+    }
+  };
+
+  // ---- MFMA: group g, step i consumes k = 16g + 4i + q ----------------------
+  floatx4 acc[JW];
+#pragma unroll
+  for (int j = 0; j < JW; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  struct Frag {
+    floatx4 a, b[JW];
+  };
+  auto frag = [&](const float* st, int g, Frag& f) {
+    const float* ap = st + ((4 * g + q) * BM + wm * 16 + r16) * 4;
+    f.a = *reinterpret_cast<const floatx4*>(ap);
+    const float* bp = st + A_TILE + ((4 * g + q) * BN + wn * 16 * JW + r16) * 4;
+#pragma unroll
+    for (int j = 0; j < JW; ++j) f.b[j] = *reinterpret_cast<const floatx4*>(bp + 64 * j);
+  };
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < JW; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[i], f.b[j][i], acc[j], 0, 0, 0);
+  };
+
+#ifdef TNS_CT4_STAMPS
+  // diagnostic build only: per-phase cycle sums of wave 0 (tile top / groups
+  // before the stores / stores / up to the barrier / last group)
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tl = __builtin_amdgcn_s_memtime();
+  const unsigned long long tk0 = tl, rt0 = __builtin_amdgcn_s_memrealtime();
+#define TNS_PH(i)                                                   \
+  do {                                                              \
+    const unsigned long long tn_ = __builtin_amdgcn_s_memtime();    \
+    ph[i] += tn_ - tl;                                              \
+    tl = tn_;                                                       \
+  } while (0)
+#else
+#define TNS_PH(i) \
+  do {            \
+  } while (0)
+#endif
+  const int nt = K / BK;
+  Frag f0, f1;
+  if (nt > 0) {
+    load_a(0);
+    gather_b();
+    store_a(smem);
+    store_b(smem + A_TILE);
+    __syncthreads();
+    frag(smem, 0, f0);
+  }
+  auto tile = [&](int t, auto MORE) {
+    constexpr bool more = decltype(MORE)::value;
+    const float* cur = smem + (t & 1) * STAGE;
+    float* nxt = smem + ((t + 1) & 1) * STAGE;
+    TNS_PH(5);
+    if constexpr (more && !G::IL && !G::ST) {
+      advance();
+      load_a((t + 1) * BK);
+      gather_b();
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
+    }
+    TNS_PH(0);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      Frag& fc = (g & 1) ? f1 : f0;
+      Frag& fn = (g & 1) ? f0 : f1;
+      if constexpr (more)
+        if (g == NG - 1) {
+          // every wave's stores of tile t+1 are in; its first group is read
+          // under this group's MFMAs
+          TNS_PH(3);
+          __syncthreads();
+          TNS_PH(4);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (more && G::ST)
+        if (g < 2 && half == g) {
+          advance();
+          load_a((t + 1) * BK);
+          gather_b();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      // one scheduling region per group: the next group's fragment reads,
+      // interleaved staging (LI / SI) and this group's MFMAs
+      const bool reads = g + 1 < NG || more;
+      if (g + 1 < NG)
+        frag(cur, g + 1, fn);
+      else if (more)
+        frag(nxt, 0, fn);
+      if constexpr (more && G::IL) {
+        if (g == 0) {
+          advance();
+          load_a((t + 1) * BK);
+          gather_b();
+        }
+      }
+      if constexpr (more && G::SI) {
+        if (g == G::SG) {
+          store_a(nxt);
+          store_b(nxt + A_TILE);
+        }
+      }
+      mma(fc);
+      if constexpr (G::RI > 0 || G::IL > 0 || G::SI) {
+#pragma unroll
+        for (int i = 0; i < 4 * JW; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+          if constexpr (G::RI > 0)
+            if (reads && i % G::RI == 0 && i / G::RI < JW + 1)
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // a fragment read
+          if constexpr (more && G::IL > 0)
+            if (g == 0) {
+              __builtin_amdgcn_sched_group_barrier(0x002, G::IL, 0);  // IL VALU
+              if (i < AU + KI * J) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // a load
+            }
+          if constexpr (more && G::SI)
+            if (g == G::SG && i < 4 * AU + KI * J)
+              __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // a store
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (more && G::ST)
+        if (g >= G::SG && g <= G::SG + 1 && g == G::SG + half) {
+          store_a(nxt);
+          store_b(nxt + A_TILE);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      if constexpr (more && !G::SI && !G::ST)
+        if (g == G::SG) {
+          TNS_PH(1);
+          store_a(nxt);
+          store_b(nxt + A_TILE);
+          __builtin_amdgcn_sched_barrier(0);
+          TNS_PH(2);
+        }
+    }
+  };
+  static_assert(NG % 2 == 0, "f0 holds group 0 at every tile start");
+  for (int t = 0; t + 1 < nt; ++t) tile(t, std::true_type{});
+  if (nt > 0) tile(nt - 1, std::false_type{});
+
+#ifdef TNS_CT4_STAMPS
+  TNS_PH(5);
+  if (tid == 0 && p.stamps != nullptr && blockIdx.x < (1u << 16)) {
+    unsigned* st = p.stamps + 8 * blockIdx.x;
+    for (int i = 0; i < 6; ++i) st[i] = (unsigned)ph[i];
+    st[6] = (unsigned)(tl - tk0);
+    st[7] = (unsigned)nt | (unsigned)(__builtin_amdgcn_s_memrealtime() - rt0) << 8;
+  }
+#endif
+#undef TNS_PH
+  // ---- epilogue: forwardBias + activate, conv output [img][filter][pixel] --
+  const bool fuse = p.epi == EPI_BIAS_ACT;
+  const int act = p.act;
+  const int64_t row0 = m0 + wm * 16 + 4 * q;
+  float bias[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bias[e] = fuse ? p.bias[row0 + e] : 0.0f;
+#pragma unroll
+  for (int j = 0; j < JW; ++j) {
+    const int n = n0 + wn * 16 * JW + 16 * j + r16;
+    if (n >= N) continue;
+    const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
+    float* cp = p.C + (int64_t)img * p.strideC + pix + row0 * p.ldc;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = acc[j][e];
+      if (fuse) v = act_apply_cheap(v + bias[e], act);
+      cp[e * p.ldc] = v;
+    }
+  }
+}
+
+#ifdef TNS_CT4_STAMPS
+unsigned* g_ct4_stamps = nullptr;
+#endif
+
+template <class G>
+hipError_t launch_g4(const GemmArgs& a_in, int ks, int dil, hipStream_t s) {
+  GemmArgs a = a_in;
+#ifdef TNS_CT4_STAMPS
+  a.stamps = g_ct4_stamps;
+#endif
+  if (a.M % G::BM || a.K % G::BK || a.K <= 0 || a.lda % 4 ||
+      (reinterpret_cast<uintptr_t>(a.A) & 15))
+    return hipErrorInvalidValue;
+  const int64_t tiles = (a.M / G::BM) * ((a.N + G::BN - 1) / G::BN);
+  if (tiles > 0x7fffffff || a.N > 0x7fffffff || a.K > 0x7fffffff) return hipErrorInvalidValue;
+  if (ks == 3)
+    hipLaunchKernelGGL((conv_tile4_kernel<G, 3>), dim3((unsigned)tiles), dim3(G::NT), 0, s, a, dil);
+  else if (ks == 1)
+    hipLaunchKernelGGL((conv_tile4_kernel<G, 1>), dim3((unsigned)tiles), dim3(G::NT), 0, s, a, dil);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+struct TileInfo4 {
+  int bm, bn, bk;
+  hipError_t (*fn)(const GemmArgs&, int, int, hipStream_t);
+  const char* name;
+};
+#define TNS_CT4(BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, STv)                      \
+  {BMv, BNv, BKv, launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, STv>>,    \
+   "conv_tile4<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si" #SIv \
+   ",ri" #RIv ",st" #STv ">"}
+const TileInfo4 kTiles4[] = {
+    TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
+    TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
+    TNS_CT4(128, 176, 8, 1, 64, 1, 0, true, 3, false),   // 2: stores and reads interleaved
+    TNS_CT4(128, 176, 8, 1, 64, 1, 0, true, 2, false),   // 3
+    TNS_CT4(128, 176, 8, 1, 64, 1, 0, false, 3, true),   // 4: staggered halves
+    TNS_CT4(128, 176, 8, 1, 64, 1, 0, false, 0, true),   // 5
+    TNS_CT4(128, 176, 8, 1, 64, 1, 0, false, 2, true),   // 6
+    TNS_CT4(64, 96, 4, 1, 32, 0, 0, false, 0, false),    // 7
+    TNS_CT4(64, 96, 4, 1, 32, 0, 0, false, 3, false),    // 8
+    TNS_CT4(64, 192, 4, 2, 64, 1, 0, false, 3, true),    // 9
+    TNS_CT4(64, 96, 4, 2, 64, 1, 0, false, 3, true),     // 10
+    // multi-block tiles for the 512 / 1024-filter layers (26^2, 13^2 planes)
+    TNS_CT4(64, 64, 4, 2, 32, 0, 0, false, 0, false),    // 11
+    TNS_CT4(64, 64, 4, 1, 32, 0, 0, false, 0, false),    // 12
+    TNS_CT4(64, 32, 4, 1, 32, 0, 0, false, 0, false),    // 13
+    TNS_CT4(64, 32, 4, 2, 32, 0, 0, false, 0, false),    // 14
+    TNS_CT4(64, 64, 4, 1, 64, 2, 0, false, 0, false),    // 15
+    TNS_CT4(64, 32, 4, 1, 64, 2, 0, false, 0, false),    // 16
+};
+#undef TNS_CT4
+constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
+
+}  // namespace
+
+int conv_tile4_count() { return kNumTiles4; }
+const char* conv_tile4_name(int v) { return v >= 0 && v < kNumTiles4 ? kTiles4[v].name : ""; }
+int conv_tile4_bk(int v) { return v >= 0 && v < kNumTiles4 ? kTiles4[v].bk : 0; }
+
+#ifdef TNS_CT4_STAMPS
+// diagnostic build only (not in include/tns.h): per-block phase cycle sums
+// of wave 0 into dev_buf (8 words per block), or nothing when NULL
+extern "C" int tns_debug_ct4_stamps(unsigned* dev_buf) {
+  g_ct4_stamps = dev_buf;
+  return 0;
+}
+#endif
+
+hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStream_t s) {
+  if (v < 0 || v >= kNumTiles4) return hipErrorInvalidValue;
+  return kTiles4[v].fn(a, ks, dil, s);
+}
+
+}  // namespace tns

@@ -119,6 +119,13 @@ int conv_tile_count();
 const char* conv_tile_name(int v);
 int conv_tile_pick(const GemmArgs& a, int ks);
 hipError_t launch_conv_tile(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
+// the same tiles with k-permuted LDS images read by ds_read_b128
+// (conv_tile4.hip; K % the form's k-tile == 0): conv_tile variants
+// conv_tile_count() - conv_tile4_count() + v
+int conv_tile4_count();
+const char* conv_tile4_name(int v);
+int conv_tile4_bk(int v);
+hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
 // implicit-GEMM convolution on the ping-pong schedule (conv_pp.hip): same
 // operands and limits as conv_tile; conv_pp_pick = -1 where not measured faster
 int conv_pp_count();

@@ -411,7 +411,10 @@ def test_conv_backward_rejects_dilation(hip, torch_cuda):
 TILE_CASES = [
     (2, 32, 17, 128, 3, 1, 1, 9, 1), (3, 32, 12, 64, 3, 2, 1, 9, 1), (2, 64, 9, 32, 1, 1, 0, 4, 1),
     (1, 96, 26, 128, 3, 2, 1, 1, 1), (2, 32, 13, 256, 3, 1, 1, 0, 1), (2, 32, 21, 64, 3, 1, 2, 9, 2),
-    (1, 32, 40, 32, 3, 1, 1, 9, 1)]
+    (1, 32, 40, 32, 3, 1, 1, 9, 1),
+    # K % 64 == 0 (the 64-deep k-tiles of conv_tile4.hip), 1x1 and 3x3
+    (2, 64, 13, 128, 3, 1, 1, 9, 1), (1, 128, 11, 256, 3, 2, 1, 1, 1), (2, 128, 9, 128, 1, 1, 0, 4, 1),
+    (1, 64, 20, 64, 3, 1, 2, 9, 2)]
 
 
 def test_conv_tile_variants_bit_exact(hip, torch_cuda, ora):
