@@ -323,6 +323,8 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 // the conv_tile4.hip forms picked by default
 constexpr int kT4Big = 3;    // 128 x 176 x 64, stores after group 1 and reads interleaved
 constexpr int kT4Small = 8;  // 64 x 96 x 32, reads interleaved
+constexpr int kT4OneByOne = 13;  // 64 x 32 x 32, 4 waves (1x1 layers)
+constexpr int kT4Uneven = 18;    // 64 x 176 x 32, wave columns 6 + 5 fragments
 
 }  // namespace
 
@@ -348,10 +350,20 @@ const char* conv_tile_name(int v) {
 // the 64-filter ones (208^2 0.166 -> 0.145); the 512 / 1024-filter layers
 // keep the multi-block sgemm_kernel.hpp tiles.
 int conv_tile_pick(const GemmArgs& a, int ks) {
-  if (ks != 3 || a.K % BK || a.lda % 4 || (reinterpret_cast<uintptr_t>(a.A) & 15)) return -1;
+  if (a.K % BK || a.lda % 4 || (reinterpret_cast<uintptr_t>(a.A) & 15)) return -1;
+  // 1x1 layers with 64..256 filters over >= 5408 pixels: the 64 x 32 form
+  // (104^2 0.029 -> 0.022 ms, 52^2 0.023 -> 0.021, 26^2 0.023 -> 0.020); the
+  // 512-filter 13^2 ones keep the sgemm_kernel.hpp tiles
+  if (ks == 1)
+    return a.M % 64 == 0 && a.M <= 256 && a.N >= 5408 ? kNumTiles + kT4OneByOne : -1;
+  if (ks != 3) return -1;
   if ((a.M == 128 || a.M == 256) && a.K % conv_tile4_bk(kT4Big) == 0) return kNumTiles + kT4Big;
   if ((a.M == 128 || a.M == 256) && a.conv_sY == 1) return 0;  // (stride 2: a tie)
   if (a.M == 64) return kNumTiles + kT4Small;
+  // 512 filters (the 26^2 layers and the 52^2 -> 26^2 stride-2 one): 64 x 176
+  // with wave columns of 6 + 5 fragments, 8 x 31 blocks (warm clock 0.137 ->
+  // 0.128 ms, stride 2 0.151 -> 0.134)
+  if (a.M == 512) return kNumTiles + kT4Uneven;
   return -1;
 }
 

@@ -39,10 +39,19 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// one group's fragments of a wave: the A slot and JW B slots (4 steps each)
+template <int JW>
+struct Frag4 {
+  floatx4 a, b[JW];
+};
+
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
-          int RI_ = 0, bool ST_ = false>
+          int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0>
 struct Geo4 {
-  // WM x WN waves, each a 16-row strip of BN / WN columns
+  // WM x WN waves, each a 16-row strip of BN / WN columns; or, with JA > 0,
+  // wave columns 0..NA-1 of JA 16-column fragments and the rest of JB (176 =
+  // 6 + 5 fragments: waves w and w + NW/2 share a SIMD, so a SIMD's two waves
+  // carry 11 fragments either way)
   static constexpr int BM = BM_, BN = BN_, WM = WM_, WN = WN_, BK = BK_, SG = SG_;
   // instruction placement (sched_group_barrier) inside each group's MFMAs:
   //   IL > 0: the next tile's loads and their address arithmetic in group 0
@@ -59,7 +68,9 @@ struct Geo4 {
   static constexpr bool SI = SI_, ST = ST_;
   static constexpr int NW = WM * WN, NT = 64 * NW;
   static constexpr int J = BN / 16;             // 16-column fragments of the tile
-  static constexpr int JW = J / WN;             // ... of one wave
+  static constexpr int JA = JA_ > 0 ? JA_ : J / WN;  // ... of one wave (columns < NA)
+  static constexpr int NA = JA_ > 0 ? NA_ : WN;
+  static constexpr int JB = NA < WN ? (J - NA * JA) / (WN - NA) : 0;  // ... of the others
   static constexpr int NG = BK / 16;            // 4-step groups per k-tile
   static constexpr int ROWS = BK / 4;           // slot rows per image (4g + q)
   static constexpr int A_TILE = ROWS * BM * 4;  // floats
@@ -71,14 +82,14 @@ struct Geo4 {
   static_assert(BK % 16 == 0 && SG <= NG - 2, "stores precede the barrier");
   static_assert(!(IL && SI) || SG >= 1, "interleaved stores need a group after the loads");
   static_assert(!ST || (!IL && !SI && SG + 1 <= NG - 2 && NW % 2 == 0), "staggered staging");
-  static_assert(AU >= 1 && BM * BK / 4 % NT == 0 && KI >= 1 && BK / 4 % NW == 0 && J % WN == 0,
-                "geometry");
+  static_assert(AU >= 1 && BM * BK / 4 % NT == 0 && KI >= 1 && BK / 4 % NW == 0, "geometry");
+  static_assert(NA * JA + (WN - NA) * JB == J && NA >= 1 && NA <= WN, "wave column split");
   static_assert(2 * STAGE * 4 <= 163840, "LDS");
 };
 
 template <class G, int KS>
 __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) {
-  constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, JW = G::JW, NG = G::NG;
+  constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, NG = G::NG;
   constexpr int A_TILE = G::A_TILE, STAGE = G::STAGE, AU = G::AU, KI = G::KI;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
@@ -206,17 +217,18 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   };
 
-  // ---- MFMA: group g, step i consumes k = 16g + 4i + q ----------------------
+  // ---- MFMA: group g, step i consumes k = 16g + 4i + q; the main loop and
+  // epilogue for a wave of JW fragments from fragment column coff ------------
+  auto run = [&](auto JWC, const int coff) {
+  constexpr int JW = decltype(JWC)::value;
   floatx4 acc[JW];
 #pragma unroll
   for (int j = 0; j < JW; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  struct Frag {
-    floatx4 a, b[JW];
-  };
+  using Frag = Frag4<JW>;
   auto frag = [&](const float* st, int g, Frag& f) {
     const float* ap = st + ((4 * g + q) * BM + wm * 16 + r16) * 4;
     f.a = *reinterpret_cast<const floatx4*>(ap);
-    const float* bp = st + A_TILE + ((4 * g + q) * BN + wn * 16 * JW + r16) * 4;
+    const float* bp = st + A_TILE + ((4 * g + q) * BN + coff * 16 + r16) * 4;
 #pragma unroll
     for (int j = 0; j < JW; ++j) f.b[j] = *reinterpret_cast<const floatx4*>(bp + 64 * j);
   };
@@ -364,7 +376,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   for (int e = 0; e < 4; ++e) bias[e] = fuse ? p.bias[row0 + e] : 0.0f;
 #pragma unroll
   for (int j = 0; j < JW; ++j) {
-    const int n = n0 + wn * 16 * JW + 16 * j + r16;
+    const int n = n0 + coff * 16 + 16 * j + r16;
     if (n >= N) continue;
     const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
     float* cp = p.C + (int64_t)img * p.strideC + pix + row0 * p.ldc;
@@ -374,6 +386,15 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if (fuse) v = act_apply_cheap(v + bias[e], act);
       cp[e * p.ldc] = v;
     }
+  }
+  };
+  if constexpr (G::NA == G::WN) {
+    run(std::integral_constant<int, G::JA>{}, wn * G::JA);
+  } else {
+    if (__builtin_amdgcn_readfirstlane(wn) < G::NA)
+      run(std::integral_constant<int, G::JA>{}, wn * G::JA);
+    else
+      run(std::integral_constant<int, G::JB>{}, G::NA * G::JA + (wn - G::NA) * G::JB);
   }
 }
 
@@ -410,6 +431,10 @@ struct TileInfo4 {
   {BMv, BNv, BKv, launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, STv>>,    \
    "conv_tile4<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si" #SIv \
    ",ri" #RIv ",st" #STv ">"}
+#define TNS_CT4U(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                      \
+  {BMv, BNv, BKv, launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv>>, \
+   "conv_tile4<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv    \
+   ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -429,8 +454,13 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 32, 4, 2, 32, 0, 0, false, 0, false),    // 14
     TNS_CT4(64, 64, 4, 1, 64, 2, 0, false, 0, false),    // 15
     TNS_CT4(64, 32, 4, 1, 64, 2, 0, false, 0, false),    // 16
+    // uneven wave columns: 26^2 (8 x 31 blocks of 64 x 176), 13^2 (32 x 8 of 32 x 176)
+    TNS_CT4U(64, 176, 4, 2, 64, 1, true, 2, 6, 1),       // 17
+    TNS_CT4U(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 18
+    TNS_CT4U(32, 176, 2, 4, 64, 1, true, 2, 3, 3),       // 19
 };
 #undef TNS_CT4
+#undef TNS_CT4U
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
