@@ -59,6 +59,7 @@ const
   TNS_OPT_TT_EXACT = 5;
   TNS_OPT_SDOT_FORM = 6;
   TNS_OPT_DX_FUSED = 7;
+  TNS_OPT_DX_TILE = 8;
 
 type
   PTnsCtx = pointer;
@@ -245,6 +246,7 @@ function tns_hip_op_ms(ctx: PTnsCtx; op: longint): double; cdecl; external libtn
 
 { tuning / options }
 function tns_gemm_variant_count(): longint; cdecl; external libtns;
+function tns_conv_dx_tile_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_conv_pp_variant_count(): longint; cdecl; external libtns;

@@ -325,6 +325,7 @@ constexpr int kT4Big = 3;    // 128 x 176 x 64, stores after group 1 and reads i
 constexpr int kT4Small = 8;  // 64 x 96 x 32, reads interleaved
 constexpr int kT4OneByOne = 13;  // 64 x 32 x 32, 4 waves (1x1 layers)
 constexpr int kT4Uneven = 18;    // 64 x 176 x 32, wave columns 6 + 5 fragments
+constexpr int kT4Narrow = 21;    // 128 x 48 x 64, stores and reads interleaved
 
 }  // namespace
 
@@ -364,6 +365,9 @@ int conv_tile_pick(const GemmArgs& a, int ks) {
   // with wave columns of 6 + 5 fragments, 8 x 31 blocks (warm clock 0.137 ->
   // 0.128 ms, stride 2 0.151 -> 0.134)
   if (a.M == 512) return kNumTiles + kT4Uneven;
+  // 1024 filters (13^2 planes, N = 1352): 8 x 29 blocks of 128 x 48 (warm clock
+  // 0.149 -> 0.139 ms, the 26^2 -> 13^2 stride-2 layer 0.157 -> 0.140)
+  if (a.M == 1024 && a.K % conv_tile4_bk(kT4Narrow) == 0) return kNumTiles + kT4Narrow;
   return -1;
 }
 

@@ -46,8 +46,12 @@ struct Frag4 {
 };
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
-          int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0>
+          int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false>
 struct Geo4 {
+  // TA: A stored k-major ([K][M], gemm(Trans, ...)): a thread fills whole
+  // 16-byte slots (four dword loads down k, one ds_write_b128); used for the
+  // conv backward's col = W^T . delta as a 1x1 "convolution" over delta
+  static constexpr bool TA = TA_;
   // WM x WN waves, each a 16-row strip of BN / WN columns; or, with JA > 0,
   // wave columns 0..NA-1 of JA 16-column fragments and the rest of JB (176 =
   // 6 + 5 fragments: waves w and w + NW/2 share a SIMD, so a SIMD's two waves
@@ -191,29 +195,48 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
 
   // ---- A staging (weights [M][K]): unit = k-quad kq4 of row m; its four
   // values go to rows 4g + 0..3, component i = kq4 & 3 (g = kq4 >> 2) --------
+  // (TA, A = [K][M]: unit = slot (row 4g + q, column m), the values of
+  // k = 16g + 4i + q for i = 0..3, lanes along m)
   const float* a_src[AU];
   int a_dst[AU];
 #pragma unroll
   for (int u = 0; u < AU; ++u) {
     const int idx = tid + G::NT * u;
-    // 8 k-quads of one row per 8 lanes (128 contiguous bytes per row)
-    const int lo = idx & 7, rest = idx >> 3;
-    const int m = rest % BM, kq4 = lo + 8 * (rest / BM);
-    a_src[u] = p.A + (m0 + m) * p.lda + 4 * kq4;
-    a_dst[u] = (4 * (kq4 >> 2)) * BM * 4 + m * 4 + (kq4 & 3);
+    if constexpr (G::TA) {
+      const int m = idx % BM, row = idx / BM;
+      a_src[u] = p.A + (int64_t)(16 * (row >> 2) + (row & 3)) * p.lda + m0 + m;
+      a_dst[u] = (row * BM + m) * 4;
+    } else {
+      // 8 k-quads of one row per 8 lanes (128 contiguous bytes per row)
+      const int lo = idx & 7, rest = idx >> 3;
+      const int m = rest % BM, kq4 = lo + 8 * (rest / BM);
+      a_src[u] = p.A + (m0 + m) * p.lda + 4 * kq4;
+      a_dst[u] = (4 * (kq4 >> 2)) * BM * 4 + m * 4 + (kq4 & 3);
+    }
   }
   float4 ra[AU];
   auto load_a = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < AU; ++u) ra[u] = *reinterpret_cast<const float4*>(a_src[u] + k0);
+    for (int u = 0; u < AU; ++u) {
+      if constexpr (G::TA) {
+        const float* q0 = a_src[u] + (int64_t)k0 * p.lda;
+        ra[u] = make_float4(q0[0], q0[4 * p.lda], q0[8 * p.lda], q0[12 * p.lda]);
+      } else {
+        ra[u] = *reinterpret_cast<const float4*>(a_src[u] + k0);
+      }
+    }
   };
   auto store_a = [&](float* as) {
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
-      as[a_dst[u]] = ra[u].x;
-      as[a_dst[u] + BM * 4] = ra[u].y;
-      as[a_dst[u] + 2 * BM * 4] = ra[u].z;
-      as[a_dst[u] + 3 * BM * 4] = ra[u].w;
+      if constexpr (G::TA) {
+        *reinterpret_cast<float4*>(as + a_dst[u]) = ra[u];
+      } else {
+        as[a_dst[u]] = ra[u].x;
+        as[a_dst[u] + BM * 4] = ra[u].y;
+        as[a_dst[u] + 2 * BM * 4] = ra[u].z;
+        as[a_dst[u] + 3 * BM * 4] = ra[u].w;
+      }
     }
   };
 
@@ -408,9 +431,9 @@ hipError_t launch_g4(const GemmArgs& a_in, int ks, int dil, hipStream_t s) {
 #ifdef TNS_CT4_STAMPS
   a.stamps = g_ct4_stamps;
 #endif
-  if (a.M % G::BM || a.K % G::BK || a.K <= 0 || a.lda % 4 ||
-      (reinterpret_cast<uintptr_t>(a.A) & 15))
-    return hipErrorInvalidValue;
+  if (a.M % G::BM || a.K % G::BK || a.K <= 0) return hipErrorInvalidValue;
+  if (!G::TA && (a.lda % 4 || (reinterpret_cast<uintptr_t>(a.A) & 15))) return hipErrorInvalidValue;
+  if (G::TA && (a.lda < a.M || a.K * a.lda > 0x7fffffffLL)) return hipErrorInvalidValue;
   const int64_t tiles = (a.M / G::BM) * ((a.N + G::BN - 1) / G::BN);
   if (tiles > 0x7fffffff || a.N > 0x7fffffff || a.K > 0x7fffffff) return hipErrorInvalidValue;
   if (ks == 3)
@@ -458,9 +481,32 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4U(64, 176, 4, 2, 64, 1, true, 2, 6, 1),       // 17
     TNS_CT4U(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 18
     TNS_CT4U(32, 176, 2, 4, 64, 1, true, 2, 3, 3),       // 19
+    // 13^2 planes (N = 1352): 8 x 29 blocks of 128 x 48 (1024 filters), 8 x 29 of 64 x 48 (512)
+    TNS_CT4(128, 48, 8, 1, 32, 0, 0, false, 3, false),   // 20
+    TNS_CT4(128, 48, 8, 1, 64, 1, 0, true, 2, false),    // 21
+    TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
+    TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
+    TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
 };
+// A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
+#define TNS_CT4T(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                      \
+  {BMv, BNv, BKv,                                                                      \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, true>>,  \
+   "conv_tile4_ta<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv     \
+   ",ri" #RIv ",j" #JAv "x" #NAv ">"}
+const TileInfo4 kTiles4T[] = {
+    TNS_CT4T(128, 176, 8, 1, 64, 1, true, 2, 0, 0),   // 0
+    TNS_CT4T(128, 96, 8, 1, 64, 1, true, 2, 0, 0),    // 1
+    TNS_CT4T(128, 48, 8, 1, 64, 1, true, 2, 0, 0),    // 2
+    TNS_CT4T(64, 176, 4, 2, 32, 0, false, 3, 6, 1),   // 3
+    TNS_CT4T(64, 96, 4, 1, 32, 0, false, 3, 0, 0),    // 4
+    TNS_CT4T(64, 32, 4, 1, 32, 0, false, 0, 0, 0),    // 5
+    TNS_CT4T(128, 176, 8, 1, 32, 0, false, 3, 0, 0),  // 6
+};
+constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
 #undef TNS_CT4
 #undef TNS_CT4U
+#undef TNS_CT4T
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
@@ -477,6 +523,42 @@ extern "C" int tns_debug_ct4_stamps(unsigned* dev_buf) {
   return 0;
 }
 #endif
+
+int conv_tile4_ta_count() { return kNumTiles4T; }
+const char* conv_tile4_ta_name(int v) { return v >= 0 && v < kNumTiles4T ? kTiles4T[v].name : ""; }
+
+// col_b = W^T . delta_b for every image b at once: a 1x1 stride-1 "conv"
+// whose images are the delta planes (oh x ow, `filters` channels) and whose
+// weights are W read k-major; same chains as the TN GEMM (each col element an
+// ascending-f fma chain from +0).  Form by measured shape, -1: none applies.
+// Measured (scripts/conv_bwd_layers.py, profiles/r03_conv_tile4.json): ahead
+// of the TN GEMM on the 13^2 planes only (1x1 layers 0.222 -> 0.155 ms per
+// 7 calls, 3x3 1.197 -> 1.180); behind it on the 26^2 .. 104^2 planes, whose
+// TN tiles balance better (26^2 3x3 1.48 -> 1.65 with the 128 x 96 form).
+int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K) {
+  if (K % 64 == 0 && M % 128 == 0 && N < 4096) return 2;
+  return -1;
+}
+
+hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float* col,
+                                int64_t batch, int64_t C, int64_t ks, int64_t F, int64_t oh,
+                                int64_t ow, hipStream_t s) {
+  if (v < 0 || v >= kNumTiles4T) return hipErrorInvalidValue;
+  const int64_t M = C * ks * ks, hw = oh * ow;
+  if (batch * F * hw * 4 > 0x7fffffffLL || batch * hw > 0x7fffffffLL) return hipErrorInvalidValue;
+  GemmArgs a{};
+  a.M = M; a.N = batch * hw; a.K = F;
+  a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_ZERO;
+  a.A = w; a.lda = M; a.strideA = 0;
+  a.B = delta; a.ldb = hw; a.strideB = F * hw;
+  a.C = col; a.ldc = hw; a.strideC = M * hw;
+  a.batch = 1; a.epi = EPI_NONE; a.bias = nullptr; a.act = 0;
+  a.conv = 2;
+  a.conv_H = (int)oh; a.conv_W = (int)ow; a.conv_ow = (int)ow; a.conv_ohw = (int)hw;
+  a.conv_sY = 1; a.conv_sX = 1; a.conv_pH = 0; a.conv_pW = 0;
+  a.conv_bytes = (int)(4 * batch * F * hw);
+  return kTiles4T[v].fn(a, 1, 1, s);
+}
 
 hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStream_t s) {
   if (v < 0 || v >= kNumTiles4) return hipErrorInvalidValue;

@@ -31,6 +31,9 @@ static tns_error_hook_t g_hook = nullptr;
 static int64_t g_strict_beta0 = 1;
 static int64_t g_nt_sdot = 1;
 static int64_t g_dx_fused = 1;
+// conv backward col = W^T . delta: -1 conv_tile4's k-major-A forms where
+// they apply, -2 the TN GEMM, v >= 0 form v (TNS_OPT_DX_TILE)
+static int64_t g_dx_tile = -1;
 static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
@@ -545,6 +548,10 @@ int tns_set_option(int32_t opt, int64_t value) {
       return TNS_OK;
     case TNS_OPT_DX_FUSED:
       g_dx_fused = value < 0 ? 1 : (value > 2 ? 2 : value);
+      return TNS_OK;
+    case TNS_OPT_DX_TILE:
+      if (value >= conv_tile4_ta_count()) return set_error(TNS_ERR_ARG, "no dX tile %lld", (long long)value);
+      g_dx_tile = value < -1 ? -2 : value;
       return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
@@ -1559,10 +1566,29 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
                       "fused dX + col2im launch");
   }
   // col_b = W^T . delta_b (TN strided batched, weights shared, beta = 0 into
-  // the workspace), then col2im accumulates into state.delta (646-660)
-  if (int r = do_gemm(c, true, false, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,
-                      i_m * i_k, 0.0f, ws, i_k, colSize, batch, EPI_NONE, nullptr, 0, true))
-    return r;
+  // the workspace), then col2im accumulates into state.delta (646-660).  All
+  // images in one launch on conv_tile4's k-major-A forms where they apply (a
+  // 1x1 "convolution" over the delta planes, the same chains), else the TN
+  // GEMM
+  bool done = false;
+  if (g_dx_tile != -2) {
+    const int dv = g_dx_tile >= 0 ? (int)g_dx_tile : conv_tile4_dx_pick(i_n, batch * i_k, i_m);
+    if (dv >= 0) {
+      OpTimer t(c, TNS_OP_GEMM);
+      const hipError_t e = launch_conv_tile4_dx(dv, weights, delta, ws, batch, C, kSize, filters,
+                                                g.oh, g.ow, c->stream);
+      if (e == hipSuccess)
+        done = true;
+      else if (e != hipErrorInvalidValue || g_dx_tile >= 0)
+        return e == hipErrorInvalidValue
+                   ? set_error(TNS_ERR_UNSUPPORTED, "dX tile %d does not fit this layer", dv)
+                   : hip_status(e, "dX tile launch");
+    }
+  }
+  if (!done)
+    if (int r = do_gemm(c, true, false, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,
+                        i_m * i_k, 0.0f, ws, i_k, colSize, batch, EPI_NONE, nullptr, 0, true))
+      return r;
   OpTimer t(c, TNS_OP_COL2IM);
   return hip_status(launch_col2im(g, ws, colSize, state_delta, C * H * W, batch, c->stream),
                     "col2im launch");
@@ -1598,6 +1624,7 @@ int tns_hip_conv_backward_bn(tns_ctx* c, int64_t batch, int64_t C, int64_t H, in
 int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
+int tns_conv_dx_tile_count(void) { return conv_tile4_ta_count(); }
 int tns_conv_pp_variant_count(void) { return conv_pp_count(); }
 const char* tns_conv_pp_variant_name(int32_t v) { return conv_pp_name(v); }
 int tns_conv_dma_variant_count(void) { return conv_dma_count(); }

@@ -126,6 +126,15 @@ int conv_tile4_count();
 const char* conv_tile4_name(int v);
 int conv_tile4_bk(int v);
 hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
+// conv backward col_b = W^T . delta_b (all images, col [batch][C*ks*ks][oh*ow],
+// beta = 0) on conv_tile4's k-major-A forms: form v of conv_tile4_ta_count(),
+// conv_tile4_dx_pick = -1 where none applies
+int conv_tile4_ta_count();
+const char* conv_tile4_ta_name(int v);
+int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K);
+hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float* col,
+                                int64_t batch, int64_t C, int64_t ks, int64_t F, int64_t oh,
+                                int64_t ow, hipStream_t s);
 // implicit-GEMM convolution on the ping-pong schedule (conv_pp.hip): same
 // operands and limits as conv_tile; conv_pp_pick = -1 where not measured faster
 int conv_pp_count();

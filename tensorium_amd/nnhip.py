@@ -307,6 +307,16 @@ class TNNHip:
         fits, 0 the reference's TN GEMM + col2im (bit-identical); process-wide."""
         check(self.lib.tns_set_option(7, int(mode)))
 
+    def setDxTile(self, form: int = -1):
+        """Conv backward col = W^T . delta: -1 a k-major-A conv tile where one
+        applies, -2 the TN GEMM, v >= 0 form v of convDxTiles() (all
+        bit-identical); process-wide."""
+        check(self.lib.tns_set_option(8, int(form)))
+
+    def convDxTiles(self) -> int:
+        """k-major-A conv tiles of the backward's col = W^T . delta."""
+        return int(self.lib.tns_conv_dx_tile_count())
+
     def convTileVariants(self) -> int:
         """Plane-sized implicit-conv tiles (setConvVariant(100 + v))."""
         return int(self.lib.tns_conv_tile_variant_count())

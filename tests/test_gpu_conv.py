@@ -193,6 +193,67 @@ def test_conv_backward_yolov3_batch8(hip, torch_cuda, ora, idx):
     assert np.array_equal(dbu.cpu().numpy(), rbu)
 
 
+DX_CASES = [(2, 64, 13, 64, 3, 1, 1, 9), (2, 128, 13, 64, 3, 1, 1, 1), (1, 128, 20, 128, 3, 2, 1, 9),
+            (2, 64, 9, 128, 1, 1, 0, 4), (3, 64, 11, 96, 3, 1, 1, 9)]
+
+
+def _dx_case(hip, torch, ora, batch, C, H, F, k, s, p, act, seed):
+    rng = np.random.default_rng(seed)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.3, 0.3, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    sd0 = rng.uniform(-1, 1, x.shape).astype(np.float32)
+    rd, rbu, rwu, rsd = d0.copy(), bu0.copy(), wu0.copy(), sd0.copy()
+    ora.conv_backward(x, w, F, k, s, p, act, out, rd, rbu, rwu, rsd)
+    t = lambda a: torch.from_numpy(a.copy()).cuda()  # noqa: E731
+    dx, dw, dout, dd, dbu, dwu, dsd = map(t, (x, w, out, d0, bu0, wu0, sd0))
+    hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, act, dout, dd, dbu, dwu, None, dsd)
+    hip.finish()
+    return dsd.cpu().numpy(), rsd
+
+
+def test_conv_backward_dx_tiles(hip, torch_cuda, ora):
+    """Every k-major-A conv tile of the backward's col = W^T . delta
+    (conv_tile4.hip, TNS_OPT_DX_TILE = v: all images in one launch, the delta
+    planes as a 1x1 convolution's images) — state.delta bit-exact against
+    the reference's TN GEMM + scol2im; forms whose tile does not divide the
+    layer report UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convDxTiles()
+    assert nv >= 4
+    ran = 0
+    hip.setDxFused(0)
+    try:
+        for v in range(nv):
+            hip.setDxTile(v)
+            for i, case in enumerate(DX_CASES):
+                try:
+                    got, ref = _dx_case(hip, torch_cuda, ora, *case, seed=50 + i)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, case)
+    finally:
+        hip.setDxTile(-1)
+        hip.setDxFused(1)
+    assert ran >= 2 * nv
+
+
+@pytest.mark.parametrize("idx", [3, 11, 28, 45])
+def test_conv_backward_dx_yolov3_batch8(hip, torch_cuda, ora, idx):
+    """state.delta at YOLOv3 layer shapes, batch 8, on the default path (the
+    k-major-A conv tile where one applies): bit-exact."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    spec = yolov3_conv_table()[idx]
+    got, ref = _dx_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,
+                        spec.stride, spec.pad, spec.activation, seed=idx)
+    assert np.array_equal(got, ref)
+
+
 @pytest.mark.parametrize("idx", [1, 11, 28, 44, 45, 58])
 def test_conv_backward_dw_rc_forms(hip, torch_cuda, ora, idx):
     """Every residue-register form of the dW product (sgemm_sdot_rc.hip,
