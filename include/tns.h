@@ -453,6 +453,8 @@ enum { TNS_OP_GEMM = 0, TNS_OP_IM2COL = 1, TNS_OP_COL2IM = 2, TNS_OP_BIAS = 3,
 int         tns_gemm_variant_count(void);
 /* k-major-A conv tiles of the backward's col = W^T . delta (TNS_OPT_DX_TILE = v) */
 int         tns_conv_dx_tile_count(void);
+/* implicit-im2col dW tiles of the conv backward (TNS_OPT_DW_TILE = v) */
+int         tns_conv_dw_tile_count(void);
 /* plane-sized implicit-conv tiles (TNS_OPT_CONV_VARIANT = 100 + v) */
 int         tns_conv_tile_variant_count(void);
 const char* tns_conv_tile_variant_name(int32_t variant);
@@ -515,10 +517,17 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * col_b = W^T . delta_b, for all images in one launch of a k-major-A conv
  * tile (conv_tile4.hip, the delta planes as a 1x1 convolution's images) where
  * one applies; -2 = the TN GEMM always; v >= 0 forces form v of
- * tns_conv_dx_tile_count() (tests; same bits in every form). */
+ * tns_conv_dx_tile_count() (tests; same bits in every form).
+ * TNS_OPT_DW_TILE (default -1 = by shape): the conv backward's dW product
+ * (the reference's per-image sdot-order NT GEMM over the im2col matrix) by
+ * a kernel that generates the im2col rows in its staging (dw_tile.hip: no
+ * col matrix, no im2col pass) where one applies; -2 = im2col + the sdot
+ * kernels always; v >= 0 forces form v of tns_conv_dw_tile_count() (same
+ * bits in every form). */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
-       TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8 };
+       TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,
+       TNS_OPT_DW_TILE = 9 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

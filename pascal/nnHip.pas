@@ -60,6 +60,7 @@ const
   TNS_OPT_SDOT_FORM = 6;
   TNS_OPT_DX_FUSED = 7;
   TNS_OPT_DX_TILE = 8;
+  TNS_OPT_DW_TILE = 9;
 
 type
   PTnsCtx = pointer;
@@ -247,6 +248,7 @@ function tns_hip_op_ms(ctx: PTnsCtx; op: longint): double; cdecl; external libtn
 { tuning / options }
 function tns_gemm_variant_count(): longint; cdecl; external libtns;
 function tns_conv_dx_tile_count(): longint; cdecl; external libtns;
+function tns_conv_dw_tile_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_conv_pp_variant_count(): longint; cdecl; external libtns;

@@ -20,12 +20,18 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--dx-fused", type=int, default=1, help="TNS_OPT_DX_FUSED")
+    ap.add_argument("--dw-tile", type=int, default=-1, help="TNS_OPT_DW_TILE")
+    ap.add_argument("--layers", default="", help="comma-separated layer indices (default: all)")
     a = ap.parse_args()
     hip = TNNHip(0)
     hip.setDxFused(a.dx_fused)
+    hip.setDwTile(a.dw_tile)
+    only = {int(v) for v in a.layers.split(",") if v}
     batch = 8
     out = []
     for s in yolov3_conv_table():
+        if only and s.index not in only:
+            continue
         x = torch.rand(batch, s.c, s.h, s.h, device="cuda")
         w = torch.rand(s.filters, s.K, device="cuda") * 0.1
         o = torch.rand(batch, s.filters, s.out_h, s.out_h, device="cuda")

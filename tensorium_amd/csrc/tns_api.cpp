@@ -34,6 +34,9 @@ static int64_t g_dx_fused = 1;
 // conv backward col = W^T . delta: -1 conv_tile4's k-major-A forms where
 // they apply, -2 the TN GEMM, v >= 0 form v (TNS_OPT_DX_TILE)
 static int64_t g_dx_tile = -1;
+// conv backward dW with the im2col matrix generated in the staging
+// (dw_tile.hip): -1 by measured shape, -2 never, v >= 0 form v (TNS_OPT_DW_TILE)
+static int64_t g_dw_tile = -1;
 static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
@@ -548,6 +551,10 @@ int tns_set_option(int32_t opt, int64_t value) {
       return TNS_OK;
     case TNS_OPT_DX_FUSED:
       g_dx_fused = value < 0 ? 1 : (value > 2 ? 2 : value);
+      return TNS_OK;
+    case TNS_OPT_DW_TILE:
+      if (value >= dw_tile_count()) return set_error(TNS_ERR_ARG, "no dW tile %lld", (long long)value);
+      g_dw_tile = value < -1 ? -2 : value;
       return TNS_OK;
     case TNS_OPT_DX_TILE:
       if (value >= conv_tile4_ta_count()) return set_error(TNS_ERR_ARG, "no dX tile %lld", (long long)value);
@@ -1510,11 +1517,40 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
       state_delta && dilation == 1 &&
       ((g_dx_fused == 1 && conv_dx_fused_applies(C, H, W, kSize, stride, filters, g.oh, g.ow)) ||
        (g_dx_fused == 2 && conv_dx_fused_fits(C, H, W, stride, filters, g.oh, g.ow)));
+  // dW with the im2col matrix generated inside the sdot-order product
+  // (dw_tile.hip): no col matrix, no im2col pass
+  DwArgs da{};
+  int dwv = -1;
+  if (g_nt_sdot && g_dw_tile != -2 && (kSize == 1 || kSize == 3) &&
+      C * H * W < (1LL << 27) && i_n <= 0x7fffffffLL && i_k <= 0x7fffffffLL && batch <= 65535) {
+    da.delta = delta; da.x = input; da.part = nullptr;
+    da.M = (int)i_m; da.N = (int)i_n; da.HW = (int)i_k;
+    da.C = (int)C; da.H = (int)H; da.W = (int)W; da.oW = (int)g.ow;
+    da.stride = (int)stride; da.pad = (int)(padding * dilation); da.dil = (int)dilation;
+    da.va = i_k % 4 == 0 && (reinterpret_cast<uintptr_t>(delta) & 15) == 0;
+    da.alpha = 1.0f;
+    da.strideA = i_m * i_k; da.strideX = C * H * W; da.strideP = i_m * i_n; da.batch = batch;
+    dwv = g_dw_tile >= 0 ? (int)g_dw_tile : dw_tile_pick(da, (int)kSize);
+  }
   float* ws = workspace;
-  if (!ws && (needs_col || (state_delta && !fused_dx)))
+  if (!ws && ((needs_col && dwv < 0) || (state_delta && !fused_dx)))
     if (int r = ensure_scratch(c, 0, batch * colSize, &ws)) return r;
   const float* col = input;
-  if (needs_col) {
+  if (dwv >= 0) {
+    float* part = nullptr;
+    if (int r = ensure_scratch(c, 4, batch * i_m * i_n, &part)) return r;
+    da.part = part;
+    {
+      OpTimer t(c, TNS_OP_GEMM);
+      const hipError_t e = launch_dw_tile(dwv, da, (int)kSize, c->stream);
+      if (e == hipErrorInvalidValue)
+        return set_error(TNS_ERR_UNSUPPORTED, "dW tile %d does not fit this layer", dwv);
+      if (int r = hip_status(e, "dW tile launch")) return r;
+    }
+    if (int r = hip_status(launch_add_in_order(weight_updates, part, i_m * i_n, batch, c->stream),
+                           "dW accumulate launch"))
+      return r;
+  } else if (needs_col) {
     OpTimer t(c, TNS_OP_IM2COL);
     if (int r = hip_status(launch_im2col(g, input, C * H * W, ws, colSize, batch, c->stream),
                            "im2col launch"))
@@ -1528,7 +1564,9 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // (each stored as is, BETA_STORE), then added to C image by image in the
   // reference's order — the same roundings, batch-fold more parallelism for
   // the few-tile, long-k dW shapes.
-  if (g_nt_sdot && batch > 1) {
+  if (dwv >= 0) {
+    // (done above)
+  } else if (g_nt_sdot && batch > 1) {
     float* part = nullptr;
     if (int r = ensure_scratch(c, 4, batch * i_m * i_n, &part)) return r;
     GemmArgs a{};
@@ -1625,6 +1663,7 @@ int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
 int tns_conv_dx_tile_count(void) { return conv_tile4_ta_count(); }
+int tns_conv_dw_tile_count(void) { return dw_tile_count(); }
 int tns_conv_pp_variant_count(void) { return conv_pp_count(); }
 const char* tns_conv_pp_variant_name(int32_t v) { return conv_pp_name(v); }
 int tns_conv_dma_variant_count(void) { return conv_dma_count(); }

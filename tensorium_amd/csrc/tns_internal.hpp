@@ -153,6 +153,23 @@ int conv_patch_count();
 const char* conv_patch_name(int v);
 int conv_patch_pick(const GemmArgs& a);
 hipError_t launch_conv_patch(int v, const GemmArgs& a, hipStream_t s);
+// conv backward dW in the sdot order with the im2col matrix generated in the
+// staging (dw_tile.hip): part[b][m][n] = alpha * sdot over the pixels of
+// delta_b[m][.] and the im2col row n of image b (BETA_STORE; the caller adds
+// the images in order); M % tile rows == 0, N % tile columns == 0
+struct DwArgs {
+  const float* delta;  // [batch][M][HW]
+  const float* x;      // [batch][C][H][W]
+  float* part;         // [batch][M][N]
+  int M, N, HW, C, H, W, oW, stride, pad, dil;
+  int va;              // delta rows float4-loadable (HW % 4 == 0, 16-byte aligned)
+  float alpha;
+  int64_t strideA, strideX, strideP, batch;
+};
+int dw_tile_count();
+const char* dw_tile_name(int v);
+int dw_tile_pick(const DwArgs& a, int ks);
+hipError_t launch_dw_tile(int v, const DwArgs& a, int ks, hipStream_t s);
 // direct convolution (conv_direct.hip) for 3-channel 3x3 layers with 16 or
 // 32 filters: bias (nullable: raw output) + activation fused
 bool conv_direct_applies(int64_t C, int64_t ks, int64_t filters);

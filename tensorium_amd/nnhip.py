@@ -313,6 +313,16 @@ class TNNHip:
         bit-identical); process-wide."""
         check(self.lib.tns_set_option(8, int(form)))
 
+    def setDwTile(self, form: int = -1):
+        """Conv backward dW: -1 the implicit-im2col sdot kernel where measured
+        faster, -2 im2col + the sdot kernels, v >= 0 form v of convDwTiles()
+        (all bit-identical); process-wide."""
+        check(self.lib.tns_set_option(9, int(form)))
+
+    def convDwTiles(self) -> int:
+        """Implicit-im2col dW tiles of the conv backward."""
+        return int(self.lib.tns_conv_dw_tile_count())
+
     def convDxTiles(self) -> int:
         """k-major-A conv tiles of the backward's col = W^T . delta."""
         return int(self.lib.tns_conv_dx_tile_count())

@@ -254,6 +254,54 @@ def test_conv_backward_dx_yolov3_batch8(hip, torch_cuda, ora, idx):
     assert np.array_equal(got, ref)
 
 
+DW_CASES = [(2, 64, 13, 64, 3, 1, 1, 9), (3, 128, 9, 64, 1, 1, 0, 4), (1, 64, 17, 128, 3, 1, 1, 1),
+            (2, 16, 20, 64, 3, 2, 1, 9), (2, 128, 11, 128, 3, 1, 1, 9), (9, 64, 12, 64, 3, 1, 1, 9)]
+
+
+def _dw_case(hip, torch, ora, batch, C, H, F, k, s, p, act, seed):
+    rng = np.random.default_rng(seed)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.3, 0.3, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    rd, rbu, rwu = d0.copy(), bu0.copy(), wu0.copy()
+    ora.conv_backward(x, w, F, k, s, p, act, out, rd, rbu, rwu, None)
+    t = lambda a: torch.from_numpy(a.copy()).cuda()  # noqa: E731
+    dx, dw, dout, dd, dbu, dwu = map(t, (x, w, out, d0, bu0, wu0))
+    hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, act, dout, dd, dbu, dwu)
+    hip.finish()
+    return dwu.cpu().numpy(), rwu
+
+
+def test_conv_backward_dw_tiles(hip, torch_cuda, ora):
+    """Every implicit-im2col dW tile (dw_tile.hip, TNS_OPT_DW_TILE = v: the
+    im2col rows generated in the staging of the sdot-order product, all
+    images in one launch, added in image order): weight_updates bit-exact
+    against the reference's per-image im2col + beta = 1 sdot loop; 1x1 and
+    3x3, stride 2, pixel counts off the 64-pixel tile and odd (scalar delta
+    loads), batch 9; tiles that do not divide the layer report UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convDwTiles()
+    assert nv >= 3
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setDwTile(v)
+            for i, case in enumerate(DW_CASES):
+                try:
+                    got, ref = _dw_case(hip, torch_cuda, ora, *case, seed=70 + i)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, case)
+    finally:
+        hip.setDwTile(-1)
+    assert ran >= 2 * nv
+
+
 @pytest.mark.parametrize("idx", [1, 11, 28, 44, 45, 58])
 def test_conv_backward_dw_rc_forms(hip, torch_cuda, ora, idx):
     """Every residue-register form of the dW product (sgemm_sdot_rc.hip,
