@@ -162,6 +162,53 @@ __global__ __launch_bounds__(512, 1) void m16_lds4(float* out, float x) {
   out[blockIdx.x * 512 + threadIdx.x] = r;
 }
 
+
+// m32_lds4: the 256x256 SGEMM wave loop (wave tile 128 x 64 = 4 x 2 32x32x2
+// accumulators) with k-permuted slots: per 4 MFMA steps one ds_read_b128 per
+// A fragment (4) and per B fragment (2), 6 reads per 32 MFMAs (vs 12)
+__global__ __launch_bounds__(512, 1) void m32_lds4(float* out, float x) {
+  __shared__ float lds[32 * 256 * 2];
+  for (int i = threadIdx.x; i < 32 * 512; i += 512) lds[i] = x * i;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, lc = lane & 31, h = lane >> 5, wid = threadIdx.x >> 6;
+  const int g = wid >> 2, wq = wid & 3;
+  floatx16 acc[8];
+  for (int j = 0; j < 8; ++j)
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0;
+  // slot images [group][h][row] of 16 bytes: A 256 rows, B 256 columns
+  auto frag = [&](int s, float4 (&a)[4], float4 (&b)[2]) {
+    const int gg = s & 3;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      a[i] = *reinterpret_cast<const float4*>(lds + ((gg * 2 + h) * 256 + g * 128 + 32 * i + lc) * 4);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      b[j] = *reinterpret_cast<const float4*>(lds + 8192 + ((gg * 2 + h) * 256 + wq * 64 + 32 * j + lc) * 4);
+  };
+  auto mm = [&](const float4 (&a)[4], const float4 (&b)[2]) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[2 * i + j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][c], b[j][c], acc[2 * i + j], 0, 0, 0);
+  };
+  float4 a0[4], b0[2], a1[4], b1[2];
+  frag(0, a0, b0);
+  for (int s = 0; s < STEPS / 8; s += 2) {
+    frag(s + 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a0, b0);
+    frag(s + 2, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(a1, b1);
+  }
+  float r = 0;
+  for (int j = 0; j < 8; ++j) r += acc[j][0] + acc[j][15];
+  out[blockIdx.x * 512 + threadIdx.x] = r;
+}
+
 template <class F>
 void run(const char* name, F kernel, double flop_per_wave, float* out) {
   hipEvent_t e0, e1;
@@ -190,6 +237,7 @@ int main() {
   run("m16_lds4", m16_lds4, f16, out);
   run("m32_regs", m32_regs, f32, out);
   run("m32_lds", m32_lds, f32, out);
+  run("m32_lds4", m32_lds4, f32, out);
   (void)hipFree(out);
   return 0;
 }

@@ -38,6 +38,14 @@ constexpr int WTM = 128, WTN = 64, TM = 4, TN = 2;  // wave tile, 32x32 accumula
 constexpr int LDA = BM, LDB = BN;                     // k-major LDS rows
 constexpr int A_TILE = BK * LDA, B_TILE = BK * LDB, STAGE = A_TILE + B_TILE;
 
+// BP: B register-staged into a k-permuted slot image instead of the row
+// image by LDS-DMA: slot (g, h, column) holds the four k = 8g + h + 2i
+// (i = 0..3) a lane consumes over MFMA steps 4g..4g+3, so a wave reads its
+// two B fragments once per four steps (two ds_read_b128) instead of two
+// ds_read_b32 per step (the bare loop: 0.923 -> see scripts/mfma_probe.hip
+// m32_lds4); a group thread owns one column of the half's 16 k-rows (16
+// coalesced dword loads, four ds_write_b128)
+template <bool BP>
 __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar branches
@@ -132,7 +140,20 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
   // had finished reading — hipcc copies the loop-carried registers right
   // after the loads and waits on them there: 4096^3 0.972 -> 1.137 ms.)
   float4 ra[AU];
+  float rbp[BP ? 16 : 1];
+  // (BP) buffer loads: the column in the VGPR offset, the row in the
+  // uniform SGPR offset (no 64-bit address registers per row)
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(B), 0, BP ? 0x7fffffff : 0, 0x00020000);
+  const unsigned b_voff = 4u * (unsigned)(n0 + tg);
   auto issue_half = [&](int64_t k0, int st, int half) {
+    if constexpr (BP) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const unsigned so = __builtin_amdgcn_readfirstlane((unsigned)((k0 + 16 * half + r) * ldb * 4));
+        rbp[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(brs, b_voff, so, 0));
+      }
+    } else {
 #ifndef TNS_PP_NO_B  // (diagnostic builds: timing without this part, wrong results)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -146,24 +167,39 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
           : "memory");
     }
 #endif
+    }
 #ifndef TNS_PP_NO_A
 #pragma unroll
     for (int u = 0; u < AU; ++u)
-      ra[u] = *reinterpret_cast<const float4*>(a_src[u] + k0 + 16 * half);
+      if constexpr (BP)  // unit u = unit 0 shifted by rows {0, 16, 128, 144}[u] (fewer live registers)
+        ra[u] = *reinterpret_cast<const float4*>(a_src[0] + (int64_t)((u & 1) * 16 + (u >> 1) * 128) * lda + k0 + 16 * half);
+      else
+        ra[u] = *reinterpret_cast<const float4*>(a_src[u] + k0 + 16 * half);
 #endif
   };
   auto finish_half = [&](int st, int half) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A loads and B DMA landed
+    if constexpr (BP) {
+      float* bs = smem + st * STAGE + A_TILE;
+#pragma unroll
+      for (int gl = 0; gl < 2; ++gl)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          *reinterpret_cast<float4*>(bs + (((2 * half + gl) * 2 + hh) * BN + tg) * 4) =
+              make_float4(rbp[8 * gl + hh], rbp[8 * gl + hh + 2], rbp[8 * gl + hh + 4],
+                          rbp[8 * gl + hh + 6]);
+    }
 #ifndef TNS_PP_NO_A
     float* as = smem + st * STAGE + 16 * half * LDA;
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       float4 v = ra[u];  // A_PART = ALPHA*A[kk] (1*x == x bit for bit)
       v.x = alpha * v.x; v.y = alpha * v.y; v.z = alpha * v.z; v.w = alpha * v.w;
-      as[a_dst[u]] = v.x;
-      as[a_dst[u] + LDA] = v.y;
-      as[a_dst[u] + 2 * LDA] = v.z;
-      as[a_dst[u] + 3 * LDA] = v.w;
+      const int d = BP ? a_dst[0] + 64 * u : a_dst[u];  // (mm + 64u) ^ x = (mm ^ x) + 64u
+      as[d] = v.x;
+      as[d + LDA] = v.y;
+      as[d + 2 * LDA] = v.z;
+      as[d + 3 * LDA] = v.w;
     }
 #endif
   };
@@ -188,18 +224,66 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
   };
   float a0[TM], b0[TN];
+  // (BP) the B slots of four steps: bq[j] = column b_frag + 32j of group g
+  float4 bq0[TN];
+  auto fragA = [&](const float* st, int s, float (&a)[TM]) {
+    const int k = 2 * s + h;
+    const float4 v = *reinterpret_cast<const float4*>(st + k * LDA + (a_frag ^ (((k >> 2) & 3) << 3)));
+    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+  };
+  auto fragBq = [&](const float* st, int g4, float4 (&bq)[TN]) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      bq[j] = *reinterpret_cast<const float4*>(st + A_TILE + ((g4 * 2 + h) * BN + b_frag + 32 * j) * 4);
+  };
+  // step-0 fragments of a stage into a0 / b0 (or a0 / bq0)
+  auto frag0 = [&](const float* st) {
+    if constexpr (BP) {
+      fragA(st, 0, a0);
+      fragBq(st, 0, bq0);
+    } else {
+      frag(st, 0, a0, b0);
+    }
+  };
   // one k-tile of this wave's MFMAs from stage cur, step 0's fragments
   // already in a0/b0
   auto compute = [&](const float* cur) {
-    float a1[TM], b1[TN];
+    if constexpr (BP) {
+      float a1[TM];
+      float4 bq1[TN];
 #pragma unroll
-    for (int s = 0; s < BK / 2; s += 2) {
-      frag(cur, s + 1, a1, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(a0, b0);
-      if (s + 2 < BK / 2) frag(cur, s + 2, a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      mma(a1, b1);
+      for (int g4 = 0; g4 < BK / 8; ++g4) {
+        float4 (&bc)[TN] = (g4 & 1) ? bq1 : bq0;
+        float4 (&bn)[TN] = (g4 & 1) ? bq0 : bq1;
+#pragma unroll
+        for (int c = 0; c < 4; c += 2) {
+          const int s = 4 * g4 + c;
+          fragA(cur, s + 1, a1);
+          if (c == 0 && g4 + 1 < BK / 8) fragBq(cur, g4 + 1, bn);
+          __builtin_amdgcn_sched_barrier(0);
+          {
+            const float bb[TN] = {bc[0][c], bc[1][c]};
+            mma(a0, bb);
+          }
+          if (s + 2 < BK / 2) fragA(cur, s + 2, a0);
+          __builtin_amdgcn_sched_barrier(0);
+          {
+            const float bb[TN] = {bc[0][c + 1], bc[1][c + 1]};
+            mma(a1, bb);
+          }
+        }
+      }
+    } else {
+      float a1[TM], b1[TN];
+#pragma unroll
+      for (int s = 0; s < BK / 2; s += 2) {
+        frag(cur, s + 1, a1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a0, b0);
+        if (s + 2 < BK / 2) frag(cur, s + 2, a0, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        mma(a1, b1);
+      }
     }
   };
 
@@ -210,7 +294,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
     issue_half(0, 0, 1 - g);  // group 1: k 0..15, group 0: k 16..31
     finish_half(0, 1 - g);
     __syncthreads();
-    if (g == 0) frag(smem, 0, a0, b0);
+    if (g == 0) frag0(smem);
   }
   for (int t = 0; t < nt; ++t) {
     const float* cur = smem + (t & 1) * STAGE;
@@ -224,7 +308,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
         issue_half((int64_t)(t + 1) * BK, nxt, 0);
         finish_half(nxt, 0);
       }
-      frag(cur, 0, a0, b0);
+      frag0(cur);
     }
     __syncthreads();
     // phase B
@@ -233,7 +317,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_pp_kernel(GemmArgs p) {
     } else if (more) {
       issue_half((int64_t)(t + 1) * BK, nxt, 1);
       finish_half(nxt, 1);
-      frag(smem + nxt * STAGE, 0, a0, b0);  // k 0..1 of tile t+1: staged in phase A
+      frag0(smem + nxt * STAGE);  // k 0..1 (BP: 0..7) of tile t+1: staged in phase A
     }
     if (more) __syncthreads();
   }
@@ -261,8 +345,10 @@ bool sgemm_nn_pp_applies(const GemmArgs& a) {
   return (a.M / BM) * (a.N / BN) <= 0x7fffffff;
 }
 
-hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s) {
+hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s, bool bperm) {
   if (!sgemm_nn_pp_applies(a)) return hipErrorInvalidValue;
+  // (k-permuted B form: one buffer resource over each B, 31-bit byte offsets)
+  if (bperm && (a.K * a.ldb + a.N) * 4 > 0x7fffffffLL) return hipErrorInvalidValue;
   const int64_t tiles = (a.M / BM) * (a.N / BN);
   for (int64_t b0 = 0; b0 < a.batch; b0 += 65535) {
     GemmArgs sub = a;
@@ -271,7 +357,12 @@ hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s) {
     sub.B = a.B + b0 * a.strideB;
     sub.C = a.C + b0 * a.strideC;
     sub.batch = nb;
-    hipLaunchKernelGGL(sgemm_nn_pp_kernel, dim3((unsigned)tiles, (unsigned)nb), dim3(NT), 0, s, sub);
+    if (bperm)
+      hipLaunchKernelGGL(sgemm_nn_pp_kernel<true>, dim3((unsigned)tiles, (unsigned)nb), dim3(NT), 0,
+                         s, sub);
+    else
+      hipLaunchKernelGGL(sgemm_nn_pp_kernel<false>, dim3((unsigned)tiles, (unsigned)nb), dim3(NT),
+                         0, s, sub);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

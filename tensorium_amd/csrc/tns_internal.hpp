@@ -84,7 +84,7 @@ int sgemm_nn_big_pick(const GemmArgs& a);
 hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s);
 // the 256x256 NN tile on the ping-pong schedule (sgemm_nn_pp.hip; form 5)
 bool sgemm_nn_pp_applies(const GemmArgs& a);
-hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s);
+hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s, bool bperm = false);
 // gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
 // plain epilogue only
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
