@@ -523,11 +523,16 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * a kernel that generates the im2col rows in its staging (dw_tile.hip: no
  * col matrix, no im2col pass) where one applies; -2 = im2col + the sdot
  * kernels always; v >= 0 forces form v of tns_conv_dw_tile_count() (same
- * bits in every form). */
+ * bits in every form).
+ * TNS_OPT_BWD_OVERLAP (default 1): the conv backward runs the dW product and
+ * the state.delta chain (which read delta and write disjoint outputs)
+ * concurrently, the latter on a side stream of the context that the
+ * context's stream waits for before the call returns its work; 0 = in
+ * sequence (also whenever telemetry is on).  Same results either way. */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,
-       TNS_OPT_DW_TILE = 9 };
+       TNS_OPT_DW_TILE = 9, TNS_OPT_BWD_OVERLAP = 10 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

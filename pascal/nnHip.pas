@@ -61,6 +61,7 @@ const
   TNS_OPT_DX_FUSED = 7;
   TNS_OPT_DX_TILE = 8;
   TNS_OPT_DW_TILE = 9;
+  TNS_OPT_BWD_OVERLAP = 10;
 
 type
   PTnsCtx = pointer;

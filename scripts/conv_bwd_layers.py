@@ -21,11 +21,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dx-fused", type=int, default=1, help="TNS_OPT_DX_FUSED")
     ap.add_argument("--dw-tile", type=int, default=-1, help="TNS_OPT_DW_TILE")
+    ap.add_argument("--dx-tile", type=int, default=-1, help="TNS_OPT_DX_TILE")
     ap.add_argument("--layers", default="", help="comma-separated layer indices (default: all)")
     a = ap.parse_args()
     hip = TNNHip(0)
     hip.setDxFused(a.dx_fused)
     hip.setDwTile(a.dw_tile)
+    hip.setDxTile(a.dx_tile)
     only = {int(v) for v in a.layers.split(",") if v}
     batch = 8
     out = []

@@ -34,6 +34,7 @@ TNS_OPT_SDOT_FORM = 6
 TNS_OPT_DX_FUSED = 7
 TNS_OPT_DX_TILE = 8
 TNS_OPT_DW_TILE = 9
+TNS_OPT_BWD_OVERLAP = 10
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 

@@ -502,6 +502,10 @@ const TileInfo4 kTiles4T[] = {
     TNS_CT4T(64, 96, 4, 1, 32, 0, false, 3, 0, 0),    // 4
     TNS_CT4T(64, 32, 4, 1, 32, 0, false, 0, 0, 0),    // 5
     TNS_CT4T(128, 176, 8, 1, 32, 0, false, 3, 0, 0),  // 6
+    TNS_CT4T(64, 64, 4, 2, 32, 0, false, 3, 0, 0),    // 7: multi-block forms for the short-k dX
+    TNS_CT4T(64, 64, 4, 1, 32, 0, false, 3, 0, 0),    // 8
+    TNS_CT4T(128, 64, 8, 1, 32, 0, false, 3, 0, 0),   // 9
+    TNS_CT4T(64, 128, 4, 2, 32, 0, false, 3, 0, 0),   // 10
 };
 constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
 #undef TNS_CT4

@@ -37,6 +37,8 @@ static int64_t g_dx_tile = -1;
 // conv backward dW with the im2col matrix generated in the staging
 // (dw_tile.hip): -1 by measured shape, -2 never, v >= 0 form v (TNS_OPT_DW_TILE)
 static int64_t g_dw_tile = -1;
+// conv backward: dW and state.delta concurrently on two streams (TNS_OPT_BWD_OVERLAP)
+static int64_t g_bwd_overlap = 1;
 static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
@@ -67,7 +69,7 @@ struct tns_ctx {
   // 0 col workspace, 1 padded images / host staging, 2-3 host staging,
   // 4 per-image dW partial sums of the conv backward, 5 per-block results of
   // the batch-norm reductions
-  static constexpr int kSlots = 8;
+  static constexpr int kSlots = 9;
   float* scratch[kSlots] = {};
   size_t scratch_elems[kSlots] = {};
   // telemetry (TTensorMetrics-style, nopmetrics.pas:25-44)
@@ -78,6 +80,10 @@ struct tns_ctx {
   // host-pointer pipeline: copy stream and per-chunk events
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> pipe_ev;
+  // conv backward: state.delta's chain (TN + col2im) runs on this side
+  // stream while the dW product runs on `stream` (fork / join events)
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // implicit-GEMM conv k-tables, one per (C, H, W, kH, kW, dY, dX)
   std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int*> ktabs;
 };
@@ -85,13 +91,14 @@ struct tns_ctx {
 namespace {
 
 enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5,
-       SLOT_MLP = 6, SLOT_WT = 7 };
+       SLOT_MLP = 6, SLOT_WT = 7, SLOT_COL_DX = 8 };
 
 int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   if (elems < 1) elems = 1;
   if ((size_t)elems > c->scratch_elems[slot]) {
     if (c->scratch[slot]) {
       hipStreamSynchronize(c->stream);
+      if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
       hipFree(c->scratch[slot]);
       c->scratch[slot] = nullptr;
       c->scratch_elems[slot] = 0;
@@ -552,6 +559,9 @@ int tns_set_option(int32_t opt, int64_t value) {
     case TNS_OPT_DX_FUSED:
       g_dx_fused = value < 0 ? 1 : (value > 2 ? 2 : value);
       return TNS_OK;
+    case TNS_OPT_BWD_OVERLAP:
+      g_bwd_overlap = value ? 1 : 0;
+      return TNS_OK;
     case TNS_OPT_DW_TILE:
       if (value >= dw_tile_count()) return set_error(TNS_ERR_ARG, "no dW tile %lld", (long long)value);
       g_dw_tile = value < -1 ? -2 : value;
@@ -601,6 +611,9 @@ int tns_hip_destroy(tns_ctx* c) {
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
+  if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+  if (c->ev_fork) hipEventDestroy(c->ev_fork);
+  if (c->ev_join) hipEventDestroy(c->ev_join);
   for (hipEvent_t e : c->pipe_ev) hipEventDestroy(e);
   delete c;
   return TNS_OK;
@@ -1532,104 +1545,145 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     da.strideA = i_m * i_k; da.strideX = C * H * W; da.strideP = i_m * i_n; da.batch = batch;
     dwv = g_dw_tile >= 0 ? (int)g_dw_tile : dw_tile_pick(da, (int)kSize);
   }
+  // dW (im2col + sdot or dw_tile, accumulate) and state.delta (TN + col2im
+  // or the fused kernel) read delta and write disjoint outputs: with a
+  // state.delta they run concurrently, state.delta's chain on the context's
+  // side stream (fork / join events), each with its own col buffer —
+  // nothing changes in either result.  Telemetry times ops one by one, so it
+  // keeps them in sequence.
+  const bool overlap = state_delta && g_bwd_overlap && !c->telemetry;
+  const bool dw_col = needs_col && dwv < 0;  // dW reads an im2col matrix
   float* ws = workspace;
-  if (!ws && ((needs_col && dwv < 0) || (state_delta && !fused_dx)))
-    if (int r = ensure_scratch(c, 0, batch * colSize, &ws)) return r;
-  const float* col = input;
-  if (dwv >= 0) {
-    float* part = nullptr;
-    if (int r = ensure_scratch(c, 4, batch * i_m * i_n, &part)) return r;
-    da.part = part;
-    {
-      OpTimer t(c, TNS_OP_GEMM);
-      const hipError_t e = launch_dw_tile(dwv, da, (int)kSize, c->stream);
-      if (e == hipErrorInvalidValue)
-        return set_error(TNS_ERR_UNSUPPORTED, "dW tile %d does not fit this layer", dwv);
-      if (int r = hip_status(e, "dW tile launch")) return r;
+  if (!ws && (dw_col || (state_delta && !fused_dx && !(overlap && dw_col))))
+    if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws)) return r;
+  float* dx_ws = ws;  // col buffer of state.delta's chain
+  if (overlap && dw_col && !fused_dx)
+    if (int r = ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) return r;
+
+  auto run_dw = [&]() -> int {
+    const float* col = input;
+    if (dwv >= 0) {
+      float* part = nullptr;
+      if (int r = ensure_scratch(c, SLOT_DW, batch * i_m * i_n, &part)) return r;
+      da.part = part;
+      {
+        OpTimer t(c, TNS_OP_GEMM);
+        const hipError_t e = launch_dw_tile(dwv, da, (int)kSize, c->stream);
+        if (e == hipErrorInvalidValue)
+          return set_error(TNS_ERR_UNSUPPORTED, "dW tile %d does not fit this layer", dwv);
+        if (int r = hip_status(e, "dW tile launch")) return r;
+      }
+      return hip_status(launch_add_in_order(weight_updates, part, i_m * i_n, batch, c->stream),
+                        "dW accumulate launch");
     }
-    if (int r = hip_status(launch_add_in_order(weight_updates, part, i_m * i_n, batch, c->stream),
-                           "dW accumulate launch"))
-      return r;
-  } else if (needs_col) {
-    OpTimer t(c, TNS_OP_IM2COL);
-    if (int r = hip_status(launch_im2col(g, input, C * H * W, ws, colSize, batch, c->stream),
-                           "im2col launch"))
-      return r;
-    col = ws;
-  }
-  // weight_updates += delta_b . col_b^T, one NT GEMM per image (beta = 1),
-  // in image order as the reference loop (nConvolutionLayer.pas:636-640):
-  // each image adds sum_b = 1*sdot(...) to C.  The sums of different images
-  // are independent, so they are computed by ONE strided-batched sdot launch
-  // (each stored as is, BETA_STORE), then added to C image by image in the
-  // reference's order — the same roundings, batch-fold more parallelism for
-  // the few-tile, long-k dW shapes.
-  if (dwv >= 0) {
-    // (done above)
-  } else if (g_nt_sdot && batch > 1) {
-    float* part = nullptr;
-    if (int r = ensure_scratch(c, 4, batch * i_m * i_n, &part)) return r;
-    GemmArgs a{};
-    a.M = i_m; a.N = i_n; a.K = i_k;
-    a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_STORE;
-    a.A = delta; a.lda = i_k; a.strideA = i_m * i_k;
-    a.B = col; a.ldb = i_k; a.strideB = colSize;
-    a.C = part; a.ldc = i_n; a.strideC = i_m * i_n;
-    a.batch = batch; a.epi = EPI_NONE;
-    {
-      OpTimer t(c, TNS_OP_GEMM);
-      if (int r = hip_status(launch_sgemm_nt_sdot(a, c->stream), "sgemm_nt launch")) return r;
+    if (needs_col) {
+      OpTimer t(c, TNS_OP_IM2COL);
+      if (int r = hip_status(launch_im2col(g, input, C * H * W, ws, colSize, batch, c->stream),
+                             "im2col launch"))
+        return r;
+      col = ws;
     }
-    if (int r = hip_status(launch_add_in_order(weight_updates, part, i_m * i_n, batch,
-                                               c->stream), "dW accumulate launch"))
-      return r;
-  } else {
+    // weight_updates += delta_b . col_b^T, one NT GEMM per image (beta = 1),
+    // in image order as the reference loop (nConvolutionLayer.pas:636-640):
+    // each image adds sum_b = 1*sdot(...) to C.  The sums of different images
+    // are independent, so they are computed by ONE strided-batched sdot launch
+    // (each stored as is, BETA_STORE), then added to C image by image in the
+    // reference's order — the same roundings, batch-fold more parallelism for
+    // the few-tile, long-k dW shapes.
+    if (g_nt_sdot && batch > 1) {
+      float* part = nullptr;
+      if (int r = ensure_scratch(c, SLOT_DW, batch * i_m * i_n, &part)) return r;
+      GemmArgs a{};
+      a.M = i_m; a.N = i_n; a.K = i_k;
+      a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_STORE;
+      a.A = delta; a.lda = i_k; a.strideA = i_m * i_k;
+      a.B = col; a.ldb = i_k; a.strideB = colSize;
+      a.C = part; a.ldc = i_n; a.strideC = i_m * i_n;
+      a.batch = batch; a.epi = EPI_NONE;
+      {
+        OpTimer t(c, TNS_OP_GEMM);
+        if (int r = hip_status(launch_sgemm_nt_sdot(a, c->stream), "sgemm_nt launch")) return r;
+      }
+      return hip_status(launch_add_in_order(weight_updates, part, i_m * i_n, batch, c->stream),
+                        "dW accumulate launch");
+    }
     for (int64_t b = 0; b < batch; ++b)
       if (int r = do_gemm(c, false, true, i_m, i_n, i_k, 1.0f, delta + b * i_m * i_k, i_k, 0,
                           col + b * colSize, i_k, 0, 1.0f, weight_updates, i_n, 0, 1, EPI_NONE,
                           nullptr, 0))
         return r;
-  }
-  if (!state_delta) return TNS_OK;
-  if (fused_dx) {
-    // per image pixel: each window tap's ascending-f chain, added to the
-    // pixel in (kr, kc) order for the taps scol2im does not skip — the same
-    // roundings as the two stages below (646-660)
-    float* wt = nullptr;
-    if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
-    OpTimer t(c, TNS_OP_GEMM);
-    return hip_status(launch_conv_dx_col2im(weights, wt, delta, state_delta, batch, C, H, W,
-                                            filters, kSize, padding, dilation, g.oh, g.ow,
-                                            c->stream),
-                      "fused dX + col2im launch");
-  }
-  // col_b = W^T . delta_b (TN strided batched, weights shared, beta = 0 into
-  // the workspace), then col2im accumulates into state.delta (646-660).  All
-  // images in one launch on conv_tile4's k-major-A forms where they apply (a
-  // 1x1 "convolution" over the delta planes, the same chains), else the TN
-  // GEMM
-  bool done = false;
-  if (g_dx_tile != -2) {
-    const int dv = g_dx_tile >= 0 ? (int)g_dx_tile : conv_tile4_dx_pick(i_n, batch * i_k, i_m);
-    if (dv >= 0) {
+    return TNS_OK;
+  };
+
+  auto run_dx = [&]() -> int {
+    if (fused_dx) {
+      // per image pixel: each window tap's ascending-f chain, added to the
+      // pixel in (kr, kc) order for the taps scol2im does not skip — the same
+      // roundings as the two stages below (646-660)
+      float* wt = nullptr;
+      if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
       OpTimer t(c, TNS_OP_GEMM);
-      const hipError_t e = launch_conv_tile4_dx(dv, weights, delta, ws, batch, C, kSize, filters,
-                                                g.oh, g.ow, c->stream);
-      if (e == hipSuccess)
-        done = true;
-      else if (e != hipErrorInvalidValue || g_dx_tile >= 0)
-        return e == hipErrorInvalidValue
-                   ? set_error(TNS_ERR_UNSUPPORTED, "dX tile %d does not fit this layer", dv)
-                   : hip_status(e, "dX tile launch");
+      return hip_status(launch_conv_dx_col2im(weights, wt, delta, state_delta, batch, C, H, W,
+                                              filters, kSize, padding, dilation, g.oh, g.ow,
+                                              c->stream),
+                        "fused dX + col2im launch");
     }
+    // col_b = W^T . delta_b (TN strided batched, weights shared, beta = 0 into
+    // the workspace), then col2im accumulates into state.delta (646-660).  All
+    // images in one launch on conv_tile4's k-major-A forms where they apply (a
+    // 1x1 "convolution" over the delta planes, the same chains), else the TN
+    // GEMM
+    bool done = false;
+    if (g_dx_tile != -2) {
+      const int dv = g_dx_tile >= 0 ? (int)g_dx_tile : conv_tile4_dx_pick(i_n, batch * i_k, i_m);
+      if (dv >= 0) {
+        OpTimer t(c, TNS_OP_GEMM);
+        const hipError_t e = launch_conv_tile4_dx(dv, weights, delta, dx_ws, batch, C, kSize,
+                                                  filters, g.oh, g.ow, c->stream);
+        if (e == hipSuccess)
+          done = true;
+        else if (e != hipErrorInvalidValue || g_dx_tile >= 0)
+          return e == hipErrorInvalidValue
+                     ? set_error(TNS_ERR_UNSUPPORTED, "dX tile %d does not fit this layer", dv)
+                     : hip_status(e, "dX tile launch");
+      }
+    }
+    if (!done)
+      if (int r = do_gemm(c, true, false, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,
+                          i_m * i_k, 0.0f, dx_ws, i_k, colSize, batch, EPI_NONE, nullptr, 0, true))
+        return r;
+    OpTimer t(c, TNS_OP_COL2IM);
+    return hip_status(launch_col2im(g, dx_ws, colSize, state_delta, C * H * W, batch, c->stream),
+                      "col2im launch");
+  };
+
+  if (!overlap) {
+    if (int r = run_dw()) return r;
+    return state_delta ? run_dx() : TNS_OK;
   }
-  if (!done)
-    if (int r = do_gemm(c, true, false, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,
-                        i_m * i_k, 0.0f, ws, i_k, colSize, batch, EPI_NONE, nullptr, 0, true))
-      return r;
-  OpTimer t(c, TNS_OP_COL2IM);
-  return hip_status(launch_col2im(g, ws, colSize, state_delta, C * H * W, batch, c->stream),
-                    "col2im launch");
+  if (!c->aux_stream) {
+    TNS_HIP_TRY(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
+    TNS_HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
+    TNS_HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
+  }
+  TNS_HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+  TNS_HIP_TRY(hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+  int rx;
+  {
+    // state.delta's chain enqueued on the side stream (every launch inside
+    // run_dx goes to c->stream), the context's stream restored after
+    hipStream_t main = c->stream;
+    c->stream = c->aux_stream;
+    rx = run_dx();
+    c->stream = main;
+  }
+  // joined even after an error, so later work on the stream stays ordered
+  const hipError_t ej = hipEventRecord(c->ev_join, c->aux_stream);
+  const int rw = run_dw();
+  const hipError_t ew = ej == hipSuccess ? hipStreamWaitEvent(c->stream, c->ev_join, 0) : ej;
+  if (rx) return rx;
+  if (rw) return rw;
+  return hip_status(ew, "backward join");
 }
 }  // namespace
 

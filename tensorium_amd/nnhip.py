@@ -319,6 +319,11 @@ class TNNHip:
         (all bit-identical); process-wide."""
         check(self.lib.tns_set_option(9, int(form)))
 
+    def setBwdOverlap(self, on: bool = True):
+        """Conv backward: dW and state.delta concurrently on two streams (1)
+        or in sequence (0); same results; process-wide."""
+        check(self.lib.tns_set_option(10, 1 if on else 0))
+
     def convDwTiles(self) -> int:
         """Implicit-im2col dW tiles of the conv backward."""
         return int(self.lib.tns_conv_dw_tile_count())

@@ -243,6 +243,44 @@ def test_conv_backward_dx_tiles(hip, torch_cuda, ora):
     assert ran >= 2 * nv
 
 
+@pytest.mark.parametrize("idx", [2, 28, 45])
+def test_conv_backward_overlap_matches_sequential(hip, torch_cuda, ora, idx):
+    """dW and state.delta on two streams (TNS_OPT_BWD_OVERLAP = 1, the
+    default: state.delta's chain on the context's side stream with its own
+    col buffer) against the sequential schedule and the oracle: delta,
+    weight_updates, bias_updates and state.delta all identical (1x1 layer,
+    3x3 layers whose dW reads an im2col matrix)."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    spec = yolov3_conv_table()[idx]
+    batch, C, H, F, k, s, p = 8, spec.c, spec.h, spec.filters, spec.size, spec.stride, spec.pad
+    rng = np.random.default_rng(300 + idx)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.1, 0.1, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    sd0 = rng.uniform(-1, 1, x.shape).astype(np.float32)
+    rd, rbu, rwu, rsd = d0.copy(), bu0.copy(), wu0.copy(), sd0.copy()
+    ora.conv_backward(x, w, F, k, s, p, spec.activation, out, rd, rbu, rwu, rsd)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    got = []
+    try:
+        for mode in (True, False):
+            hip.setBwdOverlap(mode)
+            dx, dw, dout, dd, dbu, dwu, dsd = map(t, (x, w, out, d0, bu0, wu0, sd0))
+            hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, spec.activation, dout, dd, dbu,
+                             dwu, None, dsd)
+            hip.finish()
+            got.append([a.cpu().numpy() for a in (dd, dbu, dwu, dsd)])
+    finally:
+        hip.setBwdOverlap(True)
+    for g in got:
+        for a, r in zip(g, (rd, rbu, rwu, rsd)):
+            assert np.array_equal(a, r)
+
+
 @pytest.mark.parametrize("idx", [3, 11, 28, 45])
 def test_conv_backward_dx_yolov3_batch8(hip, torch_cuda, ora, idx):
     """state.delta at YOLOv3 layer shapes, batch 8, on the default path (the
