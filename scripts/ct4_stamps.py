@@ -10,6 +10,7 @@ import argparse
 import ctypes
 import json
 import sys
+import time
 from pathlib import Path
 
 import numpy as np
@@ -21,39 +22,54 @@ from tensorium_amd.nnhip import TNNHip  # noqa: E402
 from tensorium_amd.yolo import yolov3_conv_table  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--layer", type=int, default=11)
-ap.add_argument("--variant", type=int, default=106)
+ap.add_argument("--layer", default="11", help="layer index or comma list")
+ap.add_argument("--variant", type=int, default=-1, help="-1: the heuristic")
 ap.add_argument("--batch", type=int, default=8)
+ap.add_argument("--warm-ms", type=float, default=0.0, help="load before the stamped run")
 a = ap.parse_args()
 hip = TNNHip(0)
 lib = load()
 stamps = torch.zeros(8 * 65536, dtype=torch.int32, device="cuda")
 fn = lib.tns_debug_ct4_stamps
 fn.argtypes = [ctypes.c_void_p]
-s = yolov3_conv_table()[a.layer]
-x = torch.rand(a.batch, s.c, s.h, s.h, device="cuda")
-w = torch.rand(s.filters, s.K, device="cuda") * 0.2 - 0.1
-b = torch.rand(s.filters, device="cuda") * 0.2 - 0.1
-out = torch.empty(a.batch, s.filters, s.N, device="cuda")
-hip.setConvVariant(a.variant)
-run = lambda: hip.convForward(a.batch, s.c, s.h, s.h, x, w, b, s.filters, s.size, s.stride,  # noqa
-                              s.pad, 1, s.activation, None, out)
-for _ in range(20):
+for layer in map(int, a.layer.split(",")):
+    s = yolov3_conv_table()[layer]
+    x = torch.rand(a.batch, s.c, s.h, s.h, device="cuda")
+    w = torch.rand(s.filters, s.K, device="cuda") * 0.2 - 0.1
+    b = torch.rand(s.filters, device="cuda") * 0.2 - 0.1
+    out = torch.empty(a.batch, s.filters, s.N, device="cuda")
+    hip.setConvVariant(a.variant)
+    run = lambda: hip.convForward(a.batch, s.c, s.h, s.h, x, w, b, s.filters, s.size, s.stride,  # noqa
+                                  s.pad, 1, s.activation, None, out)
+    for _ in range(20):
+        run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < a.warm_ms:
+        for _ in range(10):
+            run()
+        torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    layer_ms = e0.elapsed_time(e1) / 20
+    stamps.zero_()
+    fn(stamps.data_ptr())
     run()
-torch.cuda.synchronize()
-fn(stamps.data_ptr())
-run()
-torch.cuda.synchronize()
-fn(None)
-st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 8).astype(np.float64)
-st = st[st[:, 7] > 0]
-nt = st[:, 7].astype(np.uint64) & 0xff
-rt = (st[:, 7].astype(np.uint64) >> 8).astype(np.float64)  # 100 MHz ticks
-nt = nt.astype(np.float64)
-names = ["top_loads", "groups_before_store", "stores", "to_barrier", "barrier_wait", "last_group_loop"]
-per_tile = {n: round(float(np.mean(st[:, i] / nt)), 1) for i, n in enumerate(names)}
-per_tile["total"] = round(float(np.mean(st[:, 6] / nt)), 1)
-clock_ghz = round(float(np.median(st[:, 6] / np.maximum(rt, 1) * 0.1)), 3)
-print(json.dumps({"layer": a.layer, "variant": a.variant, "blocks": int(len(st)),
-                  "k_tiles": int(nt[0]), "cycles_per_tile_wave0": per_tile,
-                  "clock_ghz_median": clock_ghz}))
+    torch.cuda.synchronize()
+    fn(None)
+    st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 8).astype(np.float64)
+    st = st[st[:, 7] > 0]
+    nt = st[:, 7].astype(np.uint64) & 0xff
+    rt = (st[:, 7].astype(np.uint64) >> 8).astype(np.float64)  # 100 MHz ticks
+    nt = nt.astype(np.float64)
+    names = ["top_loads", "groups_before_store", "stores", "to_barrier", "barrier_wait", "last_group_loop"]
+    per_tile = {n: round(float(np.mean(st[:, i] / nt)), 1) for i, n in enumerate(names)}
+    per_tile["total"] = round(float(np.mean(st[:, 6] / nt)), 1)
+    clock_ghz = round(float(np.median(st[:, 6] / np.maximum(rt, 1) * 0.1)), 3)
+    print(json.dumps({"layer": layer, "variant": a.variant, "blocks": int(len(st)),
+                      "k_tiles": int(nt[0]), "layer_ms": round(layer_ms, 4), "cycles_per_tile_wave0": per_tile,
+                      "clock_ghz_median": clock_ghz}))

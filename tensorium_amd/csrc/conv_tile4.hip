@@ -29,6 +29,15 @@
 //     tile's first fragments are read right after it, under those MFMAs, so
 //     no LDS latency is exposed at the tile boundary; the next tile's global
 //     loads are issued at the top of a tile and stored after group SG.
+//
+// Two other B staging forms, bit-identical, kept selectable (TNS_CT4D): BD
+// gathers by dword LDS-DMA straight into the slots, BW lets a lane fill whole
+// slots (four loads along k, one ds_write_b128, lanes along 64 pixels).  On
+// YOLOv3 layer 11 at a warm clock (scripts/ct4_stamps.py: 13.3 k cycles per
+// 64-deep tile, 11.26 k of them MFMA) both are slower: BD 0.127 ms (the DMA
+// issue doubles the tile-top phase), BW 0.123 ms (last group +0.86 k
+// cycles), against 0.115 ms — although a diagnostic build without the b32 B
+// stores runs 11.6 k cycles per tile (0.100 ms).
 #include <type_traits>
 
 #include "tns_act.hpp"
@@ -46,8 +55,18 @@ struct Frag4 {
 };
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
-          int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false>
+          int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
+          bool BD_ = false, bool BW_ = false>
 struct Geo4 {
+  // BW: a B gather lane fills whole 16-byte slots (its pixel's four k of one
+  // slot row: four dword loads, one ds_write_b128); lanes along 64
+  // consecutive pixels, the slot row wave-uniform (scalar k walk)
+  static constexpr bool BW = BW_;
+  // BD: B gathered straight into its LDS slots by dword LDS-DMA
+  // (buffer_load_dword ... lds; lanes = 16 pixels x the 4 slot components, so
+  // one wave-instruction fills 16 slots of a slot row): no staging registers,
+  // no ds_write, no wait on the gather before the mid-tile stores
+  static constexpr bool BD = BD_;
   // TA: A stored k-major ([K][M], gemm(Trans, ...)): a thread fills whole
   // 16-byte slots (four dword loads down k, one ds_write_b128); used for the
   // conv backward's col = W^T . delta as a 1x1 "convolution" over delta
@@ -89,6 +108,11 @@ struct Geo4 {
   static_assert(AU >= 1 && BM * BK / 4 % NT == 0 && KI >= 1 && BK / 4 % NW == 0, "geometry");
   static_assert(NA * JA + (WN - NA) * JB == J && NA >= 1 && NA <= WN, "wave column split");
   static_assert(2 * STAGE * 4 <= 163840, "LDS");
+  static_assert(!BD || (!IL && !ST && !TA), "DMA gather: tile-top issue only");
+  static_assert(!(BD && BW), "one gather form");
+  static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
+  static constexpr int BLD = BW ? KI * CH * 4 : KI * J;            // B loads per thread
+  static constexpr int BST = BW ? KI * CH : (BD ? 0 : KI * J);      // B LDS stores per thread
 };
 
 template <class G, int KS>
@@ -117,10 +141,15 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   const int H = p.conv_H, W = p.conv_W, HW = H * W;
 
   // ---- per-column state: window origin and the 9-bit tap validity mask ----
-  unsigned vbase[J], tmask[J];
+  // gather lanes: pixel gp of a 16-column fragment, slot component gq
+  // (BD: the DMA writes lane L to float 4 * (L >> 2) + (L & 3) of its row)
+  // (BW: lane = pixel of a 64-pixel chunk)
+  const int gp = G::BD ? lane >> 2 : r16, gq = G::BD ? lane & 3 : q;
+  constexpr int NCOL = G::BW ? G::CH : J;
+  unsigned vbase[NCOL], tmask[NCOL];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
-    int n = n0 + 16 * j + r16;
+  for (int j = 0; j < NCOL; ++j) {
+    int n = n0 + (G::BW ? 64 * j + lane : 16 * j + gp);
     n = n < N ? n : N - 1;  // past N: any valid pixel, never stored
     const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
     const int orow = pix / p.conv_ow, ocol = pix - orow * p.conv_ow;
@@ -141,11 +170,14 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
 
   // ---- B k-slots: slot sl = wm*KI + ii = 4g + r takes k = 16g + 4q + r (the
   // lane quarter is the slot component), advanced by BK per tile -------------
-  int kc_[KI], kr_[KI], cc_[KI];
+  // (BW: entry 4 ii + i = component i of slot row w*KI + ii, wave-uniform)
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  constexpr int NKS = G::BW ? 4 * KI : KI;
+  int kc_[NKS], kr_[NKS], cc_[NKS];
 #pragma unroll
-  for (int ii = 0; ii < KI; ++ii) {
-    const int sl = w * KI + ii;
-    const int k = 16 * (sl >> 2) + 4 * q + (sl & 3);
+  for (int ii = 0; ii < NKS; ++ii) {
+    const int sl = G::BW ? wu * KI + ii / 4 : w * KI + ii;
+    const int k = 16 * (sl >> 2) + 4 * (G::BW ? ii % 4 : gq) + (sl & 3);
     cc_[ii] = k / (KS * KS);
     const int rem = k - cc_[ii] * KS * KS;
     kr_[ii] = rem / KS;
@@ -153,7 +185,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   }
   auto advance = [&]() {  // k += BK
 #pragma unroll
-    for (int ii = 0; ii < KI; ++ii) {
+    for (int ii = 0; ii < NKS; ++ii) {
       if constexpr (KS == 1) {
         cc_[ii] += BK;
       } else {
@@ -167,8 +199,27 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       }
     }
   };
-  float rb[KI][J];
-  auto gather_b = [&]() {
+  float rb[KI][J];  // (unused with BD / BW)
+  floatx4 rw[G::BW ? KI : 1][G::BW ? G::CH : 1];  // (BW)
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem;
+  auto gather_b = [&](const float* bs) {
+    if constexpr (G::BW) {
+#pragma unroll
+      for (int ii = 0; ii < KI; ++ii)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int e = 4 * ii + i;
+          const unsigned x = 4u * (unsigned)(cc_[e] * HW + kr_[e] * dil * W + kc_[e] * dil);
+          const int tap = kr_[e] * KS + kc_[e];
+#pragma unroll
+          for (int c = 0; c < G::CH; ++c) {
+            const bool ok = __builtin_amdgcn_ubfe(tmask[c], tap, 1) != 0;
+            const unsigned off = ok ? vbase[c] + x : 0x80000000u;
+            rw[ii][c][i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+          }
+        }
+      return;
+    }
 #pragma unroll
     for (int ii = 0; ii < KI; ++ii) {
       const int y = kr_[ii] * dil, z = kc_[ii] * dil;
@@ -176,9 +227,26 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       const int tap = kr_[ii] * KS + kc_[ii];
 #pragma unroll
       for (int j = 0; j < J; ++j) {
-        const bool ok = __builtin_amdgcn_ubfe(tmask[j], tap, 1) != 0;
-        const unsigned off = ok ? vbase[j] + x : 0x80000000u;
-        rb[ii][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+        if constexpr (G::BD) {
+          const bool ok = __builtin_amdgcn_ubfe(tmask[j], tap, 1) != 0;
+          const unsigned off = ok ? vbase[j] + x : 0x80000000u;
+          const unsigned row = lds0 + 4u * (unsigned)((bs - smem) + ((wu * KI + ii) * BN + 16 * j) * 4);
+          unsigned keep;
+          asm volatile(
+              "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+              "buffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+              : "=&s"(keep)
+              : "v"(off), "s"(rsrc), "s"(row)
+              : "memory");
+        } else {
+#if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 1)
+          rb[ii][j] = (float)(x + j);  // diagnostic build: no B loads (timing only)
+#else
+          const bool ok = __builtin_amdgcn_ubfe(tmask[j], tap, 1) != 0;
+          const unsigned off = ok ? vbase[j] + x : 0x80000000u;
+          rb[ii][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0));
+#endif
+        }
       }
     }
   };
@@ -187,10 +255,22 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
 #pragma unroll
   for (int ii = 0; ii < KI; ++ii) b_dst[ii] = (w * KI + ii) * BN * 4 + r16 * 4 + q;
   auto store_b = [&](float* bs) {
+#if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 2)
+    return;  // diagnostic build: no B stores (timing only)
+#endif
+    if constexpr (G::BW) {
 #pragma unroll
-    for (int ii = 0; ii < KI; ++ii)
+      for (int ii = 0; ii < KI; ++ii)
 #pragma unroll
-      for (int j = 0; j < J; ++j) bs[b_dst[ii] + 64 * j] = rb[ii][j];
+        for (int c = 0; c < G::CH; ++c)
+          if (64 * (c + 1) <= BN || 64 * c + lane < BN)
+            *reinterpret_cast<floatx4*>(bs + ((wu * KI + ii) * BN + 64 * c + lane) * 4) = rw[ii][c];
+    } else if constexpr (!G::BD) {  // (BD: landed by the DMA)
+#pragma unroll
+      for (int ii = 0; ii < KI; ++ii)
+#pragma unroll
+        for (int j = 0; j < J; ++j) bs[b_dst[ii] + 64 * j] = rb[ii][j];
+    }
   };
 
   // ---- A staging (weights [M][K]): unit = k-quad kq4 of row m; its four
@@ -216,6 +296,10 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   }
   float4 ra[AU];
   auto load_a = [&](int k0) {
+#if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 4)
+    for (int u = 0; u < AU; ++u) ra[u] = make_float4(k0, k0 + 1, k0 + 2, k0 + 3);
+    return;  // diagnostic build: no A loads (timing only)
+#endif
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       if constexpr (G::TA) {
@@ -227,6 +311,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   };
   auto store_a = [&](float* as) {
+#if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 8)
+    return;  // diagnostic build: no A stores (timing only)
+#endif
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       if constexpr (G::TA) {
@@ -283,9 +370,10 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   Frag f0, f1;
   if (nt > 0) {
     load_a(0);
-    gather_b();
+    gather_b(smem + A_TILE);
     store_a(smem);
     store_b(smem + A_TILE);
+    if constexpr (G::BD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     frag(smem, 0, f0);
   }
@@ -296,8 +384,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     TNS_PH(5);
     if constexpr (more && !G::IL && !G::ST) {
       advance();
-      load_a((t + 1) * BK);
-      gather_b();
+      if constexpr (G::BD) {
+        gather_b(nxt + A_TILE);
+        load_a((t + 1) * BK);
+      } else {
+        load_a((t + 1) * BK);
+        gather_b(nxt + A_TILE);
+      }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
     }
     TNS_PH(0);
@@ -310,6 +403,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           // every wave's stores of tile t+1 are in; its first group is read
           // under this group's MFMAs
           TNS_PH(3);
+          if constexpr (G::BD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
           TNS_PH(4);
         }
@@ -318,7 +412,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
         if (g < 2 && half == g) {
           advance();
           load_a((t + 1) * BK);
-          gather_b();
+          gather_b(nxt + A_TILE);
           __builtin_amdgcn_sched_barrier(0);
         }
       // one scheduling region per group: the next group's fragment reads,
@@ -332,7 +426,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
         if (g == 0) {
           advance();
           load_a((t + 1) * BK);
-          gather_b();
+          gather_b(nxt + A_TILE);
         }
       }
       if constexpr (more && G::SI) {
@@ -352,10 +446,10 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           if constexpr (more && G::IL > 0)
             if (g == 0) {
               __builtin_amdgcn_sched_group_barrier(0x002, G::IL, 0);  // IL VALU
-              if (i < AU + KI * J) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // a load
+              if (i < AU + G::BLD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // a load
             }
           if constexpr (more && G::SI)
-            if (g == G::SG && i < 4 * AU + KI * J)
+            if (g == G::SG && i < 4 * AU + G::BST)
               __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // a store
         }
       }
@@ -458,6 +552,16 @@ struct TileInfo4 {
   {BMv, BNv, BKv, launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv>>, \
    "conv_tile4<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv    \
    ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4D(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, BDv, BWv)                          \
+  {BMv, BNv, BKv,                                                                            \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, 0, 0, false, BDv, BWv>>, \
+   "conv_tile4<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv    \
+   ",bd" #BDv ",bw" #BWv ">"}
+#define TNS_CT4UD(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv, BDv, BWv)                 \
+  {BMv, BNv, BKv,                                                                              \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, false, BDv, BWv>>, \
+   "conv_tile4<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv      \
+   ",j" #JAv "x" #NAv ",bd" #BDv ",bw" #BWv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -487,6 +591,11 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
     TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
     TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
+    // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
+    // than the register-staged b32 stores on every class (kept selectable)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 25 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 26 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 27 (18, BW)
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
 #define TNS_CT4T(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                      \
@@ -510,6 +619,8 @@ const TileInfo4 kTiles4T[] = {
 constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
 #undef TNS_CT4
 #undef TNS_CT4U
+#undef TNS_CT4D
+#undef TNS_CT4UD
 #undef TNS_CT4T
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
