@@ -331,6 +331,7 @@ constexpr int kT4Narrow = 21;    // 128 x 48 x 64, stores and reads interleaved
 
 // variants kNumTiles + v: conv_tile4.hip's form v (k-permuted b128 fragments)
 int conv_tile_count() { return kNumTiles + conv_tile4_count(); }
+bool conv_tile_is_ap(int v) { return v >= kNumTiles && conv_tile4_is_ap(v - kNumTiles); }
 const char* conv_tile_name(int v) {
   return v >= 0 && v < kNumTiles ? kTiles[v].name : conv_tile4_name(v - kNumTiles);
 }

@@ -37,7 +37,10 @@
 // 64-deep tile, 11.26 k of them MFMA) both are slower: BD 0.127 ms (the DMA
 // issue doubles the tile-top phase), BW 0.123 ms (last group +0.86 k
 // cycles), against 0.115 ms — although a diagnostic build without the b32 B
-// stores runs 11.6 k cycles per tile (0.100 ms).
+// stores runs 11.6 k cycles per tile (0.100 ms).  Likewise AP (A by 16-byte
+// LDS-DMA from a slot-ordered copy of the weights made per call): 0.120 ms.
+#include <algorithm>
+#include <cstring>
 #include <type_traits>
 
 #include "tns_act.hpp"
@@ -56,8 +59,14 @@ struct Frag4 {
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
           int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
-          bool BD_ = false, bool BW_ = false>
+          bool BD_ = false, bool BW_ = false, bool AP_ = false>
 struct Geo4 {
+  // AP: A read from a pre-permuted copy of the weights (conv_tile4_permute:
+  // slot row R = 4g + q of the whole K, then m, then the slot's 4 values), so
+  // a tile's slot row is contiguous and arrives by 16-byte LDS-DMA
+  // (global_load_lds_dwordx4, 64 slots per wave-instruction): no A staging
+  // registers and no transposing stores
+  static constexpr bool AP = AP_;
   // BW: a B gather lane fills whole 16-byte slots (its pixel's four k of one
   // slot row: four dword loads, one ds_write_b128); lanes along 64
   // consecutive pixels, the slot row wave-uniform (scalar k walk)
@@ -110,6 +119,10 @@ struct Geo4 {
   static_assert(2 * STAGE * 4 <= 163840, "LDS");
   static_assert(!BD || (!IL && !ST && !TA), "DMA gather: tile-top issue only");
   static_assert(!(BD && BW), "one gather form");
+  static_assert(!AP || (!IL && !ST && !TA && BM % 64 == 0 && ROWS * BM % (64 * NW) == 0),
+                "A DMA: tile-top issue, whole 64-slot pieces");
+  static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
+  static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
   static constexpr int BLD = BW ? KI * CH * 4 : KI * J;            // B loads per thread
   static constexpr int BST = BW ? KI * CH : (BD ? 0 : KI * J);      // B LDS stores per thread
@@ -294,8 +307,26 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       a_dst[u] = (4 * (kq4 >> 2)) * BM * 4 + m * 4 + (kq4 & 3);
     }
   }
-  float4 ra[AU];
-  auto load_a = [&](int k0) {
+  float4 ra[AU];  // (unused with AP)
+  auto load_a = [&](int k0, float* as) {
+    if constexpr (G::AP) {
+#pragma unroll
+      for (int u = 0; u < G::ADM; ++u) {
+        const int idx = wu * G::ADM + u, R = idx / (BM / 64), c = idx % (BM / 64);
+        const float* src = p.A + ((int64_t)(k0 / 4 + R) * p.M + m0 + 64 * c + lane) * 4;
+        const unsigned dst = lds0 + 4u * (unsigned)((as - smem) + (R * BM + 64 * c) * 4);
+        unsigned keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+            "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(src), "s"(dst)
+            : "memory");
+      }
+      return;
+    } else {
+      (void)as;
+    }
 #if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 4)
     for (int u = 0; u < AU; ++u) ra[u] = make_float4(k0, k0 + 1, k0 + 2, k0 + 3);
     return;  // diagnostic build: no A loads (timing only)
@@ -311,6 +342,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   };
   auto store_a = [&](float* as) {
+    if constexpr (G::AP) return;  // (landed by the DMA)
 #if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 8)
     return;  // diagnostic build: no A stores (timing only)
 #endif
@@ -369,11 +401,11 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   const int nt = K / BK;
   Frag f0, f1;
   if (nt > 0) {
-    load_a(0);
+    load_a(0, smem);
     gather_b(smem + A_TILE);
     store_a(smem);
     store_b(smem + A_TILE);
-    if constexpr (G::BD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (G::BD || G::AP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     frag(smem, 0, f0);
   }
@@ -386,9 +418,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       advance();
       if constexpr (G::BD) {
         gather_b(nxt + A_TILE);
-        load_a((t + 1) * BK);
+        load_a((t + 1) * BK, nxt);
       } else {
-        load_a((t + 1) * BK);
+        load_a((t + 1) * BK, nxt);
         gather_b(nxt + A_TILE);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
@@ -403,7 +435,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           // every wave's stores of tile t+1 are in; its first group is read
           // under this group's MFMAs
           TNS_PH(3);
-          if constexpr (G::BD) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if constexpr (G::BD || G::AP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           __syncthreads();
           TNS_PH(4);
         }
@@ -411,7 +443,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (more && G::ST)
         if (g < 2 && half == g) {
           advance();
-          load_a((t + 1) * BK);
+          load_a((t + 1) * BK, nxt);
           gather_b(nxt + A_TILE);
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -425,7 +457,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (more && G::IL) {
         if (g == 0) {
           advance();
-          load_a((t + 1) * BK);
+          load_a((t + 1) * BK, nxt);
           gather_b(nxt + A_TILE);
         }
       }
@@ -449,7 +481,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
               if (i < AU + G::BLD) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // a load
             }
           if constexpr (more && G::SI)
-            if (g == G::SG && i < 4 * AU + G::BST)
+            if (g == G::SG && i < G::AST + G::BST)
               __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);  // a store
         }
       }
@@ -562,6 +594,12 @@ struct TileInfo4 {
    launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, false, BDv, BWv>>, \
    "conv_tile4<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv      \
    ",j" #JAv "x" #NAv ",bd" #BDv ",bw" #BWv ">"}
+#define TNS_CT4A(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                                 \
+  {BMv, BNv, BKv,                                                                                \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, false, false, false, \
+                  true>>,                                                                        \
+   "conv_tile4_ap<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv      \
+   ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -596,6 +634,10 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 25 (3, BD)
     TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 26 (3, BW)
     TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 27 (18, BW)
+    // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
+    // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
+    // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 28 (3)
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
 #define TNS_CT4T(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                      \
@@ -620,13 +662,34 @@ constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
 #undef TNS_CT4
 #undef TNS_CT4U
 #undef TNS_CT4D
+#undef TNS_CT4A
 #undef TNS_CT4UD
 #undef TNS_CT4T
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
 
+__global__ void permute_weights_kernel(const float* __restrict__ A, float* __restrict__ Ap, int M,
+                                       int K, int64_t n) {
+  // Ap[((R * M) + m) * 4 + i] = A[m][16 (R >> 2) + 4 i + (R & 3)]
+  for (int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; o < n;
+       o += (int64_t)gridDim.x * blockDim.x) {
+    const int i = (int)(o & 3);
+    const int64_t rest = o >> 2;
+    const int m = (int)(rest % M), R = (int)(rest / M);
+    Ap[o] = A[(int64_t)m * K + 16 * (R >> 2) + 4 * i + (R & 3)];
+  }
+}
+
 int conv_tile4_count() { return kNumTiles4; }
+bool conv_tile4_is_ap(int v) { return v >= 0 && v < kNumTiles4 && std::strstr(kTiles4[v].name, "_ap<"); }
+hipError_t conv_tile4_permute(const float* A, float* Ap, int64_t M, int64_t K, hipStream_t s) {
+  if (M <= 0 || K % 16 || M * K > 0x7fffffffLL) return hipErrorInvalidValue;
+  const int64_t n = M * K;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(permute_weights_kernel, dim3(blocks), dim3(256), 0, s, A, Ap, (int)M, (int)K, n);
+  return hipGetLastError();
+}
 const char* conv_tile4_name(int v) { return v >= 0 && v < kNumTiles4 ? kTiles4[v].name : ""; }
 int conv_tile4_bk(int v) { return v >= 0 && v < kNumTiles4 ? kTiles4[v].bk : 0; }
 

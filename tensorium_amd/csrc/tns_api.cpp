@@ -69,7 +69,7 @@ struct tns_ctx {
   // 0 col workspace, 1 padded images / host staging, 2-3 host staging,
   // 4 per-image dW partial sums of the conv backward, 5 per-block results of
   // the batch-norm reductions
-  static constexpr int kSlots = 9;
+  static constexpr int kSlots = 10;
   float* scratch[kSlots] = {};
   size_t scratch_elems[kSlots] = {};
   // telemetry (TTensorMetrics-style, nopmetrics.pas:25-44)
@@ -91,7 +91,7 @@ struct tns_ctx {
 namespace {
 
 enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5,
-       SLOT_MLP = 6, SLOT_WT = 7, SLOT_COL_DX = 8 };
+       SLOT_MLP = 6, SLOT_WT = 7, SLOT_COL_DX = 8, SLOT_WPERM = 9 };
 
 int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   if (elems < 1) elems = 1;
@@ -1269,6 +1269,17 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
       if (g_conv_variant >= 400 && ev < 0)
         return set_error(TNS_ERR_UNSUPPORTED, "conv_patch needs a 3x3 stride-1 pad-1 layer");
       if (tv >= 0) {
+        // forms reading A from the slot-ordered weights: permute them first
+        const float* wA = weights;
+        if (tv < 1000 && conv_tile_is_ap(tv)) {
+          float* wp = nullptr;
+          if (int r = ensure_scratch(c, SLOT_WPERM, filters * k, &wp)) return r;
+          OpTimer t(c, TNS_OP_GEMM);
+          if (int r = hip_status(conv_tile4_permute(weights, wp, filters, k, c->stream),
+                                 "weight permute launch"))
+            return r;
+          wA = wp;
+        }
         const int64_t chunk = std::max<int64_t>(
             1, std::min<int64_t>(0x7fffffffLL / (4 * img0),
                                  0x7fffffffLL / std::max<int64_t>(outImg, 1)));
@@ -1277,7 +1288,7 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
           GemmArgs a{};
           a.M = filters; a.N = nb * outImg; a.K = k;
           a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_ZERO;
-          a.A = weights; a.lda = k; a.strideA = 0;
+          a.A = wA; a.lda = k; a.strideA = 0;
           a.B = input + b0 * img0; a.ldb = outImg; a.strideB = img0;
           a.C = out + b0 * outImg * filters; a.ldc = outImg; a.strideC = outImg * filters;
           a.batch = 1; a.epi = bias_act ? EPI_BIAS_ACT : EPI_NONE; a.bias = biases;

@@ -123,6 +123,12 @@ hipError_t launch_conv_tile(int v, const GemmArgs& a, int ks, int dil, hipStream
 // (conv_tile4.hip; K % the form's k-tile == 0): conv_tile variants
 // conv_tile_count() - conv_tile4_count() + v
 int conv_tile4_count();
+// conv_tile4 forms that read A from a pre-permuted copy of the weights
+// (conv_tile4_permute into M*K floats of scratch first); conv_tile_is_ap
+// takes a conv_tile index (conv_tile.hip)
+bool conv_tile4_is_ap(int v);
+bool conv_tile_is_ap(int v);
+hipError_t conv_tile4_permute(const float* A, float* Ap, int64_t M, int64_t K, hipStream_t s);
 const char* conv_tile4_name(int v);
 int conv_tile4_bk(int v);
 hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
