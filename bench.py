@@ -74,6 +74,12 @@ def _free_port() -> int:
     return port
 
 
+def profiler_preloaded(env) -> bool:
+    """rocprofv3 / roctracer injected into this process (LD_PRELOAD)."""
+    preload = env.get("LD_PRELOAD", "")
+    return any(tag in preload for tag in ("rocprof", "roctracer", "rocprofiler"))
+
+
 def launch_ranks(args) -> int | None:
     """One process per GPU.  Returns None when this process is a rank (the
     caller goes on to benchmark), else the launcher's exit code.
@@ -95,29 +101,58 @@ def launch_ranks(args) -> int | None:
         return None
     if args.gpus <= 1:
         return None
+    # A profiler's preloaded library has already initialised the GPU in this
+    # process: starting ranks from here would be a spawn after GPU init.
+    # Profile a multi-GPU run through torchrun (WORLD_SIZE set) instead.
+    if profiler_preloaded(os.environ):
+        print("bench.py: a profiler library is preloaded; refusing to start rank processes "
+              "from a profiled launcher (run the ranks under torchrun)", file=sys.stderr,
+              flush=True)
+        return 2
+    import signal
     import subprocess
     port = str(_free_port())
     procs = []
-    for r in range(args.gpus):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] +
-                                      sys.argv[1:], env=env))
     rc = 0
-    alive = list(procs)
-    while alive:
-        for p in list(alive):
-            code = p.poll()
-            if code is None:
-                continue
-            alive.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 1
-                print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the other "
-                      f"ranks", file=sys.stderr, flush=True)
-                for q in alive:
-                    q.terminate()
-        time.sleep(0.05)
+
+    def stop(signum, _frame):   # a timeout or Ctrl-C of the launcher stops the ranks
+        raise KeyboardInterrupt(signum)
+
+    old = {sig: signal.signal(sig, stop) for sig in (signal.SIGTERM, signal.SIGHUP)}
+    try:
+        for r in range(args.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                       LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=port)
+            procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] +
+                                          sys.argv[1:], env=env))
+        alive = list(procs)
+        while alive:
+            for p in list(alive):
+                code = p.poll()
+                if code is None:
+                    continue
+                alive.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    print(f"bench.py: rank {procs.index(p)} exited with {code}; stopping the "
+                          f"other ranks", file=sys.stderr, flush=True)
+                    for q in alive:
+                        q.terminate()
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        rc = rc or 130
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        for sig, h in old.items():
+            signal.signal(sig, h)
     return rc
 
 
@@ -127,6 +162,10 @@ def dry_run(args):
     from tensorium_amd import dist as tdist
     if os.environ.get("TNS_DRYRUN_FAIL_RANK") == os.environ.get("RANK", "0"):
         sys.exit(3)   # test hook: a rank that dies before the rendezvous
+    if os.environ.get("TNS_DRYRUN_HANG_DIR"):   # test hook: ranks that never finish
+        Path(os.environ["TNS_DRYRUN_HANG_DIR"], f"rank{os.environ.get('RANK', '0')}").write_text(
+            str(os.getpid()))
+        time.sleep(3600)
     ctx = tdist.init("gloo", use_gpu=False)
     ranks = ctx.gather_floats([float(ctx.rank), float(os.getpid())])
     t = ctx.max(float(ctx.rank))

@@ -169,6 +169,20 @@ int tns_hip_gemm_strided_batched(tns_ctx* ctx, uint8_t transA, uint8_t transB,
                                  float BETA, float* C, int64_t cOffset, int64_t ldc, int64_t strideC,
                                  int64_t batchCount);
 
+/* TNNCuda.gemmBatched — nncuda.pas:727-760 (cublasSgemmBatched_64 over
+ * arrays of matrix pointers).  A, B, C are arrays of batchCount pointers,
+ * device-resident as the reference builds them with writeBuffer
+ * (nConvolutionLayer.pas:1083-1085) or host-resident; the element offsets
+ * apply to every entry.  The arrays are read in stream order (the call
+ * waits for them); equally spaced entries run as one strided-batched
+ * launch, others GEMM by GEMM in array order.  Results as tns_hip_gemm. */
+int tns_hip_gemm_batched(tns_ctx* ctx, uint8_t transA, uint8_t transB,
+                         int64_t M, int64_t N, int64_t K, float ALPHA,
+                         const float* const* A, int64_t aOffset, int64_t lda,
+                         const float* const* B, int64_t bOffset, int64_t ldb,
+                         float BETA, float* const* C, int64_t cOffset, int64_t ldc,
+                         int64_t batchCount);
+
 /* TNNCuda.im2col — nncuda.pas:1144 (output layout = CPU sim2Col). */
 int tns_hip_im2col(tns_ctx* ctx, int64_t aChannels, int64_t aHeight, int64_t aWidth,
                    int64_t kernelHeight, int64_t kernelWidth, int64_t padHeight, int64_t padWidth,
@@ -285,6 +299,17 @@ int tns_hip_yolo_forward(tns_ctx* ctx, int64_t batch, int64_t anchors, int64_t c
 /* meansAndVars: blockSize = srcSize/(dstSize*groups); unbiased variance */
 int tns_hip_means_and_vars(tns_ctx* ctx, int64_t srcSize, int64_t dstSize, int64_t groups,
                            const float* src, int64_t offset, float* means, float* vars);
+/* TNNCuda.means / TNNCuda.variances — nncuda.pas:1330-1369, the pair the
+ * reference's batchNormGPU (nbaselayer.pas:583-584) and
+ * TConnectedLayer.forwardGPU (nconnectedlayer.pas:664-665) call.  Same
+ * blockSize and results as the two halves of tns_hip_means_and_vars (CPU
+ * MeansAndVars order, ntensors.pas:9102-9177: vssum_avx2 lanes per block for
+ * the mean, srss lanes about the GIVEN means for the unbiased variance,
+ * TNS_OPT_SRSS_QUIRK applying to the latter). */
+int tns_hip_means(tns_ctx* ctx, int64_t srcSize, int64_t dstSize, int64_t groups,
+                  const float* src, int64_t offset, float* means);
+int tns_hip_variances(tns_ctx* ctx, int64_t srcSize, int64_t dstSize, int64_t groups,
+                      const float* src, int64_t offset, const float* means, float* vars);
 /* normalize: blockSize = dstSize/(srcSize*groups); bs==1: (x-m)/sqrt(max(v,eps)),
  * bs>1: (x-m)/max(sqrt(v),eps) */
 int tns_hip_normalize(tns_ctx* ctx, int64_t srcSize, int64_t dstSize, int64_t groups,
@@ -495,9 +520,12 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * TNS_OPT_NT_SDOT (default 1): gemm(NoTrans, Trans) sums in the reference's
  * sdot_avx2 order (8 residue chains, ntensors.pas:1233-1306, 1957-2005), bit
  * for bit; 0 = one ascending-k chain per element (faster, within 1e-4).
- * TNS_OPT_SRSS_QUIRK (default 0): 1 reproduces the reference's srss dropping
- * lanes 4..7 of the variance sum when a block is a multiple of 8 long
- * (ntensors.pas:1493-1523, meansAndVars with blockSize % 8 == 0).
+ * TNS_OPT_SRSS_QUIRK (library default 0): 1 reproduces the reference's srss
+ * dropping lanes 4..7 of the variance sum when a block is a multiple of 8
+ * long (ntensors.pas:1493-1523, meansAndVars with blockSize % 8 == 0; and
+ * sVarinceDelta_avx, 8739-8741).  The Pascal binding's initHIP and
+ * useHipOpTable (pascal/nnHip.pas) set it to 1 by default, so a drop-in
+ * reproduces the configured USE_AVX2 CPU build.
  * TNS_OPT_TT_EXACT (default 1): gemm(Trans, Trans) sums in the reference's
  * scalar s_tt order (mul, mul, add each rounded; ntensors.pas:2159-2182) on
  * the VALU, bit for bit; 0 = the fp32 MFMA kernel (faster, within 1e-4).
@@ -528,7 +556,14 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * the state.delta chain (which read delta and write disjoint outputs)
  * concurrently, the latter on a side stream of the context that the
  * context's stream waits for before the call returns its work; 0 = in
- * sequence (also whenever telemetry is on).  Same results either way. */
+ * sequence (also whenever telemetry is on).  Same results either way.
+ * Memory: when dW reads an im2col matrix and state.delta takes the TN +
+ * col2im chain, the overlap gives that chain its own batch*C*k*k*oH*oW-float
+ * col buffer, allocated by the context IN ADDITION to the caller's workspace
+ * (which then holds dW's col matrix only); if that allocation fails, or the
+ * side stream cannot be created, the call runs in sequence within the
+ * caller's workspace instead of failing.  Set 0 to bound the backward's
+ * memory to the workspace. */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,

@@ -249,6 +249,7 @@ _PROTO2 = {
     "ora_means_and_vars": (None, [fp, i64, i64, i64, fp, fp]),
     "ora_means_and_vars_q": (None, [fp, i64, i64, i64, fp, fp, i32]),
     "ora_normalize": (None, [fp, i64, i64, i64, fp, fp]),
+    "ora_batch_norm": (None, [fp, i64, i64, i64, fp, fp, fp, fp, f32, i32, fp, fp, fp, fp, i32]),
     "ora_forward_scale": (None, [fp, i64, i64, i64, fp]),
     "ora_add_dots": (None, [fp, fp, fp, i64, i64, i64]),
     "ora_add_sums": (None, [fp, fp, i64, i64, i64]),
@@ -291,6 +292,17 @@ def means_and_vars(x, groups, N, bs, quirk=0):
 def normalize(x, groups, N, bs, m, v):
     _lib2().ora_normalize(_p(x), groups, N, bs, _p(m), _p(v))
     return x
+
+
+def batch_norm(out, groups, N, bs, scales, biases, rmean, rvar, momentum, training, quirk=0):
+    """Restated TBaseLayer.batchNorm (nbaselayer.pas:336-370) on out in place;
+    rmean / rvar updated in place; returns (mean, var, x, x_norm)."""
+    m, v = np.zeros(N, np.float32), np.zeros(N, np.float32)
+    x, xn = np.zeros_like(out), np.zeros_like(out)
+    _lib2().ora_batch_norm(_p(out), groups, N, bs, _p(scales), _p(biases), _p(rmean), _p(rvar),
+                           float(momentum), int(bool(training)), _p(m), _p(v), _p(x), _p(xn),
+                           int(quirk))
+    return m, v, x, xn
 
 
 def forward_scale(x, groups, N, bs, s):

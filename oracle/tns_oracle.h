@@ -132,6 +132,13 @@ void    ora_conv_forward_train(int64_t batch, int64_t C, int64_t H, int64_t W,
                                float* rolling_mean, float* rolling_variance, float momentum,
                                int32_t training, float* mean, float* variance, float* x,
                                float* x_norm, float* workspace, float* out, int32_t quirk);
+/* TBaseLayer.batchNorm (nbaselayer.pas:336-370) over out [groups][N][bs] in
+ * place (see tns_oracle_train.c). */
+void ora_batch_norm(float* out, int64_t groups, int64_t N, int64_t bs, const float* scales,
+                    const float* biases, float* rolling_mean, float* rolling_variance,
+                    float momentum, int32_t training, float* mean, float* variance, float* x,
+                    float* x_norm, int32_t quirk);
+
 /* TConvolutionalLayer.backward with batch norm: Derivative, batchNormBack
  * (nbaselayer.pas:372-395: addDots into scale_updates, forwardScale,
  * MeansAndVarsDelta, normalizeDelta — no bias_updates term), then the

@@ -245,6 +245,35 @@ void ora_normalize_delta(const float* x, const float* mean, const float* var,
     }
 }
 
+/* ---- TBaseLayer.batchNorm (nbaselayer.pas:336-370) --------------------------
+ * output [groups][N][bs] in place: training: MeansAndVars, rolling update
+ * (Multiply(1-m), then axpy(m, stat) as a saxpy FMA), CopyTo(x),
+ * blockNormalize, copyTo(x_norm); otherwise blockNormalize with the rolling
+ * statistics; then forwardScale (vsMulB) and forwardBias (vsAddB). */
+void ora_batch_norm(float* out, int64_t groups, int64_t N, int64_t bs, const float* scales,
+                    const float* biases, float* rolling_mean, float* rolling_variance,
+                    float momentum, int32_t training, float* mean, float* variance, float* x,
+                    float* x_norm, int32_t quirk) {
+  const int64_t n = groups * N * bs;
+  if (training) {
+    ora_means_and_vars_q(out, groups, N, bs, mean, variance, quirk);
+    const float keep = 1.0f - momentum;
+    for (int64_t i = 0; i < N; i++) {
+      rolling_mean[i] = rolling_mean[i] * keep;
+      rolling_mean[i] = fmaf(momentum, mean[i], rolling_mean[i]);
+      rolling_variance[i] = rolling_variance[i] * keep;
+      rolling_variance[i] = fmaf(momentum, variance[i], rolling_variance[i]);
+    }
+    memcpy(x, out, sizeof(float) * n);
+    ora_normalize(out, groups, N, bs, mean, variance);
+    memcpy(x_norm, out, sizeof(float) * n);
+  } else {
+    ora_normalize(out, groups, N, bs, rolling_mean, rolling_variance);
+  }
+  ora_forward_scale(out, groups, N, bs, scales);
+  ora_add_bias(N, out, bs, biases, 1, groups);
+}
+
 /* ---- convolutional layer with batch norm (training) ----------------------- */
 void ora_conv_forward_train(int64_t batch, int64_t C, int64_t H, int64_t W, const float* input,
                             const float* weights, int64_t filters, int64_t kSize, int64_t stride,
@@ -259,23 +288,8 @@ void ora_conv_forward_train(int64_t batch, int64_t C, int64_t H, int64_t W, cons
   const int64_t bs = (H + 2 * padding - (dilation * (kSize - 1) + 1)) / stride + 1;
   const int64_t bsw = (W + 2 * padding - (dilation * (kSize - 1) + 1)) / stride + 1;
   const int64_t blk = bs * bsw, n = batch * filters * blk;
-  if (training) { /* TBaseLayer.batchNorm (nbaselayer.pas:351-359) */
-    ora_means_and_vars_q(out, batch, filters, blk, mean, variance, quirk);
-    const float keep = 1.0f - momentum;
-    for (int64_t i = 0; i < filters; i++) { /* Multiply(1-m), then axpy(m, stat) (saxpy FMA) */
-      rolling_mean[i] = rolling_mean[i] * keep;
-      rolling_mean[i] = fmaf(momentum, mean[i], rolling_mean[i]);
-      rolling_variance[i] = rolling_variance[i] * keep;
-      rolling_variance[i] = fmaf(momentum, variance[i], rolling_variance[i]);
-    }
-    memcpy(x, out, sizeof(float) * n);
-    ora_normalize(out, batch, filters, blk, mean, variance);
-    memcpy(x_norm, out, sizeof(float) * n);
-  } else {
-    ora_normalize(out, batch, filters, blk, rolling_mean, rolling_variance);
-  }
-  ora_forward_scale(out, batch, filters, blk, scales); /* forwardScale (vsMulB) */
-  ora_add_bias(filters, out, blk, biases, 1, batch);  /* forwardBias (vsAddB) */
+  ora_batch_norm(out, batch, filters, blk, scales, biases, rolling_mean, rolling_variance,
+                 momentum, training, mean, variance, x, x_norm, quirk);
   ora_activate(out, n, act);
 }
 

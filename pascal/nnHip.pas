@@ -115,6 +115,9 @@ function tns_hip_read_buffer(ctx: PTnsCtx; dev: THipMem; bytes: int64; host: poi
 function tns_hip_gemm(ctx: PTnsCtx; transA, transB: boolean; M, N, K: int64; ALPHA: single;
   A: THipMem; aOffset, lda: int64; B: THipMem; bOffset, ldb: int64; BETA: single; C: THipMem;
   cOffset, ldc: int64): longint; cdecl; external libtns;
+function tns_hip_gemm_batched(ctx: PTnsCtx; transA, transB: boolean; M, N, K: int64;
+  ALPHA: single; A: PHipMem; aOffset, lda: int64; B: PHipMem; bOffset, ldb: int64;
+  BETA: single; C: PHipMem; cOffset, ldc, batchCount: int64): longint; cdecl; external libtns;
 function tns_hip_gemm_strided_batched(ctx: PTnsCtx; transA, transB: boolean; M, N, K: int64;
   ALPHA: single; A: THipMem; aOffset, lda, strideA: int64; B: THipMem; bOffset, ldb,
   strideB: int64; BETA: single; C: THipMem; cOffset, ldc, strideC, batchCount: int64): longint;
@@ -183,6 +186,10 @@ function tns_hip_yolo_forward(ctx: PTnsCtx; batch, anchors, classes, hw: int64; 
 
 { batch norm / softmax }
 function tns_hip_means_and_vars(ctx: PTnsCtx; srcSize, dstSize, groups: int64; src: THipMem;
+  offset: int64; means, vars: THipMem): longint; cdecl; external libtns;
+function tns_hip_means(ctx: PTnsCtx; srcSize, dstSize, groups: int64; src: THipMem;
+  offset: int64; means: THipMem): longint; cdecl; external libtns;
+function tns_hip_variances(ctx: PTnsCtx; srcSize, dstSize, groups: int64; src: THipMem;
   offset: int64; means, vars: THipMem): longint; cdecl; external libtns;
 function tns_hip_normalize(ctx: PTnsCtx; srcSize, dstSize, groups: int64; means: THipMem;
   meansStride: int64; vars: THipMem; varsStride: int64; dst: THipMem; dstOffset: int64): longint;
@@ -348,8 +355,11 @@ var
   hip: TNNHip<single> = nil;
 
 { initCUDART twin (ntensors.pas:6191-6210): one context per process, created
-  once; device buffers of TTensor mirror as under USE_CUDART. }
-procedure initHIP(const deviceIndex: SizeInt);
+  once; device buffers of TTensor mirror as under USE_CUDART.  srssQuirk as
+  useHipOpTable below: true (the default) selects the configured USE_AVX2
+  lane drop of srss / sVarinceDelta_avx, so TNNHip.variances /
+  meansAndVarsDelta reproduce the CPU build's batch-norm statistics. }
+procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean = true);
 
 { Bind the host-pointer op-table drop-ins (boundary A) after
   TTensorOps.initSingle, as USE_OPENBLAS / USE_MKL do (ntensors.pas:
@@ -458,11 +468,13 @@ begin
 end;
 
 procedure TNNHip<T>.gemmBatched(const transA, transB: boolean; const M, N, K: SizeInt; const ALPHA: T; const A: PCUMem; const aOffset: SizeInt; const lda: SizeInt; const B: PCUMem; const bOffset: SizeInt; const ldb: SizeInt; const BETA: T; const C: PCUMem; const cOffset: SizeInt; const ldc: SizeInt; const batchCount: SizeInt);
-var i: SizeInt;
 begin
-  { host arrays of device pointers: one stream-ordered GEMM per entry }
-  for i := 0 to batchCount - 1 do
-    gemm(transA, transB, M, N, K, ALPHA, A[i], aOffset, lda, B[i], bOffset, ldb, BETA, C[i], cOffset, ldc)
+  { A, B, C: arrays of device pointers, device-resident as the reference
+    builds them with writeBuffer (nConvolutionLayer.pas:1083-1085) for
+    cublasSgemmBatched_64 (nncuda.pas:752); the library reads them in stream
+    order }
+  check(tns_hip_gemm_batched(FCtx, transA, transB, M, N, K, s(ALPHA), PHipMem(A), aOffset, lda,
+    PHipMem(B), bOffset, ldb, s(BETA), PHipMem(C), cOffset, ldc, batchCount))
 end;
 
 procedure TNNHip<T>.gemmStridedBatched(const transA, transB: boolean; const M, N, K: SizeInt; const ALPHA: T; A: TCUMem; const aOffset: SizeInt; const lda: SizeInt; const strideA: SizeInt; B: TCUMem; const bOffset: SizeInt; const ldb: SizeInt; const strideB: SizeInt; const BETA: T; C: TCUMem; const cOffset: SizeInt; const ldc: SizeInt; const strideC: SizeInt; const batchCount: SizeInt);
@@ -579,12 +591,17 @@ end;
 
 procedure TNNHip<T>.means(const srcSize, dstSize, groups: SizeInt; const src: TCUMem; const offset: SizeInt; means: TCUMem);
 begin
-  raise ENotSupportedException.Create('TNNHip.means: use meansAndVars (MeansAndVars computes both, ntensors.pas:9102)')
+  { batchNormGPU (nbaselayer.pas:583), TConnectedLayer.forwardGPU
+    (nconnectedlayer.pas:664): MeansAndVars' mean (vssum_avx2 lanes) }
+  check(tns_hip_means(FCtx, srcSize, dstSize, groups, THipMem(src), offset, THipMem(means)))
 end;
 
 procedure TNNHip<T>.variances(const srcSize, dstSize, groups: SizeInt; const src: TCUMem; const offset: SizeInt; means, vars: TCUMem);
 begin
-  raise ENotSupportedException.Create('TNNHip.variances: use meansAndVars (MeansAndVars computes both, ntensors.pas:9102)')
+  { batchNormGPU (nbaselayer.pas:584): the unbiased variance about the given
+    means in MeansAndVars' srss order (TNS_OPT_SRSS_QUIRK as set by initHIP) }
+  check(tns_hip_variances(FCtx, srcSize, dstSize, groups, THipMem(src), offset, THipMem(means),
+    THipMem(vars)))
 end;
 
 procedure TNNHip<T>.normalize(const srcSize, dstSize, groups: SizeInt; means: TCUMem; const meansStride: SizeInt; vars: TCUMem; const varsStride: SizeInt; dst: TCUMem; const dstOffset: SizeInt);
@@ -707,8 +724,12 @@ end;
 
 { ---- process-wide setup ---------------------------------------------------- }
 
-procedure initHIP(const deviceIndex: SizeInt);
+procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean);
 begin
+  if srssQuirk then
+    tns_set_option(TNS_OPT_SRSS_QUIRK, 1)
+  else
+    tns_set_option(TNS_OPT_SRSS_QUIRK, 0);
   if not assigned(hip) then
     hip := TNNHip<single>.Create(deviceIndex)
 end;

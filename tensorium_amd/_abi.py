@@ -185,6 +185,10 @@ PROTOTYPES.update({
     "tns_set_op_devices": (C.c_int, [C.POINTER(i32), i32]),
     "tns_hip_yolo_forward": (C.c_int, [vp, i64, i64, i64, i64, fptr, fptr]),
     "tns_hip_means_and_vars": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, fptr]),
+    "tns_hip_means": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr]),
+    "tns_hip_variances": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, fptr]),
+    "tns_hip_gemm_batched": (C.c_int, [vp, u8, u8, i64, i64, i64, f32, vp, i64, i64, vp, i64, i64,
+                                       f32, vp, i64, i64, i64]),
     "tns_hip_normalize": (C.c_int, [vp, i64, i64, i64, fptr, i64, fptr, i64, fptr, i64]),
     "tns_hip_forward_scale": (C.c_int, [vp, i64, fptr, i64, i64, fptr, i64, i64]),
     "tns_hip_forward_scale_add": (C.c_int, [vp, i64, fptr, i64, i64, fptr, fptr, i64, i64]),

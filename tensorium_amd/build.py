@@ -69,6 +69,8 @@ def build_hip(verbose: bool = False, force: bool = False, out: Path | None = Non
         if force or _newer(obj, [src, *headers]):
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
             extra = os.environ.get("TNS_EXTRA_CFLAGS", "").split()  # A/B side builds
+            if os.environ.get("TNS_DIAG") == "1":   # + the measured, not picked forms
+                extra.append("-DTNS_DIAG_KERNELS")
             jobs.append([HIPCC, *CXXFLAGS, *extra, *lang, "-c", str(src), "-o", str(obj)])
     if jobs:
         with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:

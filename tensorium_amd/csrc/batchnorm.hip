@@ -65,16 +65,26 @@ __device__ __forceinline__ float srss8(const float* a, int64_t n, float mean, in
   return (x0 + (acc[1] + acc[5])) + ((acc[2] + acc[6]) + (acc[3] + acc[7]));
 }
 
-// one thread per channel (FC layers: blockSize 1, groups = batch)
+// one thread per channel (FC layers: blockSize 1, groups = batch).  what:
+// MV_MEAN and / or MV_VAR; the variance alone (TNNCuda.variances) reads the
+// caller's means
+enum { MV_MEAN = 1, MV_VAR = 2 };
 __global__ void means_vars_seq(const float* __restrict__ x, int64_t groups, int64_t N, int64_t bs,
-                               float* __restrict__ means, float* __restrict__ vars, int quirk) {
+                               float* __restrict__ means, float* __restrict__ vars, int quirk,
+                               int what) {
   const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (i >= N) return;
   const float S = (float)(groups * bs), S2 = (float)(groups * bs - 1);
-  float m = 0.0f;
-  for (int64_t b = 0; b < groups; ++b) m = m + vssum8(x + (i + b * N) * bs, bs);
-  m = m / S;
-  means[i] = m;
+  float m;
+  if (what & MV_MEAN) {
+    m = 0.0f;
+    for (int64_t b = 0; b < groups; ++b) m = m + vssum8(x + (i + b * N) * bs, bs);
+    m = m / S;
+    means[i] = m;
+  } else {
+    m = means[i];
+  }
+  if (!(what & MV_VAR)) return;
   float v = 0.0f;
   for (int64_t b = 0; b < groups; ++b) v = v + srss8(x + (i + b * N) * bs, bs, m, quirk);
   vars[i] = v / S2;
@@ -929,20 +939,23 @@ namespace {
 }  // namespace
 
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
-                             float* vars, int quirk, float* part, hipStream_t s) {
+                             float* vars, int quirk, float* part, hipStream_t s, int what) {
   if (N <= 0) return hipSuccess;
   // one thread per channel for FC shapes (blockSize 1) and short blocks;
   // longer blocks: the lane chains per block, then the group-order sums
   // (the variance pass needs the finished means)
   if (!use_chains(bs, part)) {
     hipLaunchKernelGGL(means_vars_seq, dim3(nblk(N)), dim3(TPB), 0, s, x, groups, N, bs, means,
-                       vars, quirk);
+                       vars, quirk, what);
     return hipGetLastError();
   }
   hipError_t e;
-  if ((e = run_chains<CH_SUM>(x, nullptr, nullptr, groups, N, bs, 0, part, nullptr, s)) ||
-      (e = run_finish<FIN_MEAN>(part, nullptr, groups, N, bs, nullptr, means, nullptr, s)) ||
-      (e = run_chains<CH_SRSS>(x, nullptr, means, groups, N, bs, quirk, part, nullptr, s)))
+  if (what & MV_MEAN)
+    if ((e = run_chains<CH_SUM>(x, nullptr, nullptr, groups, N, bs, 0, part, nullptr, s)) ||
+        (e = run_finish<FIN_MEAN>(part, nullptr, groups, N, bs, nullptr, means, nullptr, s)))
+      return e;
+  if (!(what & MV_VAR)) return hipSuccess;
+  if ((e = run_chains<CH_SRSS>(x, nullptr, means, groups, N, bs, quirk, part, nullptr, s)))
     return e;
   return run_finish<FIN_VAR>(part, nullptr, groups, N, bs, nullptr, vars, nullptr, s);
 }

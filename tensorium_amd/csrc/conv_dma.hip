@@ -30,6 +30,11 @@
 #include "tns_internal.hpp"
 
 namespace tns {
+// Measured and not picked (profiles/): compiled only into the
+// diagnostics build (TNS_DIAG=1 python -m tensorium_amd.build); the default
+// library reports no forms of this family.
+#ifdef TNS_DIAG_KERNELS
+
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -324,5 +329,12 @@ hipError_t launch_conv_dma(int v, const GemmArgs& a, int ks, int dil, hipStream_
   if (v < 0 || v >= kNumTiles) return hipErrorInvalidValue;
   return kTiles[v].fn(a, ks, dil, s);
 }
+
+#else
+int conv_dma_count() { return 0; }
+const char* conv_dma_name(int) { return ""; }
+int conv_dma_pick(const GemmArgs&, int) { return -1; }
+hipError_t launch_conv_dma(int, const GemmArgs&, int, int, hipStream_t) { return hipErrorInvalidValue; }
+#endif  // TNS_DIAG_KERNELS
 
 }  // namespace tns

@@ -23,6 +23,11 @@
 #include "tns_internal.hpp"
 
 namespace tns {
+// Measured and not picked (profiles/): compiled only into the
+// diagnostics build (TNS_DIAG=1 python -m tensorium_amd.build); the default
+// library reports no forms of this family.
+#ifdef TNS_DIAG_KERNELS
+
 namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -275,5 +280,12 @@ hipError_t launch_conv_patch(int v, const GemmArgs& a, hipStream_t s) {
   if (v < 0 || v >= kNumTiles) return hipErrorInvalidValue;
   return kTiles[v].fn(a, s);
 }
+
+#else
+int conv_patch_count() { return 0; }
+const char* conv_patch_name(int) { return ""; }
+int conv_patch_pick(const GemmArgs&) { return -1; }
+hipError_t launch_conv_patch(int, const GemmArgs&, hipStream_t) { return hipErrorInvalidValue; }
+#endif  // TNS_DIAG_KERNELS
 
 }  // namespace tns

@@ -629,6 +629,7 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
     TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
     TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
+#ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
     TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 25 (3, BD)
@@ -638,6 +639,7 @@ const TileInfo4 kTiles4[] = {
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
     TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 28 (3)
+#endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
 #define TNS_CT4T(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                      \

@@ -325,13 +325,18 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 // registers at the 512 cap — not instantiated)
 // (form 5 is the ping-pong schedule of the 256x256 tile, sgemm_nn_pp.hip;
 // form 6 the same with B register-staged into k-permuted slots)
+// (form 6 is compiled into the diagnostics build only: measured, not picked)
+#ifdef TNS_DIAG_KERNELS
 int sgemm_nn_big_count() { return 7; }
+#else
+int sgemm_nn_big_count() { return 6; }
+#endif
 const char* sgemm_nn_big_name(int v) {
   static const char* names[] = {"256x256x32_w2x4_nn_big", "128x128x32_w2x2_nn_big",
                                 "256x128x32_w2x2_nn_big", "256x256x32_w4x4_nn_big",
                                 "256x128x16_w2x2_b2_nn_big", "256x256x32_w2x4_pp_nn_big",
                                 "256x256x32_w2x4_ppbq_nn_big"};
-  return v >= 0 && v < 7 ? names[v] : "";
+  return v >= 0 && v < sgemm_nn_big_count() ? names[v] : "";
 }
 
 // heuristic: the 256x256 tile when it gives about a block per CU, on the
@@ -351,7 +356,9 @@ hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s) {
     case 3: return launch<G256w16>(a, s);
     case 4: return launch<G256x128k16>(a, s);
     case 5: return launch_sgemm_nn_pp(a, s);
+#ifdef TNS_DIAG_KERNELS
     case 6: return launch_sgemm_nn_pp(a, s, true);  // k-permuted B slots
+#endif
     default: return hipErrorInvalidValue;
   }
 }

@@ -357,10 +357,14 @@ hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s, bool bperm) {
     sub.B = a.B + b0 * a.strideB;
     sub.C = a.C + b0 * a.strideC;
     sub.batch = nb;
+#ifdef TNS_DIAG_KERNELS  // (the k-permuted B form: diagnostics build only)
     if (bperm)
       hipLaunchKernelGGL(sgemm_nn_pp_kernel<true>, dim3((unsigned)tiles, (unsigned)nb), dim3(NT), 0,
                          s, sub);
     else
+#else
+    if (bperm) return hipErrorInvalidValue;
+#endif
       hipLaunchKernelGGL(sgemm_nn_pp_kernel<false>, dim3((unsigned)tiles, (unsigned)nb), dim3(NT),
                          0, s, sub);
     hipError_t e = hipGetLastError();

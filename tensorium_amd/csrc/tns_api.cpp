@@ -113,6 +113,29 @@ int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   return TNS_OK;
 }
 
+// the conv backward's side stream and its fork / join events, created
+// together on the context's device; false (nothing kept) if any of them
+// cannot be created, and the caller runs its sequential schedule
+bool ensure_side_stream(tns_ctx* c) {
+  if (c->aux_stream && c->ev_fork && c->ev_join) return true;
+  int prev = -1;
+  hipGetDevice(&prev);
+  bool ok = hipSetDevice(c->device) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    if (c->ev_fork) hipEventDestroy(c->ev_fork);
+    if (c->ev_join) hipEventDestroy(c->ev_join);
+    c->aux_stream = nullptr;
+    c->ev_fork = c->ev_join = nullptr;
+    hipGetLastError();
+  }
+  if (prev >= 0) hipSetDevice(prev);
+  return ok;
+}
+
 struct OpTimer {
   tns_ctx* c;
   int op;
@@ -687,6 +710,53 @@ int tns_hip_gemm_strided_batched(tns_ctx* c, uint8_t transA, uint8_t transB, int
                  C ? C + cOffset : nullptr, ldc, strideC, batchCount, EPI_NONE, nullptr, 0);
 }
 
+int tns_hip_gemm_batched(tns_ctx* c, uint8_t transA, uint8_t transB, int64_t M, int64_t N,
+                         int64_t K, float ALPHA, const float* const* A, int64_t aOffset,
+                         int64_t lda, const float* const* B, int64_t bOffset, int64_t ldb,
+                         float BETA, float* const* C, int64_t cOffset, int64_t ldc,
+                         int64_t batchCount) {
+  if (int r = check_ctx(c)) return r;
+  if (batchCount < 0) return set_error(TNS_ERR_ARG, "gemmBatched: batchCount < 0");
+  if (batchCount == 0) return TNS_OK;
+  if (!A || !B || !C) return set_error(TNS_ERR_ARG, "gemmBatched: null pointer array");
+  // The pointer arrays are read where they live (hipMemcpyDefault: device
+  // arrays written by writeBuffer as nConvolutionLayer.pas:1083-1085 builds
+  // them, or host arrays), in stream order after the work that wrote them.
+  const size_t bytes = (size_t)batchCount * sizeof(void*);
+  std::vector<const float*> pa(batchCount), pb(batchCount);
+  std::vector<float*> pc(batchCount);
+  TNS_HIP_TRY(hipSetDevice(c->device));
+  TNS_HIP_TRY(hipMemcpyAsync(pa.data(), A, bytes, hipMemcpyDefault, c->stream));
+  TNS_HIP_TRY(hipMemcpyAsync(pb.data(), B, bytes, hipMemcpyDefault, c->stream));
+  TNS_HIP_TRY(hipMemcpyAsync(pc.data(), C, bytes, hipMemcpyDefault, c->stream));
+  TNS_HIP_TRY(hipStreamSynchronize(c->stream));
+  for (int64_t i = 0; i < batchCount; ++i)
+    if (!pa[i] || !pb[i] || !pc[i])
+      return set_error(TNS_ERR_ARG, "gemmBatched: null matrix pointer at entry %lld", (long long)i);
+  // equally spaced entries (the common case: slices of one buffer) run as one
+  // strided-batched launch; anything else GEMM by GEMM in array order
+  auto stride_of = [&](auto& v, int64_t* st) {
+    const intptr_t d = batchCount > 1 ? (const char*)v[1] - (const char*)v[0] : 0;
+    if (d < 0 || d % (intptr_t)sizeof(float)) return false;
+    for (int64_t i = 2; i < batchCount; ++i)
+      if ((const char*)v[i] - (const char*)v[i - 1] != d) return false;
+    *st = (int64_t)(d / (intptr_t)sizeof(float));
+    return true;
+  };
+  int64_t sA, sB, sC;
+  if (stride_of(pa, &sA) && stride_of(pb, &sB) && stride_of(pc, &sC) &&
+      (sC > 0 || batchCount == 1))
+    return do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, pa[0] + aOffset, lda, sA,
+                   pb[0] + bOffset, ldb, sB, BETA, pc[0] + cOffset, ldc, sC, batchCount, EPI_NONE,
+                   nullptr, 0);
+  for (int64_t i = 0; i < batchCount; ++i)
+    if (int r = do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, pa[i] + aOffset, lda, 0,
+                        pb[i] + bOffset, ldb, 0, BETA, pc[i] + cOffset, ldc, 0, 1, EPI_NONE,
+                        nullptr, 0))
+      return r;
+  return TNS_OK;
+}
+
 int tns_hip_im2col_strided_batched(tns_ctx* c, int64_t aChannels, int64_t aHeight,
                                    int64_t aWidth, int64_t kernelHeight, int64_t kernelWidth,
                                    int64_t padHeight, int64_t padWidth, int64_t strideY,
@@ -991,6 +1061,33 @@ int tns_hip_means_and_vars(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t
   return hip_status(launch_means_vars(src + offset, groups, dstSize, bs, means, vars,
                                       (int)g_srss_quirk, part, c->stream),
                     "meansAndVars");
+}
+
+int tns_hip_means(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
+                  const float* src, int64_t offset, float* means) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(srcSize, dstSize, groups, &bs, "means")) return r;
+  if (!src || !means) return set_error(TNS_ERR_ARG, "means: null pointer");
+  float* part;
+  if (int r = ensure_scratch(c, SLOT_BN, 2 * groups * dstSize, &part)) return r;
+  return hip_status(launch_means_vars(src + offset, groups, dstSize, bs, means, nullptr,
+                                      (int)g_srss_quirk, part, c->stream, 1),
+                    "means");
+}
+
+int tns_hip_variances(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
+                      const float* src, int64_t offset, const float* means, float* vars) {
+  if (int r = check_ctx(c)) return r;
+  int64_t bs;
+  if (int r = blocks_of(srcSize, dstSize, groups, &bs, "variances")) return r;
+  if (!src || !means || !vars) return set_error(TNS_ERR_ARG, "variances: null pointer");
+  float* part;
+  if (int r = ensure_scratch(c, SLOT_BN, 2 * groups * dstSize, &part)) return r;
+  return hip_status(launch_means_vars(src + offset, groups, dstSize, bs,
+                                      const_cast<float*>(means), vars, (int)g_srss_quirk, part,
+                                      c->stream, 2),
+                    "variances");
 }
 
 int tns_hip_normalize(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
@@ -1562,14 +1659,25 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // side stream (fork / join events), each with its own col buffer —
   // nothing changes in either result.  Telemetry times ops one by one, so it
   // keeps them in sequence.
-  const bool overlap = state_delta && g_bwd_overlap && !c->telemetry;
+  bool overlap = state_delta && g_bwd_overlap && !c->telemetry && ensure_side_stream(c);
   const bool dw_col = needs_col && dwv < 0;  // dW reads an im2col matrix
+  // state.delta's own col buffer when both chains need one at once (the
+  // overlap's extra memory, tns.h); if it cannot be had, the sequential
+  // schedule shares the one col buffer instead
+  float* dx_ws = nullptr;
+  if (overlap && dw_col && !fused_dx && ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) {
+    tns_clear_error();
+    overlap = false;
+  }
   float* ws = workspace;
   if (!ws && (dw_col || (state_delta && !fused_dx && !(overlap && dw_col))))
     if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws)) return r;
-  float* dx_ws = ws;  // col buffer of state.delta's chain
-  if (overlap && dw_col && !fused_dx)
-    if (int r = ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) return r;
+  if (!dx_ws) dx_ws = ws;  // col buffer of state.delta's chain
+  // scratch of the fused state.delta kernel, sized before any fork (a growth
+  // inside the side-stream chain would free a buffer the main stream may use)
+  float* wt = nullptr;
+  if (fused_dx)
+    if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
 
   auto run_dw = [&]() -> int {
     const float* col = input;
@@ -1631,8 +1739,6 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
       // per image pixel: each window tap's ascending-f chain, added to the
       // pixel in (kr, kc) order for the taps scol2im does not skip — the same
       // roundings as the two stages below (646-660)
-      float* wt = nullptr;
-      if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
       OpTimer t(c, TNS_OP_GEMM);
       return hip_status(launch_conv_dx_col2im(weights, wt, delta, state_delta, batch, C, H, W,
                                               filters, kSize, padding, dilation, g.oh, g.ow,
@@ -1671,11 +1777,6 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   if (!overlap) {
     if (int r = run_dw()) return r;
     return state_delta ? run_dx() : TNS_OK;
-  }
-  if (!c->aux_stream) {
-    TNS_HIP_TRY(hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking));
-    TNS_HIP_TRY(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming));
-    TNS_HIP_TRY(hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming));
   }
   TNS_HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
   TNS_HIP_TRY(hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));

@@ -264,8 +264,10 @@ hipError_t launch_clamp(int64_t n, float alpha, const float* src, float* dst, in
 // part: device scratch of >= 2*groups*N floats for per-block results (conv
 // blocks, bs >= 64, take the lane-chain kernels with it); nullptr = the
 // one-thread-per-channel kernels only
+// what: 1 the means, 2 the variances about the given means (TNNCuda.means /
+// .variances, nncuda.pas:1330-1369), 3 both (meansAndVars)
 hipError_t launch_means_vars(const float* x, int64_t groups, int64_t N, int64_t bs, float* means,
-                             float* vars, int quirk, float* part, hipStream_t s);
+                             float* vars, int quirk, float* part, hipStream_t s, int what = 3);
 hipError_t launch_normalize(float* x, int64_t groups, int64_t N, int64_t bs, const float* means,
                             int64_t mstride, const float* vars, int64_t vstride, hipStream_t s);
 hipError_t launch_scale_add(float* x, int64_t groups, int64_t N, int64_t bs, const float* scales,

@@ -95,6 +95,21 @@ class TNNHip:
             aOffset, lda, strideA, _ptr(B), bOffset, ldb, strideB, float(BETA), _ptr(C_), cOffset,
             ldc, strideC, batchCount))
 
+    def gemmBatched(self, transA, transB, M, N, K, ALPHA, A, aOffset, lda, B, bOffset, ldb,
+                    BETA, C_, cOffset, ldc, batchCount):
+        """TNNCuda.gemmBatched (nncuda.pas:727): A, B, C are arrays of matrix
+        pointers — device buffers holding them (int64 tensors, as the
+        reference's writeBuffer-built arrays) or raw addresses."""
+        def arr(x):
+            if torch is not None and isinstance(x, torch.Tensor):
+                if x.dtype != torch.int64 or not x.is_contiguous():
+                    raise TnsError("gemmBatched pointer arrays are contiguous int64 tensors")
+                return x.data_ptr()
+            return int(x)
+        check(self.lib.tns_hip_gemm_batched(
+            self.ctx, int(bool(transA)), int(bool(transB)), M, N, K, float(ALPHA), arr(A),
+            aOffset, lda, arr(B), bOffset, ldb, float(BETA), arr(C_), cOffset, ldc, batchCount))
+
     def gemmVariant(self, variant, transA, transB, M, N, K, ALPHA, A, aOffset, lda, strideA, B,
                     bOffset, ldb, strideB, BETA, C_, cOffset, ldc, strideC, batchCount=1):
         """Force one SGEMM tile shape (tuning sweeps); variant < 0 = heuristic."""
@@ -365,6 +380,17 @@ class TNNHip:
         check(self.lib.tns_hip_means_and_vars(self.ctx, srcSize, dstSize, groups, _ptr(src),
                                               offset, _ptr(means), _ptr(vars_)))
 
+    def means(self, srcSize, dstSize, groups, src, offset, means):
+        """TNNCuda.means (nncuda.pas:1330): the first half of meansAndVars."""
+        check(self.lib.tns_hip_means(self.ctx, srcSize, dstSize, groups, _ptr(src), offset,
+                                     _ptr(means)))
+
+    def variances(self, srcSize, dstSize, groups, src, offset, means, vars_):
+        """TNNCuda.variances (nncuda.pas:1350): the unbiased variance about the
+        given means, in MeansAndVars' srss order."""
+        check(self.lib.tns_hip_variances(self.ctx, srcSize, dstSize, groups, _ptr(src), offset,
+                                         _ptr(means), _ptr(vars_)))
+
     def normalize(self, srcSize, dstSize, groups, means, meansStride, vars_, varsStride, dst,
                   dstOffset):
         check(self.lib.tns_hip_normalize(self.ctx, srcSize, dstSize, groups, _ptr(means),
@@ -421,3 +447,21 @@ class TNNHip:
                                               batch, _ptr(X), _ptr(truth), float(lr),
                                               float(momentum), float(decay), _ptr(buf),
                                               _ptr(cost)))
+
+
+def initHIP(deviceIndex: int = 0, srssQuirk: bool = True) -> TNNHip:
+    """initHIP twin of pascal/nnHip.pas (initCUDART, ntensors.pas:6191-6210):
+    one backend context for the process, with the reference's configured
+    USE_AVX2 BN lane order selected (TNS_OPT_SRSS_QUIRK = 1: srss /
+    sVarinceDelta_avx drop lanes 4..7 of blocks a multiple of 8 long,
+    ntensors.pas:1509-1511, 8739-8741), so a forwardGPU / backwardGPU caller
+    reproduces the CPU build's statistics by default."""
+    global hip
+    lib = load()
+    check(lib.tns_set_option(4, 1 if srssQuirk else 0))
+    if hip is None:
+        hip = TNNHip(deviceIndex)
+    return hip
+
+
+hip: TNNHip | None = None

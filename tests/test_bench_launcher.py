@@ -50,3 +50,32 @@ def test_failing_rank_stops_the_launch():
     assert r.returncode == 3, (r.returncode, r.stderr)
     assert "rank 1 exited with 3" in r.stderr
     assert "{" not in r.stdout
+
+
+def test_profiler_preload_detection():
+    sys.path.insert(0, str(ROOT))
+    import bench
+    assert bench.profiler_preloaded({"LD_PRELOAD": "/opt/rocm/lib/librocprofiler-sdk-tool.so"})
+    assert not bench.profiler_preloaded({"LD_PRELOAD": "/usr/lib/libfoo.so"})
+    assert not bench.profiler_preloaded({})
+
+
+def test_sigterm_to_launcher_stops_the_ranks(tmp_path):
+    """A timeout (SIGTERM) of the launcher must not leave ranks behind."""
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["TNS_DRYRUN_HANG_DIR"] = str(tmp_path)
+    p = subprocess.Popen([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--dry-run"],
+                         env=env)
+    deadline = time.time() + 120
+    while time.time() < deadline and len(list(tmp_path.glob("rank*"))) < 2:
+        time.sleep(0.2)
+    pids = [int(f.read_text()) for f in tmp_path.glob("rank*")]
+    assert len(pids) == 2
+    p.send_signal(signal.SIGTERM)
+    assert p.wait(timeout=60) != 0
+    for pid in pids:   # each rank was terminated and reaped by the launcher
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)

@@ -277,6 +277,55 @@ def test_strided_batched_shared_a(hip, torch_cuda, ora):
     assert np.array_equal(dC.cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False)])
+@pytest.mark.parametrize("layout", ["strided", "irregular", "host"])
+def test_gemm_batched_pointer_arrays(hip, torch_cuda, ora, ta, tb, layout):
+    """TNNCuda.gemmBatched (nncuda.pas:727-760): arrays of matrix pointers
+    written to the device with writeBuffer, as nConvolutionLayer.pas:1083-1085
+    builds them (shared weights: every A entry the same), equally spaced
+    (one strided launch), irregular (GEMM by GEMM), or host-resident."""
+    T = torch_cuda
+    batch, M, N, K = 5, 48, 70, 37
+    rng = np.random.default_rng(7)
+    A = rng.uniform(-1, 1, (M * K,)).astype(np.float32)
+    Bs = [rng.uniform(-1, 1, (K * N,)).astype(np.float32) for _ in range(batch)]
+    C0 = [rng.uniform(-1, 1, (M * N,)).astype(np.float32) for _ in range(batch)]
+    off = 3
+    dA = T.from_numpy(np.concatenate([np.zeros(off, np.float32), A])).cuda()
+    if layout == "irregular":   # separate allocations, unequal gaps
+        dB = [T.from_numpy(np.concatenate([np.zeros(off, np.float32), b])).cuda() for b in Bs]
+        dC = [T.from_numpy(np.concatenate([np.zeros(off, np.float32), c])).cuda() for c in C0]
+        pb = [t.data_ptr() for t in dB]
+        pc = [t.data_ptr() for t in dC]
+    else:
+        bigB = T.from_numpy(np.concatenate([np.zeros(off, np.float32), *Bs])).cuda()
+        bigC = T.from_numpy(np.concatenate([np.zeros(off, np.float32), *C0])).cuda()
+        pb = [bigB.data_ptr() + 4 * i * K * N for i in range(batch)]
+        pc = [bigC.data_ptr() + 4 * i * M * N for i in range(batch)]
+    pa = [dA.data_ptr()] * batch
+    lda, ldb = (M if ta else K), (K if tb else N)
+    if layout == "host":
+        arrs = [np.array(p, np.int64) for p in (pa, pb, pc)]
+        args = [a.ctypes.data for a in arrs]
+    else:
+        args = [T.zeros(batch, dtype=T.int64, device="cuda") for _ in range(3)]
+        for d, p in zip(args, (pa, pb, pc)):   # writeBuffer of the pointer arrays
+            host = np.array(p, np.int64)
+            hip.lib.tns_hip_write_buffer(hip.ctx, d.data_ptr(), host.nbytes, host.ctypes.data)
+    hip.gemmBatched(ta, tb, M, N, K, 1.0, args[0], off, lda, args[1], off, ldb, 0.5, args[2], off,
+                    N, batch)
+    hip.finish()
+    if layout == "irregular":
+        got = [t.cpu().numpy()[off:] for t in dC]
+    else:
+        g = bigC.cpu().numpy()[off:]
+        got = [g[i * M * N:(i + 1) * M * N] for i in range(batch)]
+    for i in range(batch):
+        ref = C0[i].copy()
+        ora.sgemm(ta, tb, M, N, K, 1.0, A, lda, Bs[i], ldb, 0.5, ref, N)
+        assert np.array_equal(got[i], ref), i
+
+
 def test_beta0_strict_propagates_nan(hip, torch_cuda, hiplib):
     A = np.ones((4, 4), np.float32)
     C = np.zeros((4, 4), np.float32)

@@ -62,6 +62,111 @@ def test_means_vars_srss_quirk(hip, torch_cuda, ora, groups, N, bs):
         assert np.array_equal(dm.cpu().numpy(), m) and np.array_equal(dv.cpu().numpy(), v)
 
 
+BN_REPLAY = [(32, 64, 1), (32, 10, 1), (3, 5, 24), (2, 7, 65), (8, 32, 173056), (8, 64, 43264),
+             (8, 256, 2704), (8, 1024, 169)]
+
+
+@pytest.mark.parametrize("quirk", [0, 1])
+@pytest.mark.parametrize("groups,N,bs", BN_REPLAY)
+def test_batchnorm_gpu_call_sequence(hip, torch_cuda, ora, groups, N, bs, quirk):
+    """The reference's BN forward on the GPU, call for call: batchNormGPU
+    (nbaselayer.pas:583-643; blocks > 1, conv layers) and TConnectedLayer.
+    forwardGPU (nconnectedlayer.pas:664-714; blockSize 1, forwardScaleAdd) —
+    means, variances, scale/axpy rolling updates, copy to x, normalize, copy
+    to x_norm, scale + bias — through TNNHip at state.step = 1 (element
+    offset = outputStep), bit-exact against the CPU batchNorm restated
+    (ora_batch_norm, nbaselayer.pas:336-370) in both srss lane modes."""
+    T = torch_cuda
+    n = groups * N * bs
+    fc = bs == 1
+    mom = np.float32(0.05 if fc else 0.1)
+    y = ora.uniform(n, 61, N, -2.0, 3.0)
+    sc = ora.uniform(N, 62, N, 0.5, 1.5)
+    bi = ora.uniform(N, 63, N, -0.2, 0.2)
+    rm = ora.uniform(N, 64, N, -0.5, 0.5)
+    rv = ora.uniform(N, 65, N, 0.5, 1.5)
+    ref, rm_ref, rv_ref = y.copy(), rm.copy(), rv.copy()
+    m, v, xr, xnr = ora.batch_norm(ref, groups, N, bs, sc, bi, rm_ref, rv_ref, mom, True, quirk)
+
+    off = n  # state.step = 1
+    out = T.zeros(2 * n, device="cuda")
+    out[off:] = dev(T, y)
+    x, xn = T.zeros(2 * n, device="cuda"), T.zeros(2 * n, device="cuda")
+    mean, var = T.zeros(N, device="cuda"), T.zeros(N, device="cuda")
+    drm, drv, dsc, dbi = dev(T, rm), dev(T, rv), dev(T, sc), dev(T, bi)
+    keep = float(np.float32(1) - mom)
+    hip.setSrssQuirk(bool(quirk))
+    try:
+        hip.means(n, N, groups, out, off, mean)
+        hip.variances(n, N, groups, out, off, mean, var)
+        hip.scale(N, keep, drm, 1)
+        hip.axpy(N, float(mom), mean, 0, 1, drm, 0, 1)
+        hip.scale(N, keep, drv, 1)
+        hip.axpy(N, float(mom), var, 0, 1, drv, 0, 1)
+        hip.copy(n, out, off, 1, x, off, 1)
+        hip.normalize(N, n, groups, mean, 1, var, 1, out, off)
+        hip.copy(n, out, off, 1, xn, off, 1)
+        if fc:
+            hip.forwardScaleAdd(n, out, off, N, dsc, dbi, 1, groups)
+        else:
+            hip.forwardScale(n, out, off, N, dsc, 1, groups)
+            hip.forwardBias(n, out, off, N, dbi, 1, groups)
+        hip.finish()
+    finally:
+        hip.setSrssQuirk(False)
+    assert np.array_equal(mean.cpu().numpy(), m), "mean"
+    assert np.array_equal(var.cpu().numpy(), v), "variance"
+    assert np.array_equal(drm.cpu().numpy(), rm_ref), "rolling_mean"
+    assert np.array_equal(drv.cpu().numpy(), rv_ref), "rolling_variance"
+    assert np.array_equal(x.cpu().numpy()[off:], xr), "x"
+    assert np.array_equal(xn.cpu().numpy()[off:], xnr), "x_norm"
+    assert np.array_equal(out.cpu().numpy()[off:], ref), "output"
+    assert not out[:off].any(), "wrote outside the step's slice"
+
+
+def test_variances_read_the_given_means(hip, torch_cuda, ora):
+    """TNNCuda.variances takes the means as an input: the srss lanes run
+    about whatever the caller passes (here the means of another tensor)."""
+    T = torch_cuda
+    groups, N, bs = 4, 6, 4099
+    x = ora.uniform(groups * N * bs, 66, N, -2.0, 3.0)
+    other = ora.uniform(groups * N * bs, 67, N, 0.0, 1.0)
+    mu, _ = ora.means_and_vars(other, groups, N, bs)
+    # oracle: MeansAndVars' variance pass with mu substituted (srss per block)
+    v = np.zeros(N, np.float32)
+    for i in range(N):
+        acc = np.float32(0)
+        for g in range(groups):
+            blk = x[(g * N + i) * bs:(g * N + i + 1) * bs]
+            acc = np.float32(acc + np.float32(ora.srss(mu[i], blk)))
+        v[i] = np.float32(acc / np.float32(groups * bs - 1))
+    dv = T.zeros(N, device="cuda")
+    hip.variances(x.size, N, groups, dev(T, x), 0, dev(T, mu), dv)
+    hip.finish()
+    assert np.array_equal(dv.cpu().numpy(), v)
+
+
+def test_init_hip_selects_the_reference_lane_drop(hiplib, torch_cuda, ora):
+    """initHIP (pascal/nnHip.pas; Python twin tensorium_amd.nnhip.initHIP)
+    selects TNS_OPT_SRSS_QUIRK = 1, so a Boundary-B caller gets the configured
+    USE_AVX2 reference's variances on tail-less blocks without asking."""
+    from tensorium_amd import nnhip
+    T = torch_cuda
+    groups, N, bs = 8, 4, 2704   # 52^2 blocks: a multiple of 8
+    x = ora.uniform(groups * N * bs, 68, N, -2.0, 3.0)
+    m1, v1 = ora.means_and_vars(x, groups, N, bs, quirk=1)
+    h = nnhip.initHIP(0)
+    try:
+        dm, dv = T.zeros(N, device="cuda"), T.zeros(N, device="cuda")
+        dx = dev(T, x)
+        h.means(x.size, N, groups, dx, 0, dm)
+        h.variances(x.size, N, groups, dx, 0, dm, dv)
+        h.finish()
+        assert np.array_equal(dm.cpu().numpy(), m1) and np.array_equal(dv.cpu().numpy(), v1)
+    finally:
+        h.setSrssQuirk(False)
+
+
 BN_BWD = [(32, 64, 1), (4, 8, 9), (8, 16, 2704), (300, 3, 65), (2, 5, 1029), (3, 4, 16),
           (8, 4, 173056), (2, 3, 43264), (8, 6, 169), (5, 2, 64), (2, 3, 20011), (1, 3, 16392)]
 
@@ -258,4 +363,7 @@ def test_bn_null_pointers_are_arg_errors(hip, torch_cuda):
     assert L.tns_hip_normalize_delta(hip.ctx, 64, 4, 2, p, None, 0, p, p, p, p) == 1
     assert L.tns_hip_add_dots(hip.ctx, 64, 4, 2, p, None, 0, p) == 1
     assert L.tns_hip_means_and_vars(hip.ctx, 64, 4, 2, None, 0, p, p) == 1
+    assert L.tns_hip_means(hip.ctx, 64, 4, 2, p, 0, None) == 1
+    assert L.tns_hip_variances(hip.ctx, 64, 4, 2, p, 0, None, p) == 1
+    assert L.tns_hip_variances(hip.ctx, 63, 4, 2, p, 0, p, p) == 1   # sizes do not align
     hip.finish()

@@ -140,7 +140,9 @@ def test_tnnhip_has_tnncuda_method_list():
 
 def test_init_and_op_table_binding():
     src = PAS.read_text()
-    assert re.search(r"procedure initHIP\(const deviceIndex: SizeInt\);", src)
+    assert "procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean = true);" in src
+    body = src[src.index("procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean);"):]
+    assert "tns_set_option(TNS_OPT_SRSS_QUIRK, 1)" in body[:400]   # initHIP applies the drop
     assert "procedure useHipOpTable(const srssQuirk: boolean = true);" in src
     assert "tns_set_option(TNS_OPT_SRSS_QUIRK, 1)" in src
     for slot, fn in [("gemm", "tns_cblas_sgemm"), ("gemmStridedBatched",
@@ -152,7 +154,8 @@ def test_init_and_op_table_binding():
 
 
 @pytest.mark.parametrize("name", ["tns_hip_gemm", "tns_hip_conv_backward_bn",
-                                  "tns_hip_sgemm_strided_batched_multi"])
+                                  "tns_hip_sgemm_strided_batched_multi", "tns_hip_means",
+                                  "tns_hip_variances", "tns_hip_gemm_batched"])
 def test_spot_widths(name):
     decls = parse_pascal_externals()
     protos = parse_header()
