@@ -51,6 +51,26 @@ namespace {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+template <int I, int N, class F>
+__device__ __forceinline__ void cfor(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    cfor<I + 1, N>(f);
+  }
+}
+
+// ds_write_addtid_b32: LDS[M0 + OFF + 4 * lane] = v (M0 saved and restored)
+template <int OFF>
+__device__ __forceinline__ void st_addtid(float v, unsigned m0v) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "ds_write_addtid_b32 %1 offset:%3\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(v), "s"(m0v), "i"(OFF)
+      : "memory");
+}
+
 // one group's fragments of a wave: the A slot and JW B slots (4 steps each)
 template <int JW>
 struct Frag4 {
@@ -59,8 +79,14 @@ struct Frag4 {
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
           int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
-          bool BD_ = false, bool BW_ = false, bool AP_ = false>
+          bool BD_ = false, bool BW_ = false, bool AP_ = false, bool AT_ = false>
 struct Geo4 {
+  // AT: B stored by ds_write_addtid_b32 (address M0 + offset + 4 * lane: no
+  // address VGPR, 2 cycles a store against 4 for ds_write_b32): the gather
+  // lanes are (pixel = lane >> 2, slot component = lane & 3), so a wave's 64
+  // stores of one (slot row, fragment) are 64 consecutive dwords; the two
+  // stages' B images sit below the A images (M0 + offset reach them)
+  static constexpr bool AT = AT_;
   // AP: A read from a pre-permuted copy of the weights (conv_tile4_permute:
   // slot row R = 4g + q of the whole K, then m, then the slot's 4 values), so
   // a tile's slot row is contiguous and arrives by 16-byte LDS-DMA
@@ -107,6 +133,7 @@ struct Geo4 {
   static constexpr int ROWS = BK / 4;           // slot rows per image (4g + q)
   static constexpr int A_TILE = ROWS * BM * 4;  // floats
   static constexpr int STAGE = ROWS * (BM + BN) * 4;
+  static constexpr int B_TILE = ROWS * BN * 4;  // floats
   static constexpr int AU = BM * BK / 4 / NT;   // float4 A units per thread
   static constexpr int KI = BK / 4 / NW;        // B k-slots per thread
   static_assert(BM == 16 * WM, "one 16-row strip per wave");
@@ -119,6 +146,8 @@ struct Geo4 {
   static_assert(2 * STAGE * 4 <= 163840, "LDS");
   static_assert(!BD || (!IL && !ST && !TA), "DMA gather: tile-top issue only");
   static_assert(!(BD && BW), "one gather form");
+  static_assert(!AT || (!BD && !BW && !TA && !AP && !SI && 2 * B_TILE * 4 <= 98304),
+                "addtid B stores: register-staged gather, block-placed stores, B images below 96 KB");
   static_assert(!AP || (!IL && !ST && !TA && BM % 64 == 0 && ROWS * BM % (64 * NW) == 0),
                 "A DMA: tile-top issue, whole 64-slot pieces");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
@@ -133,6 +162,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, NG = G::NG;
   constexpr int A_TILE = G::A_TILE, STAGE = G::STAGE, AU = G::AU, KI = G::KI;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  // stage st: A image and B image (AT: [B0][B1][A0][A1], else [A0 B0][A1 B1])
+  auto a_st = [&](int st) -> float* {
+    return G::AT ? smem + 2 * G::B_TILE + st * A_TILE : smem + st * STAGE;
+  };
+  auto b_st = [&](int st) -> float* {
+    return G::AT ? smem + st * G::B_TILE : smem + st * STAGE + A_TILE;
+  };
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w % G::WM, wn = w / G::WM;
   const int half = __builtin_amdgcn_readfirstlane(w >= G::NW / 2 ? 1 : 0);  // (ST)
@@ -157,7 +193,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   // gather lanes: pixel gp of a 16-column fragment, slot component gq
   // (BD: the DMA writes lane L to float 4 * (L >> 2) + (L & 3) of its row)
   // (BW: lane = pixel of a 64-pixel chunk)
-  const int gp = G::BD ? lane >> 2 : r16, gq = G::BD ? lane & 3 : q;
+  // (AT: the same lane split, for consecutive-dword stores)
+  const int gp = (G::BD || G::AT) ? lane >> 2 : r16, gq = (G::BD || G::AT) ? lane & 3 : q;
   constexpr int NCOL = G::BW ? G::CH : J;
   unsigned vbase[NCOL], tmask[NCOL];
 #pragma unroll
@@ -278,6 +315,22 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
         for (int c = 0; c < G::CH; ++c)
           if (64 * (c + 1) <= BN || 64 * c + lane < BN)
             *reinterpret_cast<floatx4*>(bs + ((wu * KI + ii) * BN + 64 * c + lane) * 4) = rw[ii][c];
+    } else if constexpr (G::AT) {
+#pragma unroll
+      for (int ii = 0; ii < KI; ++ii) {
+        // slot row w*KI + ii: fragment j's 64 dwords at row start + 256 j bytes
+        const unsigned base = lds0 + 4u * (unsigned)((bs - smem) + (wu * KI + ii) * BN * 4);
+        if (base < 65536u - 256u * J)
+          cfor<0, J>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            st_addtid<256 * j>(rb[ii][j], base);
+          });
+        else
+          cfor<0, J>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            st_addtid<32768 + 256 * j>(rb[ii][j], base - 32768u);
+          });
+      }
     } else if constexpr (!G::BD) {  // (BD: landed by the DMA)
 #pragma unroll
       for (int ii = 0; ii < KI; ++ii)
@@ -367,10 +420,10 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
 #pragma unroll
   for (int j = 0; j < JW; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   using Frag = Frag4<JW>;
-  auto frag = [&](const float* st, int g, Frag& f) {
-    const float* ap = st + ((4 * g + q) * BM + wm * 16 + r16) * 4;
+  auto frag = [&](int stg, int g, Frag& f) {
+    const float* ap = a_st(stg) + ((4 * g + q) * BM + wm * 16 + r16) * 4;
     f.a = *reinterpret_cast<const floatx4*>(ap);
-    const float* bp = st + A_TILE + ((4 * g + q) * BN + coff * 16 + r16) * 4;
+    const float* bp = b_st(stg) + ((4 * g + q) * BN + coff * 16 + r16) * 4;
 #pragma unroll
     for (int j = 0; j < JW; ++j) f.b[j] = *reinterpret_cast<const floatx4*>(bp + 64 * j);
   };
@@ -401,27 +454,27 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   const int nt = K / BK;
   Frag f0, f1;
   if (nt > 0) {
-    load_a(0, smem);
-    gather_b(smem + A_TILE);
-    store_a(smem);
-    store_b(smem + A_TILE);
+    load_a(0, a_st(0));
+    gather_b(b_st(0));
+    store_a(a_st(0));
+    store_b(b_st(0));
     if constexpr (G::BD || G::AP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (G::AT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (asm stores)
     __syncthreads();
-    frag(smem, 0, f0);
+    frag(0, 0, f0);
   }
   auto tile = [&](int t, auto MORE) {
     constexpr bool more = decltype(MORE)::value;
-    const float* cur = smem + (t & 1) * STAGE;
-    float* nxt = smem + ((t + 1) & 1) * STAGE;
+    const int tc = t & 1, tx = (t + 1) & 1;
     TNS_PH(5);
     if constexpr (more && !G::IL && !G::ST) {
       advance();
       if constexpr (G::BD) {
-        gather_b(nxt + A_TILE);
-        load_a((t + 1) * BK, nxt);
+        gather_b(b_st(tx));
+        load_a((t + 1) * BK, a_st(tx));
       } else {
-        load_a((t + 1) * BK, nxt);
-        gather_b(nxt + A_TILE);
+        load_a((t + 1) * BK, a_st(tx));
+        gather_b(b_st(tx));
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
     }
@@ -436,6 +489,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           // under this group's MFMAs
           TNS_PH(3);
           if constexpr (G::BD || G::AP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if constexpr (G::AT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (asm stores)
           __syncthreads();
           TNS_PH(4);
         }
@@ -443,28 +497,28 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (more && G::ST)
         if (g < 2 && half == g) {
           advance();
-          load_a((t + 1) * BK, nxt);
-          gather_b(nxt + A_TILE);
+          load_a((t + 1) * BK, a_st(tx));
+          gather_b(b_st(tx));
           __builtin_amdgcn_sched_barrier(0);
         }
       // one scheduling region per group: the next group's fragment reads,
       // interleaved staging (LI / SI) and this group's MFMAs
       const bool reads = g + 1 < NG || more;
       if (g + 1 < NG)
-        frag(cur, g + 1, fn);
+        frag(tc, g + 1, fn);
       else if (more)
-        frag(nxt, 0, fn);
+        frag(tx, 0, fn);
       if constexpr (more && G::IL) {
         if (g == 0) {
           advance();
-          load_a((t + 1) * BK, nxt);
-          gather_b(nxt + A_TILE);
+          load_a((t + 1) * BK, a_st(tx));
+          gather_b(b_st(tx));
         }
       }
       if constexpr (more && G::SI) {
         if (g == G::SG) {
-          store_a(nxt);
-          store_b(nxt + A_TILE);
+          store_a(a_st(tx));
+          store_b(b_st(tx));
         }
       }
       mma(fc);
@@ -488,15 +542,15 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (more && G::ST)
         if (g >= G::SG && g <= G::SG + 1 && g == G::SG + half) {
-          store_a(nxt);
-          store_b(nxt + A_TILE);
+          store_a(a_st(tx));
+          store_b(b_st(tx));
           __builtin_amdgcn_sched_barrier(0);
         }
       if constexpr (more && !G::SI && !G::ST)
         if (g == G::SG) {
           TNS_PH(1);
-          store_a(nxt);
-          store_b(nxt + A_TILE);
+          store_a(a_st(tx));
+          store_b(b_st(tx));
           __builtin_amdgcn_sched_barrier(0);
           TNS_PH(2);
         }
@@ -600,6 +654,12 @@ struct TileInfo4 {
                   true>>,                                                                        \
    "conv_tile4_ap<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv      \
    ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4X(BMv, BNv, WMv, WNv, BKv, SGv, RIv, JAv, NAv)                                  \
+  {BMv, BNv, BKv,                                                                             \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, false, RIv, false, JAv, NAv, false, false, \
+                  false, false, true>>,                                                       \
+   "conv_tile4_at<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",ri" #RIv ",j" #JAv   \
+   "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -629,6 +689,14 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
     TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
     TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
+    // B stored by ds_write_addtid_b32 (AT), the picked shapes with block-placed stores
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 25 (1 / 3)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 26
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 27 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 28 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 29 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 30 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 31 (11)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
@@ -666,6 +734,7 @@ constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
 #undef TNS_CT4D
 #undef TNS_CT4A
 #undef TNS_CT4UD
+#undef TNS_CT4X
 #undef TNS_CT4T
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
