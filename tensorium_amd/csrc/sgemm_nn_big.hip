@@ -325,20 +325,21 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 // registers at the 512 cap — not instantiated)
 // (form 5 is the ping-pong schedule of the 256x256 tile, sgemm_nn_pp.hip;
 // forms 6 and 7 the tile at one wave per SIMD with both operands by LDS-DMA,
-// sgemm_nn_w4.hip (7: the barrier before a tile's last step); form 8, the
+// sgemm_nn_w4.hip (7: the barrier before a tile's last step; 8: that with
+// interleaved columns, 16-byte B reads and C traffic); form 9, the
 // ping-pong tile with B register-staged into k-permuted slots, is compiled
 // into the diagnostics build only: measured, not picked)
 #ifdef TNS_DIAG_KERNELS
-int sgemm_nn_big_count() { return 9; }
+int sgemm_nn_big_count() { return 10; }
 #else
-int sgemm_nn_big_count() { return 8; }
+int sgemm_nn_big_count() { return 9; }
 #endif
 const char* sgemm_nn_big_name(int v) {
   static const char* names[] = {"256x256x32_w2x4_nn_big", "128x128x32_w2x2_nn_big",
                                 "256x128x32_w2x2_nn_big", "256x256x32_w4x4_nn_big",
                                 "256x128x16_w2x2_b2_nn_big", "256x256x32_w2x4_pp_nn_big",
                                 "256x256x32_w2x2_dma_nn_big", "256x256x32_w2x2_dmal_nn_big",
-                                "256x256x32_w2x4_ppbq_nn_big"};
+                                "256x256x32_w2x2_dmav_nn_big", "256x256x32_w2x4_ppbq_nn_big"};
   return v >= 0 && v < sgemm_nn_big_count() ? names[v] : "";
 }
 
@@ -361,8 +362,9 @@ hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s) {
     case 5: return launch_sgemm_nn_pp(a, s);
     case 6: return launch_sgemm_nn_w4(a, s);
     case 7: return launch_sgemm_nn_w4(a, s, true);
+    case 8: return launch_sgemm_nn_w4(a, s, true, true);
 #ifdef TNS_DIAG_KERNELS
-    case 8: return launch_sgemm_nn_pp(a, s, true);  // k-permuted B slots
+    case 9: return launch_sgemm_nn_pp(a, s, true);  // k-permuted B slots
 #endif
     default: return hipErrorInvalidValue;
   }

@@ -30,6 +30,8 @@ namespace tns {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef int int4v __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 256, BN = 256, BK = 32, NT = 256;
 constexpr int A_TILE = BM * BK, B_TILE = BK * BN, STAGE = A_TILE + B_TILE;  // floats
@@ -44,7 +46,12 @@ __device__ __forceinline__ void dma16(const float* sbase, unsigned voff, unsigne
       : "memory");
 }
 
-template <bool ALPHA1, bool LATE>
+// BV: accumulator tile j's column lc is block column wn*128 + 4 lc + j (not
+// 32 j + lc), so a lane's four B fragments of a step are one ds_read_b128 and
+// its four tiles' values of one row are 4 consecutive columns of C: the beta
+// loads and the epilogue stores move 16 bytes per lane (64 instead of 256
+// memory instructions per lane)
+template <bool ALPHA1, bool LATE, bool BV>
 __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -82,7 +89,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   const int64_t row_base = m0 + wm * 128;
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
       C + row_base * ldc, 0, 0x7fffffff, 0x00020000);
-  const unsigned c_voff = 4u * (unsigned)(4 * h * ldc + n0 + wn * 128 + lc);
+  const unsigned c_voff = 4u * (unsigned)(4 * h * ldc + n0 + wn * 128 + (BV ? 4 * lc : lc));
   auto c_soff = [&](int i, int e) {
     return (unsigned)(4 * (32 * i + (e & 3) + 8 * (e >> 2)) * ldc);
   };
@@ -105,6 +112,28 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
         t[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                              crs, c_voff + 128u * (g & 3), c_soff(g >> 2, e), 0));
     };
+    if constexpr (BV) {
+      // row group g = (i, e-block of 4): 4 float4 loads = tiles 0..3 of 4 rows
+      floatx4 v[2][4];
+      auto ldv = [&](int g, floatx4 (&t)[4]) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          t[u] = __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 crs, c_voff, c_soff(g >> 2, 4 * (g & 3) + u), 0));
+      };
+      ldv(0, v[0]);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        if (g + 1 < 16) ldv(g + 1, v[(g + 1) & 1]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float c = v[g & 1][u][j];
+            acc[g >> 2][j][4 * (g & 3) + u] = scale ? beta * c : c;
+          }
+      }
+    } else {
     ld(0, tmp[0]);
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
@@ -114,6 +143,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
         const float c = tmp[g & 1][e];
         acc[g >> 2][g & 3][e] = scale ? beta * c : c;
       }
+    }
     }
   }
 #pragma unroll
@@ -160,14 +190,20 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   const int a_lane = (wm * 128 + lc) * BK + h;
   int b_col[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) b_col[j] = A_TILE + h * BN + ((wn * 128 + 32 * j + lc - 32 * h) & 255);
+  for (int j = 0; j < 4; ++j)
+    b_col[j] = A_TILE + h * BN + ((wn * 128 + (BV ? 4 * lc + j : 32 * j + lc) - 32 * h) & 255);
   const float alpha = p.alpha;
   auto frag = [&](const float* st, int s, float (&a)[4], float (&b)[4]) {
     const int ka = 4 * ((s >> 1) ^ swz) + 2 * (s & 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = st[a_lane + 32 * BK * i + ka];
+    if constexpr (BV) {
+      const floatx4 v = *reinterpret_cast<const floatx4*>(st + b_col[0] + 2 * s * BN);
+      b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; b[3] = v[3];
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b[j] = st[b_col[j] + 2 * s * BN];
+      for (int j = 0; j < 4; ++j) b[j] = st[b_col[j] + 2 * s * BN];
+    }
   };
   auto mma = [&](const float (&a)[4], const float (&b)[4]) {
     float aa[4];
@@ -258,8 +294,18 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
     for (int e = 0; e < 16; ++e)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, acc[i][j][e]), crs,
-                                              c_voff + 128u * j, c_soff(i, e), 0);
+        if constexpr (!BV)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, acc[i][j][e]), crs,
+                                                c_voff + 128u * j, c_soff(i, e), 0);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e)
+      if constexpr (BV) {
+        const floatx4 v = {acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, v), crs, c_voff,
+                                               c_soff(i, e), 0);
+      }
 }
 
 bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
@@ -277,7 +323,7 @@ bool sgemm_nn_w4_applies(const GemmArgs& a) {
   return (a.M / BM) * (a.N / BN) <= 0x7fffffff;
 }
 
-hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late) {
+hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late, bool bv) {
   if (!sgemm_nn_w4_applies(a)) return hipErrorInvalidValue;
   const int64_t tiles = (a.M / BM) * (a.N / BN);
   const bool alpha1 = a.alpha == 1.0f;
@@ -289,16 +335,21 @@ hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late) {
     sub.C = a.C + b0 * a.strideC;
     sub.batch = nb;
     const dim3 grid((unsigned)tiles, (unsigned)nb);
-    if (late) {
+    if (bv) {  // (the late-barrier schedule)
       if (alpha1)
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, true>), grid, dim3(NT), 0, s, sub);
+        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, true, true>), grid, dim3(NT), 0, s, sub);
       else
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, true>), grid, dim3(NT), 0, s, sub);
+        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, true, true>), grid, dim3(NT), 0, s, sub);
+    } else if (late) {
+      if (alpha1)
+        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, true, false>), grid, dim3(NT), 0, s, sub);
+      else
+        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, true, false>), grid, dim3(NT), 0, s, sub);
     } else {
       if (alpha1)
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, false>), grid, dim3(NT), 0, s, sub);
+        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, false, false>), grid, dim3(NT), 0, s, sub);
       else
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, false>), grid, dim3(NT), 0, s, sub);
+        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, false, false>), grid, dim3(NT), 0, s, sub);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

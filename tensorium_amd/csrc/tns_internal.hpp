@@ -86,9 +86,11 @@ hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s);
 bool sgemm_nn_pp_applies(const GemmArgs& a);
 hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s, bool bperm = false);
 // the same tile with one wave per SIMD (4 waves of 128 x 128), A and B by
-// LDS-DMA into swizzled row images (sgemm_nn_w4.hip; forms 6, 7 = late barrier)
+// LDS-DMA into swizzled row images (sgemm_nn_w4.hip; forms 6, 7 = late barrier,
+// 8 = late barrier + interleaved columns: b128 B reads, 16-byte C traffic)
 bool sgemm_nn_w4_applies(const GemmArgs& a);
-hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late = false);
+hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late = false,
+                              bool bv = false);
 // gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
 // plain epilogue only
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
