@@ -10,4 +10,6 @@ timeout -k 10 300 python scripts/conv_tile_sweep.py --rounds 2 --only 105,107,11
 echo "conv sweep ok"
 timeout -k 10 400 python scripts/bwd_sweep.py > gpurun_out/bwd_sweep.json 2> gpurun_out/bwd_sweep.err || exit $?
 echo "bwd sweep ok"
+timeout -k 10 120 python scripts/bn_perf.py > gpurun_out/bn_perf_r4.json 2> gpurun_out/bn_perf_r4.err || exit $?
+echo "bn perf ok"
 NOBENCH=1 bash scripts/gpu_r4_check.sh || exit $?

@@ -456,8 +456,9 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
   constexpr int SNT = 192, E = 32, TILE = SNT * E, NBUF = 3;
   constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;
   // lane-major rows (a chain's terms contiguous), LDT = 8 mod 32 for
-  // conflict-free staging stores, and 64 floats of slack past a row's last
-  // term: the chain loop reads two 16-term groups ahead without a bound test
+  // conflict-free staging stores, and 72 floats of slack past a row's last
+  // term: the chain loop reads up to 47 terms past its last full group
+  // without a bound test
   constexpr int LDT = TILE / 8 + 72;
   __shared__ __attribute__((aligned(16))) float U[NBUF][8 * LDT];
   __shared__ __attribute__((aligned(16))) float V[TWO ? NBUF : 1][TWO ? 8 * LDT : 1];
@@ -548,7 +549,7 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
           const float* row =
               ((MODE == CH_VDELTA && grp == 1) ? &V[buf][0] : &U[buf][0]) + l * LDT;
           const float* rowb = TWO ? &V[buf][0] + l * LDT : row;
-          float va[16], wa[16], vb[16], wb[16];
+          float va[16], wa[16], vb[16], wb[16], vc[16], wc[16];
           auto rd = [&](int q, float (&v)[16], float (&w)[16]) {
 #pragma unroll
             for (int z = 0; z < 16; z += 4) {
@@ -567,18 +568,25 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
               else acc = acc + v[z];
             }
           };
-          // groups of 16 terms, the next two groups' reads always in flight
+          // groups of 16 terms in a ring of three register sets: a group's
+          // reads go out right after the group two ahead of it is consumed
+          // (32 dependent adds of cover for the LDS latency; with two sets
+          // only 16, and the chain waited on its reads at every group)
           // (unconditional: they may read the row's slack past cnt)
-          const int full = cnt & ~31;
+          const int full = cnt - cnt % 48;
           rd(0, va, wa);
           rd(16, vb, wb);
-          for (int q = 0; q < full; q += 32) {
+          rd(32, vc, wc);
+          for (int q = 0; q < full; q += 48) {
             add16(va, wa);
             __builtin_amdgcn_sched_barrier(0);
-            rd(q + 32, va, wa);
+            rd(q + 48, va, wa);
             add16(vb, wb);
             __builtin_amdgcn_sched_barrier(0);
-            rd(q + 48, vb, wb);
+            rd(q + 64, vb, wb);
+            add16(vc, wc);
+            __builtin_amdgcn_sched_barrier(0);
+            rd(q + 80, vc, wc);
           }
           for (int q = full; q < cnt; ++q) {
             if constexpr (MODE == CH_DOT) acc = fmaf(row[q], rowb[q], acc);

@@ -136,6 +136,12 @@ struct Geo4 {
   static constexpr int B_TILE = ROWS * BN * 4;  // floats
   static constexpr int AU = BM * BK / 4 / NT;   // float4 A units per thread
   static constexpr int KI = BK / 4 / NW;        // B k-slots per thread
+  // ATA: with AT, the A stores too by ds_write_addtid_b32 where both stages'
+  // A images lie within M0 + offset reach (lanes = 16 rows x the 4 slot
+  // components of one k group: each of a float4's values goes to one slot row
+  // as 64 consecutive dwords)
+  static constexpr bool ATA = AT && (2 * B_TILE + 2 * A_TILE) * 4 <= 126976 &&
+                              NG * (BM / 16) % NW == 0 && NG * (BM / 16) / NW == AU;
   static_assert(BM == 16 * WM, "one 16-row strip per wave");
   static_assert(BM % 16 == 0 && BN % 16 == 0, "b128 slot rows: 64-dword multiples");
   static_assert(BK % 16 == 0 && SG <= NG - 2, "stores precede the barrier");
@@ -352,6 +358,12 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       const int m = idx % BM, row = idx / BM;
       a_src[u] = p.A + (int64_t)(16 * (row >> 2) + (row & 3)) * p.lda + m0 + m;
       a_dst[u] = (row * BM + m) * 4;
+    } else if constexpr (G::ATA) {
+      // unit u of wave w: group g and 16-row block mb, lane = (row, component i)
+      const int pair = u * G::NW + w, g = pair / (BM / 16), mb = 16 * (pair % (BM / 16));
+      const int m = mb + (lane >> 2), i = lane & 3;
+      a_src[u] = p.A + (m0 + m) * p.lda + 16 * g + 4 * i;
+      a_dst[u] = ((4 * g) * BM + mb) * 4;  // slot row 4g + c: + c * BM * 4 (in floats)
     } else {
       // 8 k-quads of one row per 8 lanes (128 contiguous bytes per row)
       const int lo = idx & 7, rest = idx >> 3;
@@ -403,6 +415,17 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     for (int u = 0; u < AU; ++u) {
       if constexpr (G::TA) {
         *reinterpret_cast<float4*>(as + a_dst[u]) = ra[u];
+      } else if constexpr (G::ATA) {
+        const float v[4] = {ra[u].x, ra[u].y, ra[u].z, ra[u].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const unsigned base =
+              lds0 + 4u * (unsigned)((as - smem) + __builtin_amdgcn_readfirstlane(a_dst[u]) + c * BM * 4);
+          if (base < 65536u)
+            st_addtid<0>(v[c], base);
+          else
+            st_addtid<32768>(v[c], base - 32768u);
+        }
       } else {
         as[a_dst[u]] = ra[u].x;
         as[a_dst[u] + BM * 4] = ra[u].y;
