@@ -455,7 +455,10 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < JW; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[i], f.b[j][i], acc[j], 0, 0, 0);
+        if constexpr (G::AT)  // (transposed tile: rows = pixels, columns = filters)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.b[j][i], f.a[i], acc[j], 0, 0, 0);
+        else
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[i], f.b[j][i], acc[j], 0, 0, 0);
   };
 
 #ifdef TNS_CT4_STAMPS
@@ -596,6 +599,40 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   // ---- epilogue: forwardBias + activate, conv output [img][filter][pixel] --
   const bool fuse = p.epi == EPI_BIAS_ACT;
   const int act = p.act;
+  if constexpr (G::AT) {
+    // the MFMAs ran with the operands swapped (same products, same k order:
+    // bit-identical): lane (r16, q) holds filter m0 + wm*16 + r16 at the four
+    // consecutive pixels 16j + 4q + e, one 16-byte store where they are in
+    // one image (every image's pixel count a multiple of 4)
+    const int64_t row = m0 + wm * 16 + r16;
+    const float bi = fuse ? p.bias[row] : 0.0f;
+    const bool v4 = (p.conv_ohw & 3) == 0 && (p.strideC & 3) == 0 && (p.ldc & 3) == 0 &&
+                    (reinterpret_cast<uintptr_t>(p.C) & 15) == 0;
+#pragma unroll
+    for (int j = 0; j < JW; ++j) {
+      const int nb = n0 + coff * 16 + 16 * j + 4 * q;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fuse ? act_apply_cheap(acc[j][e] + bi, act) : acc[j][e];
+      if (v4) {
+        if (nb < N) {
+          const int img = nb / p.conv_ohw, pix = nb - img * p.conv_ohw;
+          *reinterpret_cast<float4*>(p.C + (int64_t)img * p.strideC + pix + row * p.ldc) =
+              make_float4(v[0], v[1], v[2], v[3]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int n = nb + e;
+          if (n < N) {
+            const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
+            p.C[(int64_t)img * p.strideC + pix + row * p.ldc] = v[e];
+          }
+        }
+      }
+    }
+    return;
+  }
   const int64_t row0 = m0 + wm * 16 + 4 * q;
   float bias[4];
 #pragma unroll
