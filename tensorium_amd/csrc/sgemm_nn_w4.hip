@@ -167,6 +167,19 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem;
   const float* a_row0 = A + m0 * lda;  // + (8q) * lda + k0
   const float* b_row0 = B + n0;        // + (k0 + r) * ldb
+  // DMA instruction u (0..15) of this wave for tile k0 into stage st
+  auto issue1 = [&](int u, int64_t k0, int st) {
+    const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
+    if (u < 8) {
+      const int q = 8 * wid + u;
+      dma16(a_row0 + (int64_t)(8 * q) * lda + k0, (u & 1) ? a_voff1 : a_voff,
+            sb + (unsigned)(q * 1024));
+    } else {
+      const int r = 8 * wid + (u - 8);
+      dma16(b_row0 + (k0 + r) * ldb, (u & 1) ? b_voff1 : b_voff0,
+            sb + (unsigned)(A_TILE * 4 + r * 1024));
+    }
+  };
   auto issue = [&](int64_t k0, int st) {
     const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
 #pragma unroll
@@ -214,6 +227,21 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(aa[i], b[j], acc[i][j], 0, 0, 0);
+  };
+  // (BV) a step's 16 MFMAs with the 16 DMA instructions of tile k0 issued
+  // one after each: the DMA issue (SALU + VMEM) fills the 64-cycle gaps the
+  // matrix pipe leaves between this wave's MFMAs instead of delaying them
+  auto mma_dma = [&](const float (&a)[4], const float (&b)[4], int64_t k0, int st, bool dma) {
+    float aa[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) aa[i] = ALPHA1 ? a[i] : alpha * a[i];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = u >> 2, j = u & 3;
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(aa[i], b[j], acc[i][j], 0, 0, 0);
+      if (dma) issue1(u, k0, st);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   };
 
   const int nt = (int)(p.K / BK);
@@ -279,11 +307,15 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
       if (t + 1 < nt) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1
         __syncthreads();  // every wave's; every read of tile t complete
-        if (t + 2 < nt) issue((int64_t)(t + 2) * BK, t & 1);
+        if constexpr (!BV)
+          if (t + 2 < nt) issue((int64_t)(t + 2) * BK, t & 1);
         frag(nxt, 0, a0, b0);
         __builtin_amdgcn_sched_barrier(0);
       }
-      mma(a1, b1);  // step 15
+      if constexpr (BV)
+        mma_dma(a1, b1, (int64_t)(t + 2) * BK, t & 1, t + 2 < nt);  // step 15 + tile t+2's DMA
+      else
+        mma(a1, b1);  // step 15
     }
   }
 
