@@ -4,7 +4,7 @@
 # the first failure.
 set -u
 mkdir -p gpurun_out
-timeout -k 10 240 python scripts/nn_big_ab.py --variants 5,6,7,8 --rounds 5 > gpurun_out/ab_w4.json 2> gpurun_out/ab_w4.err || exit $?
+timeout -k 10 240 python scripts/nn_big_ab.py --variants 5,6 --rounds 5 > gpurun_out/ab_w4.json 2> gpurun_out/ab_w4.err || exit $?
 echo "ab ok"; tail -2 gpurun_out/ab_w4.json
 timeout -k 10 300 python scripts/conv_tile_sweep.py --rounds 2 --only 105,107,112,117,122,125,129,130,131,132,133,134,135 > gpurun_out/ct_sweep_at.json 2> gpurun_out/ct_sweep_at.err || exit $?
 echo "conv sweep ok"

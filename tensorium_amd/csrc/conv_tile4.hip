@@ -633,6 +633,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
     return;
   }
+  const bool add = p.epi == EPI_ADD;  // dX of a 1x1 layer: col2im fused (C += col)
   const int64_t row0 = m0 + wm * 16 + 4 * q;
   float bias[4];
 #pragma unroll
@@ -647,6 +648,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     for (int e = 0; e < 4; ++e) {
       float v = acc[j][e];
       if (fuse) v = act_apply_cheap(v + bias[e], act);
+      if (add) v = cp[e * p.ldc] + v;
       cp[e * p.ldc] = v;
     }
   }
@@ -749,14 +751,6 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
     TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
     TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
-    // B stored by ds_write_addtid_b32 (AT), the picked shapes with block-placed stores
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 25 (1 / 3)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 26
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 27 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 28 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 29 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 30 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 31 (11)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
@@ -767,6 +761,19 @@ const TileInfo4 kTiles4[] = {
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
     TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 28 (3)
+    // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
+    // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
+    // shapes: timed slower on every layer class (gpurun_out/
+    // ct_sweep_at.json: 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
+    // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
+    // the gather's 4 k rows per load instruction touch 4x the cache lines
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 29 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 30
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 31 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 32 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 33 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 34 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 35 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
@@ -851,8 +858,9 @@ int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K) {
 
 hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float* col,
                                 int64_t batch, int64_t C, int64_t ks, int64_t F, int64_t oh,
-                                int64_t ow, hipStream_t s) {
+                                int64_t ow, hipStream_t s, bool add_into) {
   if (v < 0 || v >= kNumTiles4T) return hipErrorInvalidValue;
+  if (add_into && ks != 1) return hipErrorInvalidValue;
   const int64_t M = C * ks * ks, hw = oh * ow;
   if (batch * F * hw * 4 > 0x7fffffffLL || batch * hw > 0x7fffffffLL) return hipErrorInvalidValue;
   GemmArgs a{};
@@ -861,7 +869,7 @@ hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float
   a.A = w; a.lda = M; a.strideA = 0;
   a.B = delta; a.ldb = hw; a.strideB = F * hw;
   a.C = col; a.ldc = hw; a.strideC = M * hw;
-  a.batch = 1; a.epi = EPI_NONE; a.bias = nullptr; a.act = 0;
+  a.batch = 1; a.epi = add_into ? EPI_ADD : EPI_NONE; a.bias = nullptr; a.act = 0;
   a.conv = 2;
   a.conv_H = (int)oh; a.conv_W = (int)ow; a.conv_ow = (int)ow; a.conv_ohw = (int)hw;
   a.conv_sY = 1; a.conv_sX = 1; a.conv_pH = 0; a.conv_pW = 0;

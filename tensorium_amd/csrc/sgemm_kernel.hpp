@@ -482,7 +482,7 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
     st[5] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
   }
 #endif
-  const bool fuse = p.epi == EPI_BIAS_ACT;
+  const bool fuse = p.epi == EPI_BIAS_ACT, add = p.epi == EPI_ADD;
   const int act = p.act;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -498,6 +498,7 @@ __global__ __launch_bounds__(S::NT, S::MINW) void sgemm_mfma_kernel(GemmArgs p) 
         float v = acc[i][j][e];
         // forwardBias then activate (logistic/tanh: a separate pass, host side)
         if (fuse) v = act_apply_cheap(v + bias, act);
+        if (add) v = C[c_at(row, col)] + v;
         C[c_at(row, col)] = v;
       }
     }

@@ -324,31 +324,30 @@ hipError_t launch(const GemmArgs& a, hipStream_t s) {
 // (a 4-wave 256x256 form, wave tile 128x128 at one wave per SIMD, spills 67
 // registers at the 512 cap — not instantiated)
 // (form 5 is the ping-pong schedule of the 256x256 tile, sgemm_nn_pp.hip;
-// forms 6 and 7 the tile at one wave per SIMD with both operands by LDS-DMA,
-// sgemm_nn_w4.hip (7: the barrier before a tile's last step; 8: that with
-// interleaved columns, 16-byte B reads and C traffic); form 9, the
-// ping-pong tile with B register-staged into k-permuted slots, is compiled
-// into the diagnostics build only: measured, not picked)
+// form 6 the tile at one wave per SIMD with both operands by LDS-DMA and
+// interleaved columns, sgemm_nn_w4.hip; form 7, the ping-pong tile with B
+// register-staged into k-permuted slots, is compiled into the diagnostics
+// build only: measured, not picked)
 #ifdef TNS_DIAG_KERNELS
-int sgemm_nn_big_count() { return 10; }
+int sgemm_nn_big_count() { return 8; }
 #else
-int sgemm_nn_big_count() { return 9; }
+int sgemm_nn_big_count() { return 7; }
 #endif
 const char* sgemm_nn_big_name(int v) {
   static const char* names[] = {"256x256x32_w2x4_nn_big", "128x128x32_w2x2_nn_big",
                                 "256x128x32_w2x2_nn_big", "256x256x32_w4x4_nn_big",
                                 "256x128x16_w2x2_b2_nn_big", "256x256x32_w2x4_pp_nn_big",
-                                "256x256x32_w2x2_dma_nn_big", "256x256x32_w2x2_dmal_nn_big",
-                                "256x256x32_w2x2_dmav_nn_big", "256x256x32_w2x4_ppbq_nn_big"};
+                                "256x256x32_w2x2_dma_nn_big", "256x256x32_w2x4_ppbq_nn_big"};
   return v >= 0 && v < sgemm_nn_big_count() ? names[v] : "";
 }
 
-// heuristic: the 256x256 tile when it gives about a block per CU, on the
-// ping-pong schedule (form 5; 4096^3 0.994 -> 0.972 ms, 8192^3 7.83 -> 7.68,
-// bit-identical to form 0)
+// heuristic: the 256x256 tile when it gives about a block per CU, at one
+// wave per SIMD with LDS-DMA operands where it applies (form 6; 4096^3 0.983
+// -> 0.950 ms against the ping-pong form 5, which itself took 0.994 -> 0.972
+// from form 0; all bit-identical)
 int sgemm_nn_big_pick(const GemmArgs& a) {
   if (applies<G256>(a) && (a.M / 256) * (a.N / 256) * a.batch >= 192)
-    return sgemm_nn_pp_applies(a) ? 5 : 0;
+    return sgemm_nn_w4_applies(a) ? 6 : sgemm_nn_pp_applies(a) ? 5 : 0;
   return -1;
 }
 
@@ -361,10 +360,8 @@ hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s) {
     case 4: return launch<G256x128k16>(a, s);
     case 5: return launch_sgemm_nn_pp(a, s);
     case 6: return launch_sgemm_nn_w4(a, s);
-    case 7: return launch_sgemm_nn_w4(a, s, true);
-    case 8: return launch_sgemm_nn_w4(a, s, true, true);
 #ifdef TNS_DIAG_KERNELS
-    case 9: return launch_sgemm_nn_pp(a, s, true);  // k-permuted B slots
+    case 7: return launch_sgemm_nn_pp(a, s, true);  // k-permuted B slots
 #endif
     default: return hipErrorInvalidValue;
   }

@@ -18,9 +18,22 @@
 //     by row on the source side (chunk slot = chunk ^ ((m >> 1) & 7)), B as
 //     [k][256 n] rows rotated by 32 floats on odd k: both fragment reads are
 //     conflict-free or 2-way (A: lanes m and m + 16 share a bank);
-//   * two LDS stages (2 x 64 KB); the next k-tile's DMA is issued at the top
-//     of a tile and waited for (vmcnt + one barrier) at its end; fragments of
-//     step s+1 are read before step s's MFMAs (scheduling fences).
+//   * two LDS stages (2 x 64 KB); the barrier that publishes tile t+1 sits
+//     before tile t's last step, whose 16 MFMAs each carry one of the 16 DMA
+//     instructions of tile t+2 (into tile t's stage): the DMA goes out a whole
+//     tile ahead of its use; fragments of step s+1 are read before step s's
+//     MFMAs (scheduling fences);
+//   * interleaved columns: accumulator tile j's column lc is block column
+//     wn*128 + 4 lc + j (not 32 j + lc), so a lane's four B fragments of a
+//     step are one ds_read_b128 and its four tiles' values of one row are 4
+//     consecutive columns of C: beta loads and epilogue stores move 16 bytes
+//     per lane.
+//
+// Measured at 4096^3 (scripts/nn_big_ab.py, gpurun_out/ab_w4.json): 0.950 ms
+// vs 0.983 for the ping-pong form on the same box, bit-identical.  (The
+// forms with 32 j + lc columns and 4-byte B reads, with the DMA issued as one
+// burst, measured 0.988-0.992 ms and did not reproduce the ping-pong bits at
+// 4096^3; dropped.)
 //
 // alpha != 1 multiplies the A fragments after the read (one rounding, as the
 // reference's A_PART = ALPHA*A[kk]).
@@ -46,12 +59,7 @@ __device__ __forceinline__ void dma16(const float* sbase, unsigned voff, unsigne
       : "memory");
 }
 
-// BV: accumulator tile j's column lc is block column wn*128 + 4 lc + j (not
-// 32 j + lc), so a lane's four B fragments of a step are one ds_read_b128 and
-// its four tiles' values of one row are 4 consecutive columns of C: the beta
-// loads and the epilogue stores move 16 bytes per lane (64 instead of 256
-// memory instructions per lane)
-template <bool ALPHA1, bool LATE, bool BV>
+template <bool ALPHA1>
 __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -89,7 +97,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   const int64_t row_base = m0 + wm * 128;
   const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
       C + row_base * ldc, 0, 0x7fffffff, 0x00020000);
-  const unsigned c_voff = 4u * (unsigned)(4 * h * ldc + n0 + wn * 128 + (BV ? 4 * lc : lc));
+  const unsigned c_voff = 4u * (unsigned)(4 * h * ldc + n0 + wn * 128 + 4 * lc);
   auto c_soff = [&](int i, int e) {
     return (unsigned)(4 * (32 * i + (e & 3) + 8 * (e >> 2)) * ldc);
   };
@@ -105,14 +113,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
     // its accumulator registers
     const bool scale = p.beta_mode == BETA_SCALE;
     const float beta = p.beta;
-    floatx16 tmp[2];
-    auto ld = [&](int g, floatx16& t) {
-#pragma unroll
-      for (int e = 0; e < 16; ++e)
-        t[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                             crs, c_voff + 128u * (g & 3), c_soff(g >> 2, e), 0));
-    };
-    if constexpr (BV) {
+    {
       // row group g = (i, e-block of 4): 4 float4 loads = tiles 0..3 of 4 rows
       floatx4 v[2][4];
       auto ldv = [&](int g, floatx4 (&t)[4]) {
@@ -133,17 +134,6 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
             acc[g >> 2][j][4 * (g & 3) + u] = scale ? beta * c : c;
           }
       }
-    } else {
-    ld(0, tmp[0]);
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      if (g + 1 < 16) ld(g + 1, tmp[(g + 1) & 1]);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const float c = tmp[g & 1][e];
-        acc[g >> 2][g & 3][e] = scale ? beta * c : c;
-      }
-    }
     }
   }
 #pragma unroll
@@ -204,19 +194,14 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   int b_col[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    b_col[j] = A_TILE + h * BN + ((wn * 128 + (BV ? 4 * lc + j : 32 * j + lc) - 32 * h) & 255);
+    b_col[j] = A_TILE + h * BN + ((wn * 128 + 4 * lc + j - 32 * h) & 255);
   const float alpha = p.alpha;
   auto frag = [&](const float* st, int s, float (&a)[4], float (&b)[4]) {
     const int ka = 4 * ((s >> 1) ^ swz) + 2 * (s & 1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = st[a_lane + 32 * BK * i + ka];
-    if constexpr (BV) {
-      const floatx4 v = *reinterpret_cast<const floatx4*>(st + b_col[0] + 2 * s * BN);
-      b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; b[3] = v[3];
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = st[b_col[j] + 2 * s * BN];
-    }
+    const floatx4 v = *reinterpret_cast<const floatx4*>(st + b_col[0] + 2 * s * BN);
+    b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; b[3] = v[3];
   };
   auto mma = [&](const float (&a)[4], const float (&b)[4]) {
     float aa[4];
@@ -228,7 +213,7 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(aa[i], b[j], acc[i][j], 0, 0, 0);
   };
-  // (BV) a step's 16 MFMAs with the 16 DMA instructions of tile k0 issued
+  // a step's 16 MFMAs with the 16 DMA instructions of tile k0 issued
   // one after each: the DMA issue (SALU + VMEM) fills the 64-cycle gaps the
   // matrix pipe leaves between this wave's MFMAs instead of delaying them
   auto mma_dma = [&](const float (&a)[4], const float (&b)[4], int64_t k0, int st, bool dma) {
@@ -246,34 +231,8 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
 
   const int nt = (int)(p.K / BK);
   float a0[4], b0[4], a1[4], b1[4];
-  if constexpr (!LATE) {
-    if (nt > 0) {
-      issue(0, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    for (int t = 0; t < nt; ++t) {
-      const float* cur = smem + (t & 1) * STAGE;
-      // the next tile's DMA: its stage was last read in tile t-1, which every
-      // wave finished before the barrier that ended it
-      if (t + 1 < nt) issue((int64_t)(t + 1) * BK, (t + 1) & 1);
-      frag(cur, 0, a0, b0);
-#pragma unroll
-      for (int s = 0; s < BK / 2; s += 2) {
-        frag(cur, s + 1, a1, b1);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(a0, b0);
-        if (s + 2 < BK / 2) frag(cur, s + 2, a0, b0);
-        __builtin_amdgcn_sched_barrier(0);
-        mma(a1, b1);
-      }
-      if (t + 1 < nt) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of t+1 landed
-        __syncthreads();  // every wave's DMA landed; stage t&1 free for tile t+2
-      }
-    }
-  } else {
-    // LATE: the barrier that publishes tile t+1 sits before step 15 of tile
+  {
+    // the barrier that publishes tile t+1 sits before step 15 of tile
     // t, so tile t+1's first fragments are read under step 15's MFMAs and the
     // DMA of tile t+2 (into tile t's stage, whose reads all completed before
     // the barrier) goes out a whole tile ahead of its use
@@ -307,15 +266,10 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
       if (t + 1 < nt) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1
         __syncthreads();  // every wave's; every read of tile t complete
-        if constexpr (!BV)
-          if (t + 2 < nt) issue((int64_t)(t + 2) * BK, t & 1);
         frag(nxt, 0, a0, b0);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (BV)
-        mma_dma(a1, b1, (int64_t)(t + 2) * BK, t & 1, t + 2 < nt);  // step 15 + tile t+2's DMA
-      else
-        mma(a1, b1);  // step 15
+      mma_dma(a1, b1, (int64_t)(t + 2) * BK, t & 1, t + 2 < nt);  // step 15 + tile t+2's DMA
     }
   }
 
@@ -323,21 +277,11 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int e = 0; e < 16; ++e)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if constexpr (!BV)
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, acc[i][j][e]), crs,
-                                                c_voff + 128u * j, c_soff(i, e), 0);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int e = 0; e < 16; ++e)
-      if constexpr (BV) {
-        const floatx4 v = {acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, v), crs, c_voff,
-                                               c_soff(i, e), 0);
-      }
+    for (int e = 0; e < 16; ++e) {
+      const floatx4 v = {acc[i][0][e], acc[i][1][e], acc[i][2][e], acc[i][3][e]};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(int4v, v), crs, c_voff,
+                                             c_soff(i, e), 0);
+    }
 }
 
 bool aligned16(const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; }
@@ -355,7 +299,7 @@ bool sgemm_nn_w4_applies(const GemmArgs& a) {
   return (a.M / BM) * (a.N / BN) <= 0x7fffffff;
 }
 
-hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late, bool bv) {
+hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s) {
   if (!sgemm_nn_w4_applies(a)) return hipErrorInvalidValue;
   const int64_t tiles = (a.M / BM) * (a.N / BN);
   const bool alpha1 = a.alpha == 1.0f;
@@ -367,22 +311,10 @@ hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late, bool 
     sub.C = a.C + b0 * a.strideC;
     sub.batch = nb;
     const dim3 grid((unsigned)tiles, (unsigned)nb);
-    if (bv) {  // (the late-barrier schedule)
-      if (alpha1)
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, true, true>), grid, dim3(NT), 0, s, sub);
-      else
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, true, true>), grid, dim3(NT), 0, s, sub);
-    } else if (late) {
-      if (alpha1)
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, true, false>), grid, dim3(NT), 0, s, sub);
-      else
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, true, false>), grid, dim3(NT), 0, s, sub);
-    } else {
-      if (alpha1)
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<true, false, false>), grid, dim3(NT), 0, s, sub);
-      else
-        hipLaunchKernelGGL((sgemm_nn_w4_kernel<false, false, false>), grid, dim3(NT), 0, s, sub);
-    }
+    if (alpha1)
+      hipLaunchKernelGGL((sgemm_nn_w4_kernel<true>), grid, dim3(NT), 0, s, sub);
+    else
+      hipLaunchKernelGGL((sgemm_nn_w4_kernel<false>), grid, dim3(NT), 0, s, sub);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

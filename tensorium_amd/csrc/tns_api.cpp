@@ -1669,8 +1669,12 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     tns_clear_error();
     overlap = false;
   }
+  // a 1x1/s1/p0 layer's col2im adds each col element to its own pixel once:
+  // the dX product adds into state.delta in its epilogue instead (EPI_ADD,
+  // the same add), no col matrix
+  const bool dx_direct = state_delta && !needs_col && !fused_dx;
   float* ws = workspace;
-  if (!ws && (dw_col || (state_delta && !fused_dx && !(overlap && dw_col))))
+  if (!ws && (dw_col || (state_delta && !fused_dx && !dx_direct && !(overlap && dw_col))))
     if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws)) return r;
   if (!dx_ws) dx_ws = ws;  // col buffer of state.delta's chain
   // scratch of the fused state.delta kernel, sized before any fork (a growth
@@ -1751,12 +1755,13 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     // 1x1 "convolution" over the delta planes, the same chains), else the TN
     // GEMM
     bool done = false;
+    float* col = dx_direct ? state_delta : dx_ws;
     if (g_dx_tile != -2) {
       const int dv = g_dx_tile >= 0 ? (int)g_dx_tile : conv_tile4_dx_pick(i_n, batch * i_k, i_m);
       if (dv >= 0) {
         OpTimer t(c, TNS_OP_GEMM);
-        const hipError_t e = launch_conv_tile4_dx(dv, weights, delta, dx_ws, batch, C, kSize,
-                                                  filters, g.oh, g.ow, c->stream);
+        const hipError_t e = launch_conv_tile4_dx(dv, weights, delta, col, batch, C, kSize,
+                                                  filters, g.oh, g.ow, c->stream, dx_direct);
         if (e == hipSuccess)
           done = true;
         else if (e != hipErrorInvalidValue || g_dx_tile >= 0)
@@ -1767,8 +1772,10 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     }
     if (!done)
       if (int r = do_gemm(c, true, false, i_n, i_k, i_m, 1.0f, weights, i_n, 0, delta, i_k,
-                          i_m * i_k, 0.0f, dx_ws, i_k, colSize, batch, EPI_NONE, nullptr, 0, true))
+                          i_m * i_k, 0.0f, col, i_k, colSize, batch,
+                          dx_direct ? EPI_ADD : EPI_NONE, nullptr, 0, true))
         return r;
+    if (dx_direct) return TNS_OK;
     OpTimer t(c, TNS_OP_COL2IM);
     return hip_status(launch_col2im(g, dx_ws, colSize, state_delta, C * H * W, batch, c->stream),
                       "col2im launch");

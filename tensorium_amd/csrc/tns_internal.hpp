@@ -23,7 +23,8 @@ const char* hip_err_str(hipError_t e);
 // Epilogue applied after the K loop (fused conv path):
 //   EPI_NONE          C = acc
 //   EPI_BIAS_ACT      C = act(acc + bias[row])   (forwardBias + activate)
-enum EpiKind { EPI_NONE = 0, EPI_BIAS_ACT = 1 };
+//   EPI_ADD           C = C + acc (acc from +0; one add — a 1x1 col2im fused)
+enum EpiKind { EPI_NONE = 0, EPI_BIAS_ACT = 1, EPI_ADD = 2 };
 // logistic / tanh (exp in double) are applied after the GEMM, not in its
 // epilogue (tns_act.hpp)
 constexpr bool act_transcendental(int act) { return act == 0 || act == 6; }
@@ -86,11 +87,10 @@ hipError_t launch_sgemm_nn_big(int v, const GemmArgs& a, hipStream_t s);
 bool sgemm_nn_pp_applies(const GemmArgs& a);
 hipError_t launch_sgemm_nn_pp(const GemmArgs& a, hipStream_t s, bool bperm = false);
 // the same tile with one wave per SIMD (4 waves of 128 x 128), A and B by
-// LDS-DMA into swizzled row images (sgemm_nn_w4.hip; forms 6, 7 = late barrier,
-// 8 = late barrier + interleaved columns: b128 B reads, 16-byte C traffic)
+// LDS-DMA into swizzled row images, interleaved columns (b128 B reads,
+// 16-byte C traffic) — sgemm_nn_w4.hip, nn_big form 6
 bool sgemm_nn_w4_applies(const GemmArgs& a);
-hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s, bool late = false,
-                              bool bv = false);
+hipError_t launch_sgemm_nn_w4(const GemmArgs& a, hipStream_t s);
 // gemm(NoTrans, Trans) in the reference's sdot_avx2 order (sgemm_sdot.hip);
 // plain epilogue only
 hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s);
@@ -146,7 +146,8 @@ const char* conv_tile4_ta_name(int v);
 int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K);
 hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float* col,
                                 int64_t batch, int64_t C, int64_t ks, int64_t F, int64_t oh,
-                                int64_t ow, hipStream_t s);
+                                int64_t ow, hipStream_t s, bool add_into = false);
+// (add_into, 1x1 only: col is state.delta itself, each element C + col)
 // implicit-GEMM convolution on the ping-pong schedule (conv_pp.hip): same
 // operands and limits as conv_tile; conv_pp_pick = -1 where not measured faster
 int conv_pp_count();

@@ -281,10 +281,12 @@ def test_conv_backward_overlap_matches_sequential(hip, torch_cuda, ora, idx):
             assert np.array_equal(a, r)
 
 
-@pytest.mark.parametrize("idx", [3, 11, 28, 45])
+@pytest.mark.parametrize("idx", [3, 10, 11, 27, 28, 44, 45, 58])
 def test_conv_backward_dx_yolov3_batch8(hip, torch_cuda, ora, idx):
     """state.delta at YOLOv3 layer shapes, batch 8, on the default path (the
-    k-major-A conv tile where one applies): bit-exact."""
+    k-major-A conv tile where one applies; on the 1x1 layers 10, 27, 44, 58
+    the product adds into state.delta in its epilogue, col2im's one add per
+    pixel): bit-exact."""
     from tensorium_amd.yolo import yolov3_conv_table
     spec = yolov3_conv_table()[idx]
     got, ref = _dx_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,

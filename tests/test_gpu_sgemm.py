@@ -425,7 +425,7 @@ def test_nn_big_kernel_bit_exact(hip, torch_cuda, ora, M, N, K):
     swizzled transposed A), forced at small multiples of its 256x256x32 tile:
     every beta mode and alpha != 1 (the A_PART pre-multiply), bit-exact."""
     forms = [v for v, n in enumerate(hip.gemmVariants()) if n.endswith("nn_big")]
-    assert len(forms) >= 9   # (+1 in the diagnostics build)
+    assert len(forms) >= 7   # (+1 in the diagnostics build)
     rng = np.random.default_rng(M + N + K)
     A, B, C0 = operands(rng, 0, 0, M, N, K)
     C0[0, 0] = np.nan  # strict beta = 0 keeps 0*NaN (ntensors.pas:2259)
