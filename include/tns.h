@@ -478,6 +478,9 @@ enum { TNS_OP_GEMM = 0, TNS_OP_IM2COL = 1, TNS_OP_COL2IM = 2, TNS_OP_BIAS = 3,
 int         tns_gemm_variant_count(void);
 /* k-major-A conv tiles of the backward's col = W^T . delta (TNS_OPT_DX_TILE = v) */
 int         tns_conv_dx_tile_count(void);
+/* implicit transposed-convolution forms of the conv backward's state.delta
+ * (TNS_OPT_DX_CONV = v) */
+int         tns_conv_dx_conv_count(void);
 /* implicit-im2col dW tiles of the conv backward (TNS_OPT_DW_TILE = v) */
 int         tns_conv_dw_tile_count(void);
 /* plane-sized implicit-conv tiles (TNS_OPT_CONV_VARIANT = 100 + v) */
@@ -546,6 +549,13 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * tile (conv_tile4.hip, the delta planes as a 1x1 convolution's images) where
  * one applies; -2 = the TN GEMM always; v >= 0 forces form v of
  * tns_conv_dx_tile_count() (tests; same bits in every form).
+ * TNS_OPT_DX_CONV (default -1 = by shape): the conv backward's state.delta of
+ * stride-1, dilation-1 3x3 layers (C a multiple of 64, filters of 32) by one
+ * implicit transposed convolution over the delta planes: each window tap's
+ * filter chain, added to the image pixel in scol2im's (kr, kc) order for the
+ * taps it does not skip — the TN GEMM + col2im sums, no col matrix (uses a
+ * filters*C*9-float tap-major copy of the weights in the context's scratch);
+ * -2 = off; v >= 0 forces form v of tns_conv_dx_conv_count() (same bits).
  * TNS_OPT_DW_TILE (default -1 = by shape): the conv backward's dW product
  * (the reference's per-image sdot-order NT GEMM over the im2col matrix) by
  * a kernel that generates the im2col rows in its staging (dw_tile.hip: no
@@ -567,7 +577,7 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,
-       TNS_OPT_DW_TILE = 9, TNS_OPT_BWD_OVERLAP = 10 };
+       TNS_OPT_DW_TILE = 9, TNS_OPT_BWD_OVERLAP = 10, TNS_OPT_DX_CONV = 11 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

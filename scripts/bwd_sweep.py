@@ -84,6 +84,14 @@ def main():
                     pass
                 finally:
                     hip.setDxTile(-1)
+            for f in [-2] + list(range(hip.convDxConvs())):
+                try:
+                    hip.setDxConv(f)
+                    row[f"dxconv{f}"] = timed()
+                except TnsError:
+                    pass
+                finally:
+                    hip.setDxConv(-1)
             for f in (0, 2):
                 try:
                     hip.setDxFused(f)

@@ -170,16 +170,25 @@ bool conv_dx_fused_fits(int64_t C, int64_t H, int64_t W, int64_t stride, int64_t
          (int64_t)F * C <= 0x7fffffffLL;
 }
 
+// wt[t][f][c] = W[f][c*K2 + t]: the weights tap-major, k-major per tap
+hipError_t launch_transpose_taps(const float* w, float* wt, int64_t F, int64_t C, int64_t K2,
+                                 hipStream_t s) {
+  const int64_t n = F * C * K2;
+  if (n <= 0) return hipSuccess;
+  if (n > 0x7fffffffLL) return hipErrorInvalidValue;
+  const int64_t tb = std::min<int64_t>((n + 255) / 256, 65536);
+  hipLaunchKernelGGL(transpose_taps_kernel, dim3((unsigned)tb), dim3(256), 0, s, w, wt, (int)F,
+                     (int)C, (int)K2);
+  return hipGetLastError();
+}
+
 hipError_t launch_conv_dx_col2im(const float* w, float* wt, const float* delta, float* im,
                                  int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F,
                                  int64_t ks, int64_t pad, int64_t dil, int64_t oh, int64_t ow,
                                  hipStream_t s) {
   if (batch <= 0 || C <= 0 || F <= 0) return hipSuccess;
-  const int64_t K2 = ks * ks, n = F * C * K2;
-  const int64_t tb = std::min<int64_t>((n + 255) / 256, 65536);
-  hipLaunchKernelGGL(transpose_taps_kernel, dim3((unsigned)tb), dim3(256), 0, s, w, wt, (int)F,
-                     (int)C, (int)K2);
-  if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  const int64_t K2 = ks * ks;
+  if (hipError_t e = launch_transpose_taps(w, wt, F, C, K2, s); e != hipSuccess) return e;
   DxArgs a{};
   a.wt = wt; a.delta = delta; a.im = im;
   a.C = (int)C; a.F = (int)F; a.H = (int)H; a.W = (int)W; a.oh = (int)oh; a.ow = (int)ow;

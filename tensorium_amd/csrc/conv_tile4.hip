@@ -79,8 +79,17 @@ struct Frag4 {
 
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
           int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
-          bool BD_ = false, bool BW_ = false, bool AP_ = false, bool AT_ = false>
+          bool BD_ = false, bool BW_ = false, bool AP_ = false, bool AT_ = false,
+          bool DX_ = false>
 struct Geo4 {
+  // DX: the conv backward's state.delta of a stride-1 layer as one implicit
+  // transposed convolution — A = the weights tap-major, wt[t][f][c] (k-major,
+  // TA), B = the delta planes gathered through the flipped window, k = t*F + f:
+  // every tap's ascending-f chain from +0 is added to the image pixel at the
+  // tap's end, in scol2im's (kr, kc) order, skipping the taps it skips — the
+  // reference's TN GEMM + col2im sums, no col matrix (F % BK == 0: a k-tile
+  // never straddles taps)
+  static constexpr bool DX = DX_;
   // AT: B stored by ds_write_addtid_b32 (address M0 + offset + 4 * lane: no
   // address VGPR, 2 cycles a store against 4 for ds_write_b32): the gather
   // lanes are (pixel = lane >> 2, slot component = lane & 3), so a wave's 64
@@ -156,6 +165,7 @@ struct Geo4 {
                 "addtid B stores: register-staged gather, block-placed stores, B images below 96 KB");
   static_assert(!AP || (!IL && !ST && !TA && BM % 64 == 0 && ROWS * BM % (64 * NW) == 0),
                 "A DMA: tile-top issue, whole 64-slot pieces");
+  static_assert(!DX || (TA && !AT && !BD && !BW && !AP), "DX: k-major weights, b32 gather");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
   static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
@@ -202,16 +212,14 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   // (AT: the same lane split, for consecutive-dword stores)
   const int gp = (G::BD || G::AT) ? lane >> 2 : r16, gq = (G::BD || G::AT) ? lane & 3 : q;
   constexpr int NCOL = G::BW ? G::CH : J;
-  unsigned vbase[NCOL], tmask[NCOL];
-#pragma unroll
-  for (int j = 0; j < NCOL; ++j) {
-    int n = n0 + (G::BW ? 64 * j + lane : 16 * j + gp);
+  // output column n (clamped below N): its window's base offset and tap mask
+  auto col_geo = [&](int n, unsigned& vb, unsigned& m) {
     n = n < N ? n : N - 1;  // past N: any valid pixel, never stored
     const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
     const int orow = pix / p.conv_ow, ocol = pix - orow * p.conv_ow;
     const int ir0 = orow * p.conv_sY - p.conv_pH, ic0 = ocol * p.conv_sX - p.conv_pW;
-    vbase[j] = 4u * (unsigned)(img * (int)p.strideB + ir0 * W + ic0);
-    unsigned m = 0;
+    vb = 4u * (unsigned)(img * (int)p.strideB + ir0 * W + ic0);
+    m = 0;
 #pragma unroll
     for (int kr = 0; kr < KS; ++kr)
 #pragma unroll
@@ -219,8 +227,10 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
         m |= (unsigned)(((unsigned)(ir0 + kr * dil) < (unsigned)H) &
                         ((unsigned)(ic0 + kc * dil) < (unsigned)W))
              << (kr * KS + kc);
-    tmask[j] = m;
-  }
+  };
+  unsigned vbase[NCOL], tmask[NCOL];
+#pragma unroll
+  for (int j = 0; j < NCOL; ++j) col_geo(n0 + (G::BW ? 64 * j + lane : 16 * j + gp), vbase[j], tmask[j]);
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.B), 0, p.conv_bytes, 0x00020000);
 
@@ -234,12 +244,30 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   for (int ii = 0; ii < NKS; ++ii) {
     const int sl = G::BW ? wu * KI + ii / 4 : w * KI + ii;
     const int k = 16 * (sl >> 2) + 4 * (G::BW ? ii % 4 : gq) + (sl & 3);
+    if constexpr (G::DX) {  // (k < BK <= F: tap 0, filter k)
+      cc_[ii] = k;
+      kr_[ii] = kc_[ii] = 0;
+      continue;
+    }
     cc_[ii] = k / (KS * KS);
     const int rem = k - cc_[ii] * KS * KS;
     kr_[ii] = rem / KS;
     kc_[ii] = rem - kr_[ii] * KS;
   }
+  // (DX) the tile's first filter and its tap t in the forward window's
+  // terms: reference tap (kr, kc) = t reads the delta pixel at forward tap
+  // (KS-1-kr, KS-1-kc) of a window padded by KS-1-pad
+  const int F_ = G::DX ? K / (KS * KS) : 0;
+  int d_f0 = 0, d_t = 0;
   auto advance = [&]() {  // k += BK
+    if constexpr (G::DX) {
+      d_f0 += BK;
+      if (d_f0 == F_) {
+        d_f0 = 0;
+        ++d_t;
+      }
+      return;
+    }
 #pragma unroll
     for (int ii = 0; ii < NKS; ++ii) {
       if constexpr (KS == 1) {
@@ -278,9 +306,15 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
 #pragma unroll
     for (int ii = 0; ii < KI; ++ii) {
-      const int y = kr_[ii] * dil, z = kc_[ii] * dil;
-      const unsigned x = 4u * (unsigned)(cc_[ii] * HW + y * W + z);
-      const int tap = kr_[ii] * KS + kc_[ii];
+      int y = kr_[ii] * dil, z = kc_[ii] * dil, tap = kr_[ii] * KS + kc_[ii], cc = cc_[ii];
+      if constexpr (G::DX) {
+        const int fr = KS - 1 - d_t / KS, fc = KS - 1 - d_t % KS;  // wave-uniform
+        y = fr;
+        z = fc;
+        tap = fr * KS + fc;
+        cc = d_f0 + cc_[ii];
+      }
+      const unsigned x = 4u * (unsigned)(cc * HW + y * W + z);
 #pragma unroll
       for (int j = 0; j < J; ++j) {
         if constexpr (G::BD) {
@@ -442,6 +476,37 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   floatx4 acc[JW];
 #pragma unroll
   for (int j = 0; j < JW; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // (DX) the image pixels' running sums, state.delta on entry, and the
+  // columns' tap masks; a tap's chains are added at its last k-tile
+  floatx4 rs[G::DX ? JW : 1];
+  unsigned omask[G::DX ? JW : 1];
+  int fl_cnt = 0, fl_tap = 0;
+  const int fl_tiles = G::DX ? F_ / BK : 0;
+  if constexpr (G::DX) {
+    const int64_t row0 = m0 + wm * 16 + 4 * q;
+#pragma unroll
+    for (int j = 0; j < JW; ++j) {
+      const int n = n0 + coff * 16 + 16 * j + r16, nc = n < N ? n : N - 1;
+      unsigned vb;
+      col_geo(n, vb, omask[j]);
+      const int img = nc / p.conv_ohw, pix = nc - img * p.conv_ohw;
+      const float* cp = p.C + (int64_t)img * p.strideC + pix + row0 * p.ldc;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rs[j][e] = cp[e * p.ldc];
+    }
+  }
+  auto flush = [&]() {
+    if (++fl_cnt < fl_tiles) return;
+    fl_cnt = 0;
+    const int bit = KS * KS - 1 - fl_tap++;  // reference tap fl_tap, forward-window bit
+#pragma unroll
+    for (int j = 0; j < JW; ++j) {
+      const bool ok = __builtin_amdgcn_ubfe(omask[j], bit, 1) != 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rs[j][e] = ok ? rs[j][e] + acc[j][e] : rs[j][e];
+      acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
   using Frag = Frag4<JW>;
   auto frag = [&](int stg, int g, Frag& f) {
     const float* ap = a_st(stg) + ((4 * g + q) * BM + wm * 16 + r16) * 4;
@@ -581,6 +646,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           TNS_PH(2);
         }
     }
+    if constexpr (G::DX) flush();
   };
   static_assert(NG % 2 == 0, "f0 holds group 0 at every tile start");
   for (int t = 0; t + 1 < nt; ++t) tile(t, std::true_type{});
@@ -630,6 +696,19 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           }
         }
       }
+    }
+    return;
+  }
+  if constexpr (G::DX) {
+    const int64_t row0 = m0 + wm * 16 + 4 * q;
+#pragma unroll
+    for (int j = 0; j < JW; ++j) {
+      const int n = n0 + coff * 16 + 16 * j + r16;
+      if (n >= N) continue;
+      const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
+      float* cp = p.C + (int64_t)img * p.strideC + pix + row0 * p.ldc;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cp[e * p.ldc] = rs[j][e];
     }
     return;
   }
@@ -796,6 +875,24 @@ const TileInfo4 kTiles4T[] = {
     TNS_CT4T(64, 128, 4, 2, 32, 0, false, 3, 0, 0),   // 10
 };
 constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
+// k-major A, tap-major k (DX): state.delta of stride-1 3x3 layers
+#define TNS_CT4DX(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                          \
+  {BMv, BNv, BKv,                                                                          \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, true, false,  \
+                  false, false, false, true>>,                                             \
+   "conv_tile4_dx<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv         \
+   ",ri" #RIv ",j" #JAv "x" #NAv ">"}
+const TileInfo4 kTiles4DX[] = {
+    TNS_CT4DX(64, 176, 4, 2, 32, 0, false, 3, 6, 1),   // 0: >= 52^2 planes
+    TNS_CT4DX(64, 96, 4, 1, 32, 0, false, 3, 0, 0),    // 1: 26^2
+    TNS_CT4DX(64, 48, 4, 1, 32, 0, false, 3, 0, 0),    // 2: 13^2
+    TNS_CT4DX(128, 96, 8, 1, 64, 1, true, 2, 0, 0),    // 3
+    TNS_CT4DX(64, 64, 4, 2, 32, 0, false, 3, 0, 0),    // 4
+    TNS_CT4DX(128, 48, 8, 1, 64, 1, true, 2, 0, 0),    // 5
+    // (128 x 176: the running sums take it past 256 VGPRs — spills; not built)
+};
+constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
+#undef TNS_CT4DX
 #undef TNS_CT4
 #undef TNS_CT4U
 #undef TNS_CT4D
@@ -875,6 +972,51 @@ hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float
   a.conv_sY = 1; a.conv_sX = 1; a.conv_pH = 0; a.conv_pW = 0;
   a.conv_bytes = (int)(4 * batch * F * hw);
   return kTiles4T[v].fn(a, 1, 1, s);
+}
+
+int conv_tile4_dx3_count() { return kNumTiles4DX; }
+const char* conv_tile4_dx3_name(int v) { return v >= 0 && v < kNumTiles4DX ? kTiles4DX[v].name : ""; }
+
+namespace {
+// the launcher's conditions: stride 1, dilation 1, 3x3, pad <= 2, 32-bit
+// offsets, F a multiple of the form's k-tile, C of its row tile
+bool dx3_fits(int v, int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
+              int64_t pad, int64_t oh, int64_t ow) {
+  if (v < 0 || v >= kNumTiles4DX || ks != 3 || pad < 0 || pad > ks - 1) return false;
+  if (oh != H + 2 * pad - ks + 1 || ow != W + 2 * pad - ks + 1 || oh <= 0 || ow <= 0) return false;
+  if (F % kTiles4DX[v].bk || C % kTiles4DX[v].bm || batch <= 0) return false;
+  return batch * F * oh * ow * 4 <= 0x7fffffffLL && batch * C * H * W <= 0x7fffffffLL &&
+         ks * ks * F * C <= 0x7fffffffLL;
+}
+}  // namespace
+
+// by plane size, so that the grid gives about a block per CU (C = 64 .. 512
+// rows on the YOLOv3 layers: 104^2 / 52^2 planes 64 x 176 tiles, 26^2 64 x 96,
+// 13^2 64 x 48); not yet measured against the TN GEMM + col2im on every class
+int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
+                        int64_t pad) {
+  const int64_t N = batch * H * W, oh = H + 2 * pad - ks + 1, ow = W + 2 * pad - ks + 1;
+  const int v = N >= 16384 ? 0 : (N >= 4096 ? 1 : 2);
+  return dx3_fits(v, batch, C, H, W, F, ks, pad, oh, ow) ? v : -1;
+}
+
+hipError_t launch_conv_tile4_dx3(int v, const float* wt, const float* delta, float* im,
+                                 int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F,
+                                 int64_t ks, int64_t pad, int64_t oh, int64_t ow, hipStream_t s) {
+  if (!dx3_fits(v, batch, C, H, W, F, ks, pad, oh, ow)) return hipErrorInvalidValue;
+  GemmArgs a{};
+  a.M = C; a.N = batch * H * W; a.K = ks * ks * F;
+  a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_ZERO;
+  a.A = wt; a.lda = C; a.strideA = 0;
+  a.B = delta; a.ldb = oh * ow; a.strideB = F * oh * ow;
+  a.C = im; a.ldc = H * W; a.strideC = C * H * W;
+  a.batch = 1; a.epi = EPI_NONE; a.bias = nullptr; a.act = 0;
+  a.conv = 2;
+  // the forward window over the delta planes, padded by ks-1-pad
+  a.conv_H = (int)oh; a.conv_W = (int)ow; a.conv_ow = (int)W; a.conv_ohw = (int)(H * W);
+  a.conv_sY = 1; a.conv_sX = 1; a.conv_pH = (int)(ks - 1 - pad); a.conv_pW = (int)(ks - 1 - pad);
+  a.conv_bytes = (int)(4 * batch * F * oh * ow);
+  return kTiles4DX[v].fn(a, 3, 1, s);
 }
 
 hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStream_t s) {

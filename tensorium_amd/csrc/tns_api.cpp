@@ -34,6 +34,7 @@ static int64_t g_dx_fused = 1;
 // conv backward col = W^T . delta: -1 conv_tile4's k-major-A forms where
 // they apply, -2 the TN GEMM, v >= 0 form v (TNS_OPT_DX_TILE)
 static int64_t g_dx_tile = -1;
+static int64_t g_dx_conv = -1;
 // conv backward dW with the im2col matrix generated in the staging
 // (dw_tile.hip): -1 by measured shape, -2 never, v >= 0 form v (TNS_OPT_DW_TILE)
 static int64_t g_dw_tile = -1;
@@ -592,6 +593,11 @@ int tns_set_option(int32_t opt, int64_t value) {
     case TNS_OPT_DX_TILE:
       if (value >= conv_tile4_ta_count()) return set_error(TNS_ERR_ARG, "no dX tile %lld", (long long)value);
       g_dx_tile = value < -1 ? -2 : value;
+      return TNS_OK;
+    case TNS_OPT_DX_CONV:
+      if (value >= conv_tile4_dx3_count())
+        return set_error(TNS_ERR_ARG, "no dX conv form %lld", (long long)value);
+      g_dx_conv = value < -1 ? -2 : value;
       return TNS_OK;
     default:
       return set_error(TNS_ERR_ARG, "unknown option %d", opt);
@@ -1653,6 +1659,17 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     da.strideA = i_m * i_k; da.strideX = C * H * W; da.strideP = i_m * i_n; da.batch = batch;
     dwv = g_dw_tile >= 0 ? (int)g_dw_tile : dw_tile_pick(da, (int)kSize);
   }
+  // a 1x1/s1/p0 layer's col2im adds each col element to its own pixel once:
+  // the dX product adds into state.delta in its epilogue instead (EPI_ADD,
+  // the same add), no col matrix
+  const bool dx_direct = state_delta && !needs_col && !fused_dx;
+  // state.delta of a stride-1 3x3 layer as one implicit transposed
+  // convolution (conv_tile4 DX forms: each tap's filter chain added to the
+  // pixel in scol2im's order), no col matrix
+  int dxc = -1;
+  if (state_delta && !fused_dx && kSize == 3 && stride == 1 && dilation == 1 && g_dx_conv != -2)
+    dxc = g_dx_conv >= 0 ? (int)g_dx_conv
+                         : conv_tile4_dx3_pick(batch, C, H, W, filters, kSize, padding);
   // dW (im2col + sdot or dw_tile, accumulate) and state.delta (TN + col2im
   // or the fused kernel) read delta and write disjoint outputs: with a
   // state.delta they run concurrently, state.delta's chain on the context's
@@ -1665,22 +1682,19 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // overlap's extra memory, tns.h); if it cannot be had, the sequential
   // schedule shares the one col buffer instead
   float* dx_ws = nullptr;
-  if (overlap && dw_col && !fused_dx && ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) {
+  const bool dx_col = state_delta && !fused_dx && !dx_direct && dxc < 0;  // dX writes a col matrix
+  if (overlap && dw_col && dx_col && ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) {
     tns_clear_error();
     overlap = false;
   }
-  // a 1x1/s1/p0 layer's col2im adds each col element to its own pixel once:
-  // the dX product adds into state.delta in its epilogue instead (EPI_ADD,
-  // the same add), no col matrix
-  const bool dx_direct = state_delta && !needs_col && !fused_dx;
   float* ws = workspace;
-  if (!ws && (dw_col || (state_delta && !fused_dx && !dx_direct && !(overlap && dw_col))))
+  if (!ws && (dw_col || (dx_col && !(overlap && dw_col))))
     if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws)) return r;
   if (!dx_ws) dx_ws = ws;  // col buffer of state.delta's chain
   // scratch of the fused state.delta kernel, sized before any fork (a growth
   // inside the side-stream chain would free a buffer the main stream may use)
   float* wt = nullptr;
-  if (fused_dx)
+  if (fused_dx || dxc >= 0)
     if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
 
   auto run_dw = [&]() -> int {
@@ -1754,6 +1768,16 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     // images in one launch on conv_tile4's k-major-A forms where they apply (a
     // 1x1 "convolution" over the delta planes, the same chains), else the TN
     // GEMM
+    if (dxc >= 0) {
+      OpTimer t(c, TNS_OP_GEMM);
+      if (int r = hip_status(launch_transpose_taps(weights, wt, filters, C, kSize * kSize, c->stream),
+                             "weights transpose launch"))
+        return r;
+      const hipError_t e = launch_conv_tile4_dx3(dxc, wt, delta, state_delta, batch, C, H, W,
+                                                 filters, kSize, padding, g.oh, g.ow, c->stream);
+      if (e != hipErrorInvalidValue) return hip_status(e, "dX conv launch");
+      return set_error(TNS_ERR_UNSUPPORTED, "dX conv form %d does not fit this layer", dxc);
+    }
     bool done = false;
     float* col = dx_direct ? state_delta : dx_ws;
     if (g_dx_tile != -2) {
@@ -1836,6 +1860,7 @@ int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
 int tns_conv_dx_tile_count(void) { return conv_tile4_ta_count(); }
+int tns_conv_dx_conv_count(void) { return conv_tile4_dx3_count(); }
 int tns_conv_dw_tile_count(void) { return dw_tile_count(); }
 int tns_conv_pp_variant_count(void) { return conv_pp_count(); }
 const char* tns_conv_pp_variant_name(int32_t v) { return conv_pp_name(v); }

@@ -148,6 +148,19 @@ hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float
                                 int64_t batch, int64_t C, int64_t ks, int64_t F, int64_t oh,
                                 int64_t ow, hipStream_t s, bool add_into = false);
 // (add_into, 1x1 only: col is state.delta itself, each element C + col)
+// state.delta of a stride-1 3x3 layer as one implicit transposed convolution
+// over the delta planes (conv_tile4.hip DX forms): wt = the weights tap-major
+// (launch_transpose_taps), im = state.delta, added to in scol2im's order;
+// conv_tile4_dx3_pick = -1 where none applies
+int conv_tile4_dx3_count();
+const char* conv_tile4_dx3_name(int v);
+int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
+                        int64_t pad);
+hipError_t launch_conv_tile4_dx3(int v, const float* wt, const float* delta, float* im,
+                                 int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F,
+                                 int64_t ks, int64_t pad, int64_t oh, int64_t ow, hipStream_t s);
+hipError_t launch_transpose_taps(const float* w, float* wt, int64_t F, int64_t C, int64_t K2,
+                                 hipStream_t s);
 // implicit-GEMM convolution on the ping-pong schedule (conv_pp.hip): same
 // operands and limits as conv_tile; conv_pp_pick = -1 where not measured faster
 int conv_pp_count();

@@ -334,6 +334,17 @@ class TNNHip:
         (all bit-identical); process-wide."""
         check(self.lib.tns_set_option(9, int(form)))
 
+    def setDxConv(self, form: int = -1):
+        """Conv backward state.delta of stride-1 3x3 layers: -1 one implicit
+        transposed convolution (each tap's filter chain added to the pixel in
+        scol2im's order, no col matrix) where a form applies, -2 off, v >= 0
+        form v of convDxConvs() (all bit-identical); process-wide."""
+        check(self.lib.tns_set_option(11, int(form)))
+
+    def convDxConvs(self) -> int:
+        """Implicit transposed-convolution forms of the backward's state.delta."""
+        return int(self.lib.tns_conv_dx_conv_count())
+
     def setBwdOverlap(self, on: bool = True):
         """Conv backward: dW and state.delta concurrently on two streams (1)
         or in sequence (0); same results; process-wide."""

@@ -243,6 +243,36 @@ def test_conv_backward_dx_tiles(hip, torch_cuda, ora):
     assert ran >= 2 * nv
 
 
+DX3_CASES = [(2, 64, 13, 64, 3, 1, 1, 9), (2, 128, 11, 96, 3, 1, 1, 1), (3, 64, 9, 128, 3, 1, 0, 9),
+             (1, 128, 20, 128, 3, 1, 1, 4), (2, 64, 6, 64, 3, 1, 2, 9)]
+
+
+def test_conv_backward_dx_conv_forms(hip, torch_cuda, ora):
+    """Every implicit transposed-convolution form of state.delta (conv_tile4
+    DX, TNS_OPT_DX_CONV = v: each tap's filter chain from +0, added to the
+    pixel at the tap's end in scol2im's order, out-of-window taps skipped) —
+    bit-exact against the reference's TN GEMM + scol2im on stride-1 3x3
+    layers with pads 0, 1 and 2 and ragged pixel counts; forms whose tiles do
+    not divide C or F report UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convDxConvs()
+    assert nv >= 3
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setDxConv(v)
+            for i, case in enumerate(DX3_CASES):
+                try:
+                    got, ref = _dx_case(hip, torch_cuda, ora, *case, seed=80 + i)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, case)
+    finally:
+        hip.setDxConv(-1)
+    assert ran >= 2 * nv
+
+
 @pytest.mark.parametrize("idx", [2, 28, 45])
 def test_conv_backward_overlap_matches_sequential(hip, torch_cuda, ora, idx):
     """dW and state.delta on two streams (TNS_OPT_BWD_OVERLAP = 1, the
