@@ -812,7 +812,7 @@ def main():
                        "alpha": 1.0, "beta": 0.0, "gemms_per_gpu_per_step": 1,
                        "parallelism": f"{world} independent replicas, one process per GPU, "
                                       "no data-path collective"},
-            "roofline": {"bound": "mfma", "kernel": "sgemm_nn_pp_kernel (256x256x32, two 4-wave ping-pong groups; form 256x256x32_w2x4_pp_nn_big)",
+            "roofline": {"bound": "mfma", "kernel": "sgemm_nn_w4_kernel (256x256x32, 4 waves of 128x128 at one wave per SIMD, LDS-DMA operands; form 256x256x32_w2x2_dma_nn_big)",
                          "achieved": round(achieved, 3), "peak": PEAK_F32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_F32_TFLOPS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,

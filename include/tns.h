@@ -481,6 +481,8 @@ int         tns_conv_dx_tile_count(void);
 /* implicit transposed-convolution forms of the conv backward's state.delta
  * (TNS_OPT_DX_CONV = v) */
 int         tns_conv_dx_conv_count(void);
+/* residue-sequential dW forms of the conv backward (TNS_OPT_DW_RES = v) */
+int         tns_conv_dw_res_count(void);
 /* implicit-im2col dW tiles of the conv backward (TNS_OPT_DW_TILE = v) */
 int         tns_conv_dw_tile_count(void);
 /* plane-sized implicit-conv tiles (TNS_OPT_CONV_VARIANT = 100 + v) */
@@ -562,6 +564,14 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * col matrix, no im2col pass) where one applies; -2 = im2col + the sdot
  * kernels always; v >= 0 forces form v of tns_conv_dw_tile_count() (same
  * bits in every form).
+ * TNS_OPT_DW_RES (default -1 = by shape): the conv backward's dW product as
+ * the sdot order's eight residue chains run one after another per output
+ * tile over residue-major copies of delta and the im2col matrix, folded in
+ * sdot's order, then added to weight_updates image by image (dw_res.hip; the
+ * copies and the per-group partial planes live in the context's scratch);
+ * by shape on the 3x3 layers with large outputs; -2 = off; v >= 0 forces form
+ * v of tns_conv_dw_res_count() (same bits; ignored while TNS_OPT_DW_TILE
+ * forces a tile).
  * TNS_OPT_BWD_OVERLAP (default 1): the conv backward runs the dW product and
  * the state.delta chain (which read delta and write disjoint outputs)
  * concurrently, the latter on a side stream of the context that the
@@ -577,7 +587,8 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,
-       TNS_OPT_DW_TILE = 9, TNS_OPT_BWD_OVERLAP = 10, TNS_OPT_DX_CONV = 11 };
+       TNS_OPT_DW_TILE = 9, TNS_OPT_BWD_OVERLAP = 10, TNS_OPT_DX_CONV = 11,
+       TNS_OPT_DW_RES = 12 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

@@ -63,6 +63,7 @@ const
   TNS_OPT_DW_TILE = 9;
   TNS_OPT_BWD_OVERLAP = 10;
   TNS_OPT_DX_CONV = 11;
+  TNS_OPT_DW_RES = 12;
 
 type
   PTnsCtx = pointer;
@@ -258,6 +259,7 @@ function tns_hip_op_ms(ctx: PTnsCtx; op: longint): double; cdecl; external libtn
 function tns_gemm_variant_count(): longint; cdecl; external libtns;
 function tns_conv_dx_tile_count(): longint; cdecl; external libtns;
 function tns_conv_dx_conv_count(): longint; cdecl; external libtns;
+function tns_conv_dw_res_count(): longint; cdecl; external libtns;
 function tns_conv_dw_tile_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;

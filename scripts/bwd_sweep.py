@@ -61,19 +61,24 @@ def main():
         row = {"shape": f"{s.c}x{s.h} k{s.size}s{s.stride}->{s.filters}", "default": timed()}
         if "dw" in a.what:
             forms = ([("sdot", f) for f in [0] + [1 + v for v in range(n_chain)] +
-                      [64 + v for v in range(n_rc)]] + [("dwtile", v) for v in range(n_dw)])
+                      [64 + v for v in range(n_rc)]] + [("dwtile", v) for v in range(n_dw)] +
+                     [("dwres", v) for v in range(hip.convDwRes())])
             for kind, f in forms:
                 try:
                     if kind == "sdot":
                         hip.setDwTile(-2)
+                        hip.setDwRes(-2)
                         hip.setSdotForm(f)
-                    else:
+                    elif kind == "dwtile":
                         hip.setDwTile(f)
+                    else:
+                        hip.setDwRes(f)
                     row[f"{kind}{f}"] = timed()
                 except TnsError:
                     pass
                 finally:
                     hip.setDwTile(-1)
+                    hip.setDwRes(-1)
                     hip.setSdotForm(-1)
         if "dx" in a.what:
             for f in [-2] + list(range(n_dx)):

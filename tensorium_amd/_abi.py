@@ -36,6 +36,7 @@ TNS_OPT_DX_TILE = 8
 TNS_OPT_DW_TILE = 9
 TNS_OPT_BWD_OVERLAP = 10
 TNS_OPT_DX_CONV = 11
+TNS_OPT_DW_RES = 12
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 
@@ -106,6 +107,7 @@ PROTOTYPES: dict[str, tuple] = {
     "tns_conv_tile_variant_count": (C.c_int, []),
     "tns_conv_dx_tile_count": (C.c_int, []),
     "tns_conv_dx_conv_count": (C.c_int, []),
+    "tns_conv_dw_res_count": (C.c_int, []),
     "tns_conv_dw_tile_count": (C.c_int, []),
     "tns_conv_tile_variant_name": (C.c_char_p, [C.c_int32]),
     "tns_conv_pp_variant_count": (C.c_int, []),

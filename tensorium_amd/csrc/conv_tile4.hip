@@ -990,14 +990,21 @@ bool dx3_fits(int v, int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, 
 }
 }  // namespace
 
-// by plane size, so that the grid gives about a block per CU (C = 64 .. 512
-// rows on the YOLOv3 layers: 104^2 / 52^2 planes 64 x 176 tiles, 26^2 64 x 96,
-// 13^2 64 x 48); not yet measured against the TN GEMM + col2im on every class
+// by plane size.  Measured per YOLOv3 layer (scripts/bwd_sweep.py --what dx,
+// whole backward calls at batch 8, gpurun_out/bwd_dx.json): ahead of the
+// col = W^T . delta product + col2im on the 104^2 planes (64 x 64 tiles,
+// 0.453 -> 0.413 ms a call) and the 52^2 planes (128 x 96, 0.365 -> 0.336);
+// level on 26^2 (0.339 vs 0.341) and behind on 13^2 (0.44 -> 0.49 and
+// worse: too few pixels per filter tap for the per-tap tiles), so not there
 int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
                         int64_t pad) {
   const int64_t N = batch * H * W, oh = H + 2 * pad - ks + 1, ow = W + 2 * pad - ks + 1;
-  const int v = N >= 16384 ? 0 : (N >= 4096 ? 1 : 2);
-  return dx3_fits(v, batch, C, H, W, F, ks, pad, oh, ow) ? v : -1;
+  int v = -1;
+  if (N >= 50000)
+    v = 4;
+  else if (N >= 16384)
+    v = C % 128 == 0 ? 3 : 0;
+  return v >= 0 && dx3_fits(v, batch, C, H, W, F, ks, pad, oh, ow) ? v : -1;
 }
 
 hipError_t launch_conv_tile4_dx3(int v, const float* wt, const float* delta, float* im,

@@ -1,0 +1,411 @@
+// dw_res.hip — the conv backward's weight gradient in the reference's sdot
+// order, as residue chains run one after another over residue-major operands.
+//
+// TConvolutionalLayer.backward (nConvolutionLayer.pas:571-671) adds, image by
+// image, weight_updates += delta_b . col_b^T (gemm(NoTrans, Trans), beta = 1,
+// 636-640) whose every element is sdot_avx2 over k = output pixel
+// (ntensors.pas:1233-1306, 1957-2005): 8 fma lanes, lane l an ascending chain
+// over k = l (mod 8) from +0 (the masked tail is that chain's last element),
+// then s_l = lane_l + lane_{l+4}, dot = (s0 + s1) + (s2 + s3), sum = ALPHA *
+// dot, C = C + sum — each rounded.
+//
+// The kernels elsewhere keep a tile's eight residue chains side by side (8
+// waves, or 8 accumulator sets per wave), which holds the output tile to 32 x
+// 64 (sgemm_sdot.hip) or 16 x 80 per wave (dw_tile.hip).  Here the operands
+// are first rearranged residue-major, X'[row][r][i] = X[row][r + 8 i] (zero
+// for r + 8 i >= K, rows padded to K4 = 4-aligned K1 = ceil(K / 8)), so the
+// chain of residue r is a plain ascending-k product over a contiguous slice:
+//
+//   * a block owns a BM x BN output tile (2 x 2 waves, 32x32x2 MFMA tiles,
+//     each an ascending fmaf chain, profiles/r01_mfma_order_probe.txt) and
+//     runs R of the 8 residue chains in sequence, in sdot's pairing order
+//     (r, r + 4, ...); a finished chain is folded into registers at once
+//     (s_l = lane_l + lane_{l+4}, then s0 + s1 ...), so only a few
+//     accumulator sets are live and the tile is as large as a plain GEMM's;
+//   * grid.y = residue group (8 / R groups, each its own partial plane),
+//     grid.z = image; a second kernel forms dot from the group planes in
+//     sdot's order and adds ALPHA * dot to weight_updates image by image;
+//   * both operands stream global -> LDS by 16-byte LDS-DMA into row images
+//     [row][32 k] with the 16-byte k-chunks XOR-swizzled by row (as
+//     sgemm_nn_w4.hip's A), two stages, one barrier per k-tile; the last
+//     k-tile of a chain runs only the steps its (zero-padded) k covers.
+//
+// The rearranged delta (rows = filters) and col (rows = (c, kr, kc), or the
+// input planes themselves for a 1x1 / stride-1 layer) are written by one pass
+// each over their sources (reads coalesced, 32-byte write sectors).
+#include <algorithm>
+
+#include "tns_internal.hpp"
+
+namespace tns {
+namespace {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int RBK = 32;  // k per tile
+
+__device__ __forceinline__ void dma16(const float* sbase, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+
+struct ResArgs {
+  const float* A;  // [batch][M][8][K4] (delta')
+  const float* B;  // [batch][N][8][K4] (col')
+  float* P;        // [batch][G][M][N]
+  int M, N, K1, K4, G;
+  int64_t strideA, strideB, strideP;
+};
+
+// R residues per block: the residue of position rho in group g, in sdot's
+// pairing order ((r, r + 4) pairs, pairs ascending)
+template <int R>
+__device__ __forceinline__ int residue_of(int g, int rho) {
+  if constexpr (R == 1) return g;
+  return (R / 2) * g + (rho >> 1) + 4 * (rho & 1);
+}
+
+template <int BM, int BN, int R>
+__global__ __launch_bounds__(256, 2) void dw_res_kernel(
+    ResArgs p) {
+  constexpr int TI = BM / 64, TJ = BN / 64;  // 32x32 tiles of a wave (2 x 2 waves)
+  constexpr int A_T = BM * RBK, STAGE = (BM + BN) * RBK;  // floats
+  constexpr int GA = BM / 8, GT = (BM + BN) / 8, GPW = GT / 4;  // DMA row groups
+  static_assert(TI >= 1 && TJ >= 1 && GT % 4 == 0, "geometry");
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1, l31 = lane & 31, h = lane >> 5;
+  const int tiles_m = p.M / BM;
+  const int m0 = (int)(blockIdx.x % tiles_m) * BM, n0 = (int)(blockIdx.x / tiles_m) * BN;
+  const int g = blockIdx.y;
+  const int64_t img = blockIdx.z;
+  const int64_t ld = 8LL * p.K4;  // row stride, floats
+  const float* A = p.A + img * p.strideA + (int64_t)m0 * ld;
+  const float* B = p.B + img * p.strideB + (int64_t)n0 * ld;
+
+  // DMA: row group q (8 rows x 128 B) -> LDS bytes q * 1024; lane -> row
+  // 8q + (lane >> 3), slot lane & 7 <- k-chunk (lane & 7) ^ ((row >> 1) & 7)
+  // (q even: (arow >> 1) & 7, q odd: that ^ 4)
+  const int arow = lane >> 3;
+  const unsigned voff0 = (unsigned)(arow * ld * 4) + 16u * (unsigned)((lane & 7) ^ ((arow >> 1) & 7));
+  const unsigned voff1 =
+      (unsigned)(arow * ld * 4) + 16u * (unsigned)((lane & 7) ^ (((arow >> 1) & 7) ^ 4));
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem;
+  auto issue = [&](int residue, int kt, int st) {
+    const int64_t koff = (int64_t)residue * p.K4 + (int64_t)kt * RBK;
+    const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
+#pragma unroll
+    for (int u = 0; u < GPW; ++u) {
+      const int q = wid * GPW + u;
+      if (q < GA)
+        dma16(A + (int64_t)(8 * q) * ld + koff, (q & 1) ? voff1 : voff0, sb + (unsigned)(q * 1024));
+      else
+        dma16(B + (int64_t)(8 * (q - GA)) * ld + koff, ((q - GA) & 1) ? voff1 : voff0,
+              sb + (unsigned)(A_T * 4 + (q - GA) * 1024));
+    }
+  };
+
+  // fragments of step s (k = 2s + h): row R at chunk (k >> 2) ^ ((R >> 1) & 7);
+  // the wave's rows start at multiples of 32, so (R >> 1) & 7 = (l31 >> 1) & 7
+  const int swz = (l31 >> 1) & 7;
+  const int a_row = (wm * (BM / 2) + l31) * RBK + h;
+  const int b_row = A_T + (wn * (BN / 2) + l31) * RBK + h;
+  struct Frag {
+    float a[TI], b[TJ];
+  };
+  auto frag = [&](const float* st, int s, Frag& f) {
+    const int ka = 4 * ((s >> 1) ^ swz) + 2 * (s & 1);
+#pragma unroll
+    for (int i = 0; i < TI; ++i) f.a[i] = st[a_row + 32 * RBK * i + ka];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) f.b[j] = st[b_row + 32 * RBK * j + ka];
+  };
+  floatx16 acc[TI][TJ];
+  auto zero = [&](floatx16 (&x)[TI][TJ]) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) x[i][j][e] = 0.0f;
+  };
+  zero(acc);
+  auto mma = [&](const Frag& f) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+  };
+  // one k-tile: 16 steps, or `steps` (even) for a chain's last tile
+  auto compute = [&](const float* st, int steps) {
+    Frag f0, f1;
+    frag(st, 0, f0);
+#pragma unroll
+    for (int s = 0; s < RBK / 2; s += 2) {
+      if (s < steps) {  // (wave-uniform)
+        frag(st, s + 1, f1);
+        mma(f0);
+        if (s + 2 < steps) frag(st, s + 2, f0);
+        mma(f1);
+      }
+    }
+  };
+  // finished chains folded in sdot's order: even positions wait in P, odd
+  // ones give s = P + acc; R = 4: X = s0 (+ s1); R = 8: X = s0 + s1, Y = s2 + s3
+  floatx16 P[TI][TJ], X[TI][TJ], Y[TI][TJ];
+  auto fold = [&](int rho) {
+    if constexpr (R == 1) return;
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        if ((rho & 1) == 0) {
+          P[i][j] = acc[i][j];
+        } else {
+          const floatx16 s = P[i][j] + acc[i][j];
+          if constexpr (R == 2) {
+            P[i][j] = s;
+          } else if constexpr (R == 4) {
+            X[i][j] = rho == 1 ? s : X[i][j] + s;
+          } else {
+            if (rho == 1) X[i][j] = s;
+            else if (rho == 3) X[i][j] = X[i][j] + s;
+            else if (rho == 5) Y[i][j] = s;
+            else Y[i][j] = Y[i][j] + s;
+          }
+        }
+      }
+    zero(acc);
+  };
+
+  const int nt = (p.K1 + RBK - 1) / RBK;
+  const int last_steps = 2 * ((p.K1 - (nt - 1) * RBK + 3) / 4);  // covers the last tile's k, even
+  const int T = R * nt;
+  issue(residue_of<R>(g, 0), 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int rho = 0, kt = 0;
+  for (int t = 0; t < T; ++t) {
+    int nrho = rho, nkt = kt + 1;
+    if (nkt == nt) {
+      nkt = 0;
+      ++nrho;
+    }
+    // the next tile's DMA: its stage was last read in tile t-1, which every
+    // wave finished before the barrier that ended it
+    if (t + 1 < T) issue(residue_of<R>(g, nrho), nkt, (t + 1) & 1);
+    compute(smem + (t & 1) * STAGE, kt == nt - 1 ? last_steps : RBK / 2);
+    if (kt == nt - 1) fold(rho);
+    if (t + 1 < T) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    rho = nrho;
+    kt = nkt;
+  }
+
+  // ---- the group's partial plane -------------------------------------------
+  float* out = p.P + img * p.strideP + (int64_t)g * p.M * p.N;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      floatx16 v;
+      if constexpr (R == 1) v = acc[i][j];
+      else if constexpr (R == 2) v = P[i][j];
+      else if constexpr (R == 4) v = X[i][j];
+      else v = X[i][j] + Y[i][j];  // (s0 + s1) + (s2 + s3)
+      const int col = n0 + wn * (BN / 2) + 32 * j + l31;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = m0 + wm * (BM / 2) + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+        out[(int64_t)row * p.N + col] = v[e];
+      }
+    }
+}
+
+// dot from the G group planes of each image in sdot's order, then
+// C := C + ALPHA * dot image by image (the reference's beta = 1 loop)
+__global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restrict__ C,
+                                                                const float* __restrict__ P,
+                                                                int64_t mn, int G, int64_t strideP,
+                                                                int batch, float alpha) {
+  for (int64_t o = blockIdx.x * 256LL + threadIdx.x; o < mn; o += (int64_t)gridDim.x * 256) {
+    float c = C[o];
+    for (int b = 0; b < batch; ++b) {
+      const float* q = P + b * strideP + o;
+      float dot;
+      if (G == 1)
+        dot = q[0];
+      else if (G == 2)
+        dot = q[0] + q[mn];
+      else if (G == 4)
+        dot = (q[0] + q[mn]) + (q[2 * mn] + q[3 * mn]);
+      else
+        dot = ((q[0] + q[4 * mn]) + (q[mn] + q[5 * mn])) +
+              ((q[2 * mn] + q[6 * mn]) + (q[3 * mn] + q[7 * mn]));
+      c = c + alpha * dot;
+    }
+    C[o] = c;
+  }
+}
+
+// dst[row][p & 7][p >> 3] = p < K ? src[row][p] : 0 for p < 8 K4 (rows of
+// every image; reads coalesced, a wave's writes 8 runs of 32 bytes)
+__global__ __launch_bounds__(256) void res_permute_kernel(const float* __restrict__ src,
+                                                          int64_t srcImg, float* __restrict__ dst,
+                                                          int64_t dstImg, int rows, int K, int K4,
+                                                          int64_t total) {
+  const int64_t rowlen = 8LL * K4;
+  for (int64_t e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t ra = e / rowlen;
+    const int pp = (int)(e - ra * rowlen);
+    const int64_t b = ra / rows, row = ra - b * rows;
+    const float v = pp < K ? src[b * srcImg + row * K + pp] : 0.0f;
+    dst[b * dstImg + row * rowlen + (int64_t)(pp & 7) * K4 + (pp >> 3)] = v;
+  }
+}
+
+// the im2col matrix (rows n = (c, kr, kc), columns = output pixels; the
+// reference's sim2Col, ntensors.pas:11415-11532) written residue-major
+__global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict__ x, int64_t xImg,
+                                                         float* __restrict__ dst, int64_t dstImg,
+                                                         int H, int W, int kH, int kW, int sY,
+                                                         int sX, int pH, int pW, int dY, int dX,
+                                                         int oW, int HWo, int rows, int K4,
+                                                         int64_t total) {
+  const int64_t rowlen = 8LL * K4;
+  const int taps = kH * kW;
+  for (int64_t e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t ra = e / rowlen;
+    const int pp = (int)(e - ra * rowlen);
+    const int64_t b = ra / rows;
+    const int n = (int)(ra - b * rows);
+    float v = 0.0f;
+    if (pp < HWo) {
+      const int c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
+      const int oy = pp / oW, ox = pp - oy * oW;
+      const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
+      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+        v = x[b * xImg + ((int64_t)c * H + iy) * W + ix];
+    }
+    dst[b * dstImg + (int64_t)n * rowlen + (int64_t)(pp & 7) * K4 + (pp >> 3)] = v;
+  }
+}
+
+template <int BM, int BN, int R>
+hipError_t launch_res(const ResArgs& a, int64_t batch, hipStream_t s) {
+  if (a.M % BM || a.N % BN) return hipErrorInvalidValue;
+  const int64_t tiles = (int64_t)(a.M / BM) * (a.N / BN);
+  hipLaunchKernelGGL((dw_res_kernel<BM, BN, R>), dim3((unsigned)tiles, 8 / R, (unsigned)batch),
+                     dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+struct ResForm {
+  int bm, bn, r;
+  hipError_t (*fn)(const ResArgs&, int64_t, hipStream_t);
+  const char* name;
+};
+#define TNS_RES(BMv, BNv, Rv) \
+  {BMv, BNv, Rv, launch_res<BMv, BNv, Rv>, "dw_res<" #BMv "x" #BNv ",r" #Rv ">"}
+// (R = 8 on the 128-wide tiles: four live accumulator sets spill)
+const ResForm kResForms[] = {
+    TNS_RES(128, 128, 2), TNS_RES(128, 128, 4), TNS_RES(64, 128, 2),
+    TNS_RES(64, 128, 4),  TNS_RES(64, 64, 4),   TNS_RES(64, 64, 8),
+};
+#undef TNS_RES
+constexpr int kNumResForms = sizeof(kResForms) / sizeof(kResForms[0]);
+
+int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 16384); }
+
+}  // namespace
+
+int dw_res_count() { return kNumResForms; }
+const char* dw_res_name(int v) { return v >= 0 && v < kNumResForms ? kResForms[v].name : ""; }
+
+int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 3) / 4 * 4; }
+
+// by the block count the residue groups give (about two per CU or more) and
+// the chain length a block runs (R * ceil(K1 / 32) k-tiles); -1: none applies
+int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
+  if (M % 64 || N % 64 || K < 64 || batch < 1) return -1;
+  const int64_t nt = ((K + 7) / 8 + RBK - 1) / RBK;
+  int best = -1;
+  double best_cost = 0;
+  for (int v = 0; v < kNumResForms; ++v) {
+    const ResForm& f = kResForms[v];
+    if (M % f.bm || N % f.bn) continue;
+    const int64_t blocks = (M / f.bm) * (N / f.bn) * (8 / f.r) * batch;
+    const int64_t slots = 512;  // two blocks per CU
+    const int64_t rounds = (blocks + slots - 1) / slots;
+    // time ~ rounds x (a block's k-tiles + ~6 tiles of fill and epilogue),
+    // a block's tile rate scaled by its MFMA work per step
+    const double tile = (double)f.bm * f.bn / (128.0 * 128.0);
+    const double cost = (double)rounds * ((double)f.r * nt + 6.0) * tile +
+                        (f.r < 8 ? 0.02 * (8 / f.r) : 0.0);  // partial-plane traffic
+    if (best < 0 || cost < best_cost) {
+      best = v;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
+int64_t dw_res_groups(int v) { return v >= 0 && v < kNumResForms ? 8 / kResForms[v].r : 0; }
+
+hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
+  if (v < 0 || v >= kNumResForms) return hipErrorInvalidValue;
+  const ResForm& f = kResForms[v];
+  if (d.M % f.bm || d.N % f.bn || d.K <= 0 || d.batch <= 0 || d.batch > 65535)
+    return hipErrorInvalidValue;
+  const int64_t K4 = dw_res_k4(d.K), rowlen = 8 * K4;
+  if (rowlen * 4 * 8 > 0x7fffffffLL || d.M * d.N > 0x7fffffffLL) return hipErrorInvalidValue;
+  // delta' and col' (or the input planes' rearrangement)
+  {
+    const int64_t total = d.batch * d.M * rowlen;
+    hipLaunchKernelGGL(res_permute_kernel, dim3(blocks_for(total)), dim3(256), 0, s, d.delta,
+                       d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, total);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  {
+    const int64_t total = d.batch * d.N * rowlen;
+    if (d.direct) {
+      hipLaunchKernelGGL(res_permute_kernel, dim3(blocks_for(total)), dim3(256), 0, s, d.x,
+                         d.xStride, d.dB, d.N * rowlen, (int)d.N, (int)d.K, (int)K4, total);
+    } else {
+      const ConvGeom& g = d.g;
+      hipLaunchKernelGGL(im2col_res_kernel, dim3(blocks_for(total)), dim3(256), 0, s, d.x,
+                         d.xStride, d.dB, d.N * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW,
+                         (int)g.sY, (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX,
+                         (int)g.ow, (int)d.K, (int)d.N, (int)K4, total);
+    }
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  }
+  ResArgs a{};
+  a.A = d.dA;
+  a.B = d.dB;
+  a.P = d.part;
+  a.M = (int)d.M;
+  a.N = (int)d.N;
+  a.K1 = (int)((d.K + 7) / 8);
+  a.K4 = (int)K4;
+  a.G = 8 / f.r;
+  a.strideA = d.M * rowlen;
+  a.strideB = d.N * rowlen;
+  a.strideP = (int64_t)a.G * d.M * d.N;
+  if (hipError_t e = f.fn(a, d.batch, s); e != hipSuccess) return e;
+  const int64_t mn = d.M * d.N;
+  hipLaunchKernelGGL(dw_res_accumulate_kernel, dim3(blocks_for(mn)), dim3(256), 0, s,
+                     d.weight_updates, d.part, mn, a.G, a.strideP, (int)d.batch, d.alpha);
+  return hipGetLastError();
+}
+
+}  // namespace tns

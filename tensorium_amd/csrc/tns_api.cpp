@@ -35,6 +35,7 @@ static int64_t g_dx_fused = 1;
 // they apply, -2 the TN GEMM, v >= 0 form v (TNS_OPT_DX_TILE)
 static int64_t g_dx_tile = -1;
 static int64_t g_dx_conv = -1;
+static int64_t g_dw_res = -1;
 // conv backward dW with the im2col matrix generated in the staging
 // (dw_tile.hip): -1 by measured shape, -2 never, v >= 0 form v (TNS_OPT_DW_TILE)
 static int64_t g_dw_tile = -1;
@@ -92,7 +93,8 @@ struct tns_ctx {
 namespace {
 
 enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5,
-       SLOT_MLP = 6, SLOT_WT = 7, SLOT_COL_DX = 8, SLOT_WPERM = 9 };
+       SLOT_MLP = 6, SLOT_WT = 7, SLOT_COL_DX = 8, SLOT_WPERM = 9, SLOT_RES_A = 10,
+       SLOT_RES_B = 11 };
 
 int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   if (elems < 1) elems = 1;
@@ -593,6 +595,10 @@ int tns_set_option(int32_t opt, int64_t value) {
     case TNS_OPT_DX_TILE:
       if (value >= conv_tile4_ta_count()) return set_error(TNS_ERR_ARG, "no dX tile %lld", (long long)value);
       g_dx_tile = value < -1 ? -2 : value;
+      return TNS_OK;
+    case TNS_OPT_DW_RES:
+      if (value >= dw_res_count()) return set_error(TNS_ERR_ARG, "no dW res form %lld", (long long)value);
+      g_dw_res = value < -1 ? -2 : value;
       return TNS_OK;
     case TNS_OPT_DX_CONV:
       if (value >= conv_tile4_dx3_count())
@@ -1659,6 +1665,16 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     da.strideA = i_m * i_k; da.strideX = C * H * W; da.strideP = i_m * i_n; da.batch = batch;
     dwv = g_dw_tile >= 0 ? (int)g_dw_tile : dw_tile_pick(da, (int)kSize);
   }
+  // dW as residue chains in sequence over residue-major copies of delta and
+  // the im2col matrix (dw_res.hip): the 3x3 layers with large outputs
+  int dwr = -1;
+  if (g_nt_sdot && g_dw_res != -2 && g_dw_tile < 0 && batch <= 65535 && i_k >= 64) {
+    if (g_dw_res >= 0)
+      dwr = (int)g_dw_res;
+    else if (kSize == 3 && i_m * i_n >= 256 * 1152)
+      dwr = dw_res_pick(i_m, i_n, i_k, batch);
+    if (dwr >= 0) dwv = -1;
+  }
   // a 1x1/s1/p0 layer's col2im adds each col element to its own pixel once:
   // the dX product adds into state.delta in its epilogue instead (EPI_ADD,
   // the same add), no col matrix
@@ -1677,7 +1693,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // nothing changes in either result.  Telemetry times ops one by one, so it
   // keeps them in sequence.
   bool overlap = state_delta && g_bwd_overlap && !c->telemetry && ensure_side_stream(c);
-  const bool dw_col = needs_col && dwv < 0;  // dW reads an im2col matrix
+  const bool dw_col = needs_col && dwv < 0 && dwr < 0;  // dW reads an im2col matrix
   // state.delta's own col buffer when both chains need one at once (the
   // overlap's extra memory, tns.h); if it cannot be had, the sequential
   // schedule shares the one col buffer instead
@@ -1699,6 +1715,24 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
 
   auto run_dw = [&]() -> int {
     const float* col = input;
+    if (dwr >= 0) {
+      DwResArgs d{};
+      d.g = g;
+      d.x = input; d.xStride = C * H * W;
+      d.delta = delta; d.weight_updates = weight_updates;
+      d.M = i_m; d.N = i_n; d.K = i_k; d.batch = batch;
+      d.direct = !needs_col; d.alpha = 1.0f;
+      const int64_t rowlen = 8 * dw_res_k4(i_k);
+      if (int r = ensure_scratch(c, SLOT_RES_A, batch * i_m * rowlen + 32, &d.dA)) return r;
+      if (int r = ensure_scratch(c, SLOT_RES_B, batch * i_n * rowlen + 32, &d.dB)) return r;
+      if (int r = ensure_scratch(c, SLOT_DW, batch * dw_res_groups(dwr) * i_m * i_n, &d.part))
+        return r;
+      OpTimer t(c, TNS_OP_GEMM);
+      const hipError_t e = launch_dw_res(dwr, d, c->stream);
+      if (e == hipErrorInvalidValue)
+        return set_error(TNS_ERR_UNSUPPORTED, "dW res form %d does not fit this layer", dwr);
+      return hip_status(e, "dW res launch");
+    }
     if (dwv >= 0) {
       float* part = nullptr;
       if (int r = ensure_scratch(c, SLOT_DW, batch * i_m * i_n, &part)) return r;
@@ -1861,6 +1895,7 @@ int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
 int tns_conv_dx_tile_count(void) { return conv_tile4_ta_count(); }
 int tns_conv_dx_conv_count(void) { return conv_tile4_dx3_count(); }
+int tns_conv_dw_res_count(void) { return dw_res_count(); }
 int tns_conv_dw_tile_count(void) { return dw_tile_count(); }
 int tns_conv_pp_variant_count(void) { return conv_pp_count(); }
 const char* tns_conv_pp_variant_name(int32_t v) { return conv_pp_name(v); }

@@ -238,6 +238,27 @@ hipError_t launch_im2col(const ConvGeom& g, const float* im, int64_t imStride, f
                          int64_t colStride, int64_t batch, hipStream_t s);
 hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride, float* im,
                          int64_t imStride, int64_t batch, hipStream_t s);
+// the same product as residue chains run in sequence over residue-major
+// copies of delta and the im2col matrix (dw_res.hip), then added to
+// weight_updates image by image; scratch: dA batch*M*8*K4 (+32), dB
+// batch*N*8*K4 (+32), part batch*groups*M*N floats (K4 = dw_res_k4(K))
+struct DwResArgs {
+  ConvGeom g;
+  const float* x;        // input images, xStride floats apart
+  int64_t xStride;
+  const float* delta;    // [batch][M][K]
+  float* weight_updates; // [M][N]
+  float *dA, *dB, *part;
+  int64_t M, N, K, batch;
+  bool direct;           // 1x1 / stride 1 / pad 0: the input planes are the col rows
+  float alpha;
+};
+int dw_res_count();
+const char* dw_res_name(int v);
+int64_t dw_res_k4(int64_t K);
+int64_t dw_res_groups(int v);
+int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch);
+hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s);
 
 // ---- elementwise -------------------------------------------------------------
 bool act_supported(int act);

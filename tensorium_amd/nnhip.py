@@ -341,6 +341,16 @@ class TNNHip:
         form v of convDxConvs() (all bit-identical); process-wide."""
         check(self.lib.tns_set_option(11, int(form)))
 
+    def setDwRes(self, form: int = -1):
+        """Conv backward dW: -1 the residue-sequential kernel where picked
+        by shape, -2 off, v >= 0 form v of convDwRes() (all bit-identical);
+        process-wide."""
+        check(self.lib.tns_set_option(12, int(form)))
+
+    def convDwRes(self) -> int:
+        """Residue-sequential dW forms of the conv backward."""
+        return int(self.lib.tns_conv_dw_res_count())
+
     def convDxConvs(self) -> int:
         """Implicit transposed-convolution forms of the backward's state.delta."""
         return int(self.lib.tns_conv_dx_conv_count())

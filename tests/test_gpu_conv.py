@@ -380,6 +380,41 @@ def test_conv_backward_dw_tiles(hip, torch_cuda, ora):
     assert ran >= 2 * nv
 
 
+DWR_CASES = [(3, 128, 11, 128, 3, 1, 1, 9), (2, 64, 13, 64, 3, 1, 1, 9), (2, 64, 20, 128, 3, 2, 1, 1),
+             (1, 128, 26, 256, 3, 1, 1, 9), (2, 64, 9, 64, 1, 1, 0, 4), (9, 64, 12, 64, 3, 1, 1, 9),
+             (2, 128, 10, 128, 3, 1, 1, 9, 2)]
+
+
+def test_conv_backward_dw_res_forms(hip, torch_cuda, ora):
+    """Every residue-sequential dW form (dw_res.hip, TNS_OPT_DW_RES = v: the
+    sdot order's eight residue chains run one after another per output tile
+    over residue-major copies of delta and the im2col matrix, folded in sdot's
+    order, images added in order): weight_updates (and state.delta, bias)
+    bit-exact against the reference's per-image im2col + beta = 1 sdot loop;
+    k = 100 .. 676 pixels (chains of 13 .. 85 terms: ragged last k-tiles),
+    stride 2, dilation 2, a 1x1 layer (the input planes rearranged), batch 9;
+    forms whose tiles do not divide the layer report UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convDwRes()
+    assert nv >= 4
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setDwRes(v)
+            for i, case in enumerate(DWR_CASES):
+                dil = case[8] if len(case) > 8 else 1
+                try:
+                    got, ref = _dw_case(hip, torch_cuda, ora, *case[:8], seed=90 + i, dil=dil,
+                                        state_delta=i % 2 == 0)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, case)
+    finally:
+        hip.setDwRes(-1)
+    assert ran >= 2 * nv
+
+
 @pytest.mark.parametrize("dil", [1, 2])
 def test_conv_backward_dw_auto_pick_dilated(hip, torch_cuda, ora, dil):
     """The shape dw_tile_pick selects by default (3x3, 256 filters over 128
