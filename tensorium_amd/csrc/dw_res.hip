@@ -257,47 +257,43 @@ __global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restric
   }
 }
 
-// dst[row][p & 7][p >> 3] = p < K ? src[row][p] : 0 for p < 8 K4 (rows of
-// every image; reads coalesced, a wave's writes 8 runs of 32 bytes)
+// dst[row][p & 7][p >> 3] = p < K ? src[row][p] : 0 for p < 8 K4; grid.y =
+// row (b * rows + row, from row0), grid.x = 256-column chunks (reads
+// coalesced, a wave's writes 8 runs of 32 bytes)
 __global__ __launch_bounds__(256) void res_permute_kernel(const float* __restrict__ src,
                                                           int64_t srcImg, float* __restrict__ dst,
                                                           int64_t dstImg, int rows, int K, int K4,
-                                                          int64_t total) {
-  const int64_t rowlen = 8LL * K4;
-  for (int64_t e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t ra = e / rowlen;
-    const int pp = (int)(e - ra * rowlen);
-    const int64_t b = ra / rows, row = ra - b * rows;
-    const float v = pp < K ? src[b * srcImg + row * K + pp] : 0.0f;
-    dst[b * dstImg + row * rowlen + (int64_t)(pp & 7) * K4 + (pp >> 3)] = v;
-  }
+                                                          int row0) {
+  const int ra = row0 + (int)blockIdx.y;
+  const int b = ra / rows, row = ra - b * rows;
+  const int pp = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (pp >= 8 * K4) return;
+  const float v = pp < K ? src[b * srcImg + (int64_t)row * K + pp] : 0.0f;
+  dst[b * dstImg + (int64_t)row * 8 * K4 + (pp & 7) * K4 + (pp >> 3)] = v;
 }
 
 // the im2col matrix (rows n = (c, kr, kc), columns = output pixels; the
-// reference's sim2Col, ntensors.pas:11415-11532) written residue-major
+// reference's sim2Col, ntensors.pas:11415-11532) written residue-major; grid
+// as res_permute_kernel
 __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict__ x, int64_t xImg,
                                                          float* __restrict__ dst, int64_t dstImg,
                                                          int H, int W, int kH, int kW, int sY,
                                                          int sX, int pH, int pW, int dY, int dX,
                                                          int oW, int HWo, int rows, int K4,
-                                                         int64_t total) {
-  const int64_t rowlen = 8LL * K4;
-  const int taps = kH * kW;
-  for (int64_t e = blockIdx.x * 256LL + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t ra = e / rowlen;
-    const int pp = (int)(e - ra * rowlen);
-    const int64_t b = ra / rows;
-    const int n = (int)(ra - b * rows);
-    float v = 0.0f;
-    if (pp < HWo) {
-      const int c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
-      const int oy = pp / oW, ox = pp - oy * oW;
-      const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
-      if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-        v = x[b * xImg + ((int64_t)c * H + iy) * W + ix];
-    }
-    dst[b * dstImg + (int64_t)n * rowlen + (int64_t)(pp & 7) * K4 + (pp >> 3)] = v;
+                                                         int row0) {
+  const int ra = row0 + (int)blockIdx.y;
+  const int b = ra / rows, n = ra - b * rows;
+  const int taps = kH * kW, c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
+  const int pp = (int)blockIdx.x * 256 + (int)threadIdx.x;
+  if (pp >= 8 * K4) return;
+  float v = 0.0f;
+  if (pp < HWo) {
+    const int oy = pp / oW, ox = pp - oy * oW;
+    const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      v = x[b * xImg + ((int64_t)c * H + iy) * W + ix];
   }
+  dst[b * dstImg + (int64_t)n * 8 * K4 + (pp & 7) * K4 + (pp >> 3)] = v;
 }
 
 template <int BM, int BN, int R>
@@ -367,28 +363,39 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   if (d.M % f.bm || d.N % f.bn || d.K <= 0 || d.batch <= 0 || d.batch > 65535)
     return hipErrorInvalidValue;
   const int64_t K4 = dw_res_k4(d.K), rowlen = 8 * K4;
-  if (rowlen * 4 * 8 > 0x7fffffffLL || d.M * d.N > 0x7fffffffLL) return hipErrorInvalidValue;
-  // delta' and col' (or the input planes' rearrangement)
-  {
-    const int64_t total = d.batch * d.M * rowlen;
-    hipLaunchKernelGGL(res_permute_kernel, dim3(blocks_for(total)), dim3(256), 0, s, d.delta,
-                       d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, total);
-    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  }
-  {
-    const int64_t total = d.batch * d.N * rowlen;
-    if (d.direct) {
-      hipLaunchKernelGGL(res_permute_kernel, dim3(blocks_for(total)), dim3(256), 0, s, d.x,
-                         d.xStride, d.dB, d.N * rowlen, (int)d.N, (int)d.K, (int)K4, total);
-    } else {
-      const ConvGeom& g = d.g;
-      hipLaunchKernelGGL(im2col_res_kernel, dim3(blocks_for(total)), dim3(256), 0, s, d.x,
-                         d.xStride, d.dB, d.N * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW,
-                         (int)g.sY, (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX,
-                         (int)g.ow, (int)d.K, (int)d.N, (int)K4, total);
+  if (rowlen * 4 * 8 > 0x7fffffffLL || d.M * d.N > 0x7fffffffLL || d.batch * d.N > 0x7fffffffLL ||
+      d.batch * d.M > 0x7fffffffLL)
+    return hipErrorInvalidValue;
+  // delta' and col' (or the input planes' rearrangement): one block row per
+  // operand row, 65535 rows a launch
+  const unsigned gx = (unsigned)((rowlen + 255) / 256);
+  auto rows_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
+    for (int64_t r0 = 0; r0 < nrows; r0 += 65535) {
+      launch(dim3(gx, (unsigned)std::min<int64_t>(nrows - r0, 65535)), (int)r0);
+      if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
     }
-    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  }
+    return hipSuccess;
+  };
+  if (hipError_t e = rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
+        hipLaunchKernelGGL(res_permute_kernel, gr, dim3(256), 0, s, d.delta, d.M * d.K, d.dA,
+                           d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0);
+      });
+      e != hipSuccess)
+    return e;
+  if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
+        if (d.direct) {
+          hipLaunchKernelGGL(res_permute_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+                             d.N * rowlen, (int)d.N, (int)d.K, (int)K4, r0);
+        } else {
+          const ConvGeom& g = d.g;
+          hipLaunchKernelGGL(im2col_res_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+                             d.N * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
+                             (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX, (int)g.ow,
+                             (int)d.K, (int)d.N, (int)K4, r0);
+        }
+      });
+      e != hipSuccess)
+    return e;
   ResArgs a{};
   a.A = d.dA;
   a.B = d.dB;

@@ -67,11 +67,9 @@ struct tns_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
-  // device scratch (im2col workspace, host-API staging)
-  // 0 col workspace, 1 padded images / host staging, 2-3 host staging,
-  // 4 per-image dW partial sums of the conv backward, 5 per-block results of
-  // the batch-norm reductions
-  static constexpr int kSlots = 10;
+  // device scratch, one buffer per SLOT_* below (im2col workspace, host-API
+  // staging, dW partial sums, batch-norm block results, ...)
+  static constexpr int kSlots = 12;
   float* scratch[kSlots] = {};
   size_t scratch_elems[kSlots] = {};
   // telemetry (TTensorMetrics-style, nopmetrics.pas:25-44)
@@ -94,7 +92,8 @@ namespace {
 
 enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW = 4, SLOT_BN = 5,
        SLOT_MLP = 6, SLOT_WT = 7, SLOT_COL_DX = 8, SLOT_WPERM = 9, SLOT_RES_A = 10,
-       SLOT_RES_B = 11 };
+       SLOT_RES_B = 11, SLOT_COUNT = 12 };
+static_assert(SLOT_COUNT == tns_ctx::kSlots, "one scratch buffer per slot");
 
 int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   if (elems < 1) elems = 1;
