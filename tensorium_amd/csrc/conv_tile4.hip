@@ -842,8 +842,8 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 28 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
-    // shapes: timed slower on every layer class (gpurun_out/
-    // ct_sweep_at.json: 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
+    // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
+    // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
     TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 29 (1)
@@ -991,7 +991,7 @@ bool dx3_fits(int v, int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, 
 }  // namespace
 
 // by plane size.  Measured per YOLOv3 layer (scripts/bwd_sweep.py --what dx,
-// whole backward calls at batch 8, gpurun_out/bwd_dx.json): ahead of the
+// whole backward calls at batch 8, profiles/r04_bwd_dx_forms.json): ahead of the
 // col = W^T . delta product + col2im on the 104^2 planes (64 x 64 tiles,
 // 0.453 -> 0.413 ms a call) and the 52^2 planes (128 x 96, 0.365 -> 0.336);
 // level on 26^2 (0.339 vs 0.341) and behind on 13^2 (0.44 -> 0.49 and

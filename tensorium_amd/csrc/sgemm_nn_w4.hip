@@ -29,7 +29,7 @@
 //     consecutive columns of C: beta loads and epilogue stores move 16 bytes
 //     per lane.
 //
-// Measured at 4096^3 (scripts/nn_big_ab.py, gpurun_out/ab_w4.json): 0.950 ms
+// Measured at 4096^3 (scripts/nn_big_ab.py, profiles/r04_sgemm_w4_ab.json): 0.950 ms
 // vs 0.983 for the ping-pong form on the same box, bit-identical.  (The
 // forms with 32 j + lc columns and 4-byte B reads, with the DMA issued as one
 // burst, measured 0.988-0.992 ms and did not reproduce the ping-pong bits at
