@@ -143,17 +143,20 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
       for (int j = 0; j < TJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
   };
-  // one k-tile: 16 steps, or `steps` (even) for a chain's last tile
+  // steps 0 .. steps-2 of a k-tile (16 steps, or `steps`, even, for a
+  // chain's last tile) from fragments f0 = step 0; leaves the last step's
+  // fragments in f1 (its MFMAs are issued by the caller, after the barrier)
+  Frag f0, f1;
   auto compute = [&](const float* st, int steps) {
-    Frag f0, f1;
-    frag(st, 0, f0);
 #pragma unroll
     for (int s = 0; s < RBK / 2; s += 2) {
       if (s < steps) {  // (wave-uniform)
         frag(st, s + 1, f1);
         mma(f0);
-        if (s + 2 < steps) frag(st, s + 2, f0);
-        mma(f1);
+        if (s + 2 < steps) {
+          frag(st, s + 2, f0);
+          mma(f1);
+        }
       }
     }
   };
@@ -188,27 +191,47 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   const int nt = (p.K1 + RBK - 1) / RBK;
   const int last_steps = 2 * ((p.K1 - (nt - 1) * RBK + 3) / 4);  // covers the last tile's k, even
   const int T = R * nt;
-  issue(residue_of<R>(g, 0), 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int rho = 0, kt = 0;
-  for (int t = 0; t < T; ++t) {
-    int nrho = rho, nkt = kt + 1;
-    if (nkt == nt) {
-      nkt = 0;
-      ++nrho;
-    }
-    // the next tile's DMA: its stage was last read in tile t-1, which every
-    // wave finished before the barrier that ended it
-    if (t + 1 < T) issue(residue_of<R>(g, nrho), nkt, (t + 1) & 1);
-    compute(smem + (t & 1) * STAGE, kt == nt - 1 ? last_steps : RBK / 2);
-    if (kt == nt - 1) fold(rho);
-    if (t + 1 < T) {
+  // the barrier that publishes tile t+1 sits before tile t's last step: tile
+  // t+1's first fragments are read under that step's MFMAs, and the DMA of
+  // tile t+2 (into tile t's stage, every read of which completed before the
+  // barrier) goes out a whole tile ahead of its use
+  auto tile_of = [&](int t, int& res, int& kt) {
+    res = residue_of<R>(g, t / nt);
+    kt = t - (t / nt) * nt;
+  };
+  {
+    int r0, k0;
+    tile_of(0, r0, k0);
+    issue(r0, k0, 0);
+    if (T > 1) {
+      tile_of(1, r0, k0);
+      issue(r0, k0, 1);
+      // (this wave's DMA of tile 0 landed: the newer GPW may stay in flight)
+      if constexpr (GPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (GPW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (GPW == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
     }
-    rho = nrho;
-    kt = nkt;
+    __syncthreads();
+    frag(smem, 0, f0);
+  }
+  for (int t = 0; t < T; ++t) {
+    const int kt = t - (t / nt) * nt;
+    compute(smem + (t & 1) * STAGE, kt == nt - 1 ? last_steps : RBK / 2);
+    if (t + 1 < T) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1
+      __syncthreads();  // every wave's; every read of tile t complete
+      if (t + 2 < T) {
+        int r2, k2;
+        tile_of(t + 2, r2, k2);
+        issue(r2, k2, t & 1);
+      }
+      frag(smem + ((t + 1) & 1) * STAGE, 0, f0);
+    }
+    mma(f1);  // the tile's last step
+    if (kt == nt - 1) fold(t / nt);
   }
 
   // ---- the group's partial plane -------------------------------------------
@@ -257,24 +280,43 @@ __global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restric
   }
 }
 
-// dst[row][p & 7][p >> 3] = p < K ? src[row][p] : 0 for p < 8 K4; grid.y =
-// row (b * rows + row, from row0), grid.x = 256-column chunks (reads
-// coalesced, a wave's writes 8 runs of 32 bytes)
+// Residue-major rearrangement: dst[row][r][i] = v(row, r + 8 i) for i < K4,
+// v(row, p) = 0 for p >= K.  A block takes 2048 consecutive p of one row
+// (grid.y = row from row0, grid.x = chunk): coalesced reads into LDS, then
+// each residue's 256 consecutive i written as one run (LDS row stride 264:
+// both phases conflict-free).
+constexpr int RCH = 2048, RLD = 264;
+
+template <class Src>
+__device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, int K4) {
+  __shared__ float t[8 * RLD];
+  const int tid = threadIdx.x, base = (int)blockIdx.x * RCH;
+#pragma unroll
+  for (int j = 0; j < RCH / 256; ++j) {
+    const int pl = tid + 256 * j;
+    t[(pl & 7) * RLD + (pl >> 3)] = src(base + pl);
+  }
+  __syncthreads();
+  const int i = (int)blockIdx.x * (RCH / 8) + tid;
+  if (i < K4) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) drow[(int64_t)r * K4 + i] = t[r * RLD + tid];
+  }
+}
+
 __global__ __launch_bounds__(256) void res_permute_kernel(const float* __restrict__ src,
                                                           int64_t srcImg, float* __restrict__ dst,
                                                           int64_t dstImg, int rows, int K, int K4,
                                                           int row0) {
   const int ra = row0 + (int)blockIdx.y;
   const int b = ra / rows, row = ra - b * rows;
-  const int pp = (int)blockIdx.x * 256 + (int)threadIdx.x;
-  if (pp >= 8 * K4) return;
-  const float v = pp < K ? src[b * srcImg + (int64_t)row * K + pp] : 0.0f;
-  dst[b * dstImg + (int64_t)row * 8 * K4 + (pp & 7) * K4 + (pp >> 3)] = v;
+  const float* s = src + b * srcImg + (int64_t)row * K;
+  res_chunk([&](int pp) { return pp < K ? s[pp] : 0.0f; },
+            dst + b * dstImg + (int64_t)row * 8 * K4, K4);
 }
 
 // the im2col matrix (rows n = (c, kr, kc), columns = output pixels; the
-// reference's sim2Col, ntensors.pas:11415-11532) written residue-major; grid
-// as res_permute_kernel
+// reference's sim2Col, ntensors.pas:11415-11532) written residue-major
 __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict__ x, int64_t xImg,
                                                          float* __restrict__ dst, int64_t dstImg,
                                                          int H, int W, int kH, int kW, int sY,
@@ -284,16 +326,15 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
   const int ra = row0 + (int)blockIdx.y;
   const int b = ra / rows, n = ra - b * rows;
   const int taps = kH * kW, c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
-  const int pp = (int)blockIdx.x * 256 + (int)threadIdx.x;
-  if (pp >= 8 * K4) return;
-  float v = 0.0f;
-  if (pp < HWo) {
-    const int oy = pp / oW, ox = pp - oy * oW;
-    const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
-    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-      v = x[b * xImg + ((int64_t)c * H + iy) * W + ix];
-  }
-  dst[b * dstImg + (int64_t)n * 8 * K4 + (pp & 7) * K4 + (pp >> 3)] = v;
+  const float* xc = x + b * xImg + (int64_t)c * H * W;
+  res_chunk(
+      [&](int pp) {
+        if (pp >= HWo) return 0.0f;
+        const int oy = pp / oW, ox = pp - oy * oW;
+        const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
+        return ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? xc[iy * W + ix] : 0.0f;
+      },
+      dst + b * dstImg + (int64_t)n * 8 * K4, K4);
 }
 
 template <int BM, int BN, int R>
@@ -368,7 +409,7 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
     return hipErrorInvalidValue;
   // delta' and col' (or the input planes' rearrangement): one block row per
   // operand row, 65535 rows a launch
-  const unsigned gx = (unsigned)((rowlen + 255) / 256);
+  const unsigned gx = (unsigned)((rowlen + RCH - 1) / RCH);
   auto rows_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
     for (int64_t r0 = 0; r0 < nrows; r0 += 65535) {
       launch(dim3(gx, (unsigned)std::min<int64_t>(nrows - r0, 65535)), (int)r0);
