@@ -21,12 +21,14 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
+# the 4096^3 launches: 256 blocks of 256 (w4) or 512 (pp / big) threads
+MAIN_GRIDS = {65536, 131072}
 
 
 def rows(path, kernel_pred):
     out = {}
     for r in csv.DictReader(open(path)):
-        if not kernel_pred(r["Kernel_Name"]) or int(r["Grid_Size"]) != 131072:
+        if not kernel_pred(r["Kernel_Name"]) or int(r["Grid_Size"]) not in MAIN_GRIDS:
             continue
         out.setdefault(r["Counter_Name"], []).append(
             (float(r["Counter_Value"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
@@ -43,16 +45,16 @@ def main():
     stats = src / "trace" / "trace_kernel_stats.csv"
     shutil.copy(stats, prof / f"{tag}_kernel_stats.csv")
 
-    # the dominant kernel: the 4096^3 launches (grid of 256 blocks x 512 thr)
+    # the dominant kernel: the 4096^3 launches (grid of 256 blocks)
     def is_main(name):
         return ("sgemm_nn_big_kernel" in name and "Geo<256, 256, 2, 4" in name) or \
-            "sgemm_nn_pp_kernel" in name or \
+            "sgemm_nn_pp_kernel" in name or "sgemm_nn_w4_kernel" in name or \
             ("sgemm_mfma_kernel" in name and "Shape<256, 256, 32, 2, 4" in name)
 
     # kernel duration from the trace (same command, not profiled with PMC)
     durs, names = [], set()
     for r in csv.DictReader(open(src / "trace" / "trace_kernel_trace.csv")):
-        if is_main(r["Kernel_Name"]) and int(r["Grid_Size_X"]) == 131072:
+        if is_main(r["Kernel_Name"]) and int(r["Grid_Size_X"]) in MAIN_GRIDS:
             durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
             names.add(r["Kernel_Name"])
     fetch = rows(src / "fetch" / "fetch_counter_collection.csv", is_main).get("FETCH_SIZE", [])
