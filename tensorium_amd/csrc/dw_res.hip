@@ -281,60 +281,73 @@ __global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restric
 }
 
 // Residue-major rearrangement: dst[row][r][i] = v(row, r + 8 i) for i < K4,
-// v(row, p) = 0 for p >= K.  A block takes 2048 consecutive p of one row
-// (grid.y = row from row0, grid.x = chunk): coalesced reads into LDS, then
-// each residue's 256 consecutive i written as one run (LDS row stride 264:
-// both phases conflict-free).
+// v(row, p) = 0 for p >= K.  A block takes CH consecutive p of one row (CH a
+// multiple of 256 up to 2048, by row length; grid.y = row from row0, grid.x =
+// chunk): coalesced reads into LDS, then each residue's CH/8 consecutive i
+// written as one run (LDS row stride 264: both phases conflict-free).
 constexpr int RCH = 2048, RLD = 264;
 
 template <class Src>
-__device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, int K4) {
+__device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, int K4, int ch) {
   __shared__ float t[8 * RLD];
-  const int tid = threadIdx.x, base = (int)blockIdx.x * RCH;
-#pragma unroll
-  for (int j = 0; j < RCH / 256; ++j) {
+  const int tid = threadIdx.x, base = (int)blockIdx.x * ch;
+  for (int j = 0; j < ch / 256; ++j) {
     const int pl = tid + 256 * j;
-    t[(pl & 7) * RLD + (pl >> 3)] = src(base + pl);
+    t[(pl & 7) * RLD + (pl >> 3)] = src(base + pl, j);
   }
   __syncthreads();
-  const int i = (int)blockIdx.x * (RCH / 8) + tid;
-  if (i < K4) {
+  if (tid < ch / 8) {
+    const int i = (int)blockIdx.x * (ch / 8) + tid;
+    if (i < K4) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) drow[(int64_t)r * K4 + i] = t[r * RLD + tid];
+      for (int r = 0; r < 8; ++r) drow[(int64_t)r * K4 + i] = t[r * RLD + tid];
+    }
   }
 }
 
 __global__ __launch_bounds__(256) void res_permute_kernel(const float* __restrict__ src,
                                                           int64_t srcImg, float* __restrict__ dst,
                                                           int64_t dstImg, int rows, int K, int K4,
-                                                          int row0) {
+                                                          int row0, int ch) {
   const int ra = row0 + (int)blockIdx.y;
   const int b = ra / rows, row = ra - b * rows;
   const float* s = src + b * srcImg + (int64_t)row * K;
-  res_chunk([&](int pp) { return pp < K ? s[pp] : 0.0f; },
-            dst + b * dstImg + (int64_t)row * 8 * K4, K4);
+  res_chunk([&](int pp, int) { return pp < K ? s[pp] : 0.0f; },
+            dst + b * dstImg + (int64_t)row * 8 * K4, K4, ch);
 }
 
 // the im2col matrix (rows n = (c, kr, kc), columns = output pixels; the
-// reference's sim2Col, ntensors.pas:11415-11532) written residue-major
+// reference's sim2Col, ntensors.pas:11415-11532) written residue-major; a
+// thread's pixels p0 + 256 j walk the output plane by a fixed (rows,
+// columns) step, one division per thread
 __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict__ x, int64_t xImg,
                                                          float* __restrict__ dst, int64_t dstImg,
                                                          int H, int W, int kH, int kW, int sY,
                                                          int sX, int pH, int pW, int dY, int dX,
                                                          int oW, int HWo, int rows, int K4,
-                                                         int row0) {
+                                                         int row0, int ch) {
   const int ra = row0 + (int)blockIdx.y;
   const int b = ra / rows, n = ra - b * rows;
   const int taps = kH * kW, c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
   const float* xc = x + b * xImg + (int64_t)c * H * W;
+  const int p0 = (int)blockIdx.x * ch + (int)threadIdx.x;
+  const int dy = 256 / oW, dx = 256 - dy * oW;
+  int oy = p0 / oW, ox = p0 - oy * oW;
   res_chunk(
-      [&](int pp) {
+      [&](int pp, int j) {
+        if (j > 0) {  // pp = p0 + 256 j: advance the pixel by 256
+          ox += dx;
+          oy += dy;
+          if (ox >= oW) {
+            ox -= oW;
+            ++oy;
+          }
+        }
         if (pp >= HWo) return 0.0f;
-        const int oy = pp / oW, ox = pp - oy * oW;
         const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
         return ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? xc[iy * W + ix] : 0.0f;
       },
-      dst + b * dstImg + (int64_t)n * 8 * K4, K4);
+      dst + b * dstImg + (int64_t)n * 8 * K4, K4, ch);
 }
 
 template <int BM, int BN, int R>
@@ -370,30 +383,19 @@ const char* dw_res_name(int v) { return v >= 0 && v < kNumResForms ? kResForms[v
 
 int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 3) / 4 * 4; }
 
-// by the block count the residue groups give (about two per CU or more) and
-// the chain length a block runs (R * ceil(K1 / 32) k-tiles); -1: none applies
+// Measured per YOLOv3 layer (scripts/dw_res_prof.py under a kernel trace,
+// batch 8; profiles/r04_dw_res_forms/, r04_dw_res_forms_v2.jsonl): the 64 x
+// 128 tile with residue
+// pairs (4 group planes) on the 52^2 and 26^2 output planes (52^2 3x3: 133 us
+// against 184 for dw_tile; 26^2: 140 against 171 for the residue-register
+// kernel), the 64 x 64 tile with all 8 residues (one plane: the group
+// partials of a 1024 x 4608 output would cost more to add than the product
+// saves) on the 13^2 planes (198 against 241); on larger planes the
+// rearranged im2col copy costs more than the product saves.  -1: none.
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
-  if (M % 64 || N % 64 || K < 64 || batch < 1) return -1;
-  const int64_t nt = ((K + 7) / 8 + RBK - 1) / RBK;
-  int best = -1;
-  double best_cost = 0;
-  for (int v = 0; v < kNumResForms; ++v) {
-    const ResForm& f = kResForms[v];
-    if (M % f.bm || N % f.bn) continue;
-    const int64_t blocks = (M / f.bm) * (N / f.bn) * (8 / f.r) * batch;
-    const int64_t slots = 512;  // two blocks per CU
-    const int64_t rounds = (blocks + slots - 1) / slots;
-    // time ~ rounds x (a block's k-tiles + ~6 tiles of fill and epilogue),
-    // a block's tile rate scaled by its MFMA work per step
-    const double tile = (double)f.bm * f.bn / (128.0 * 128.0);
-    const double cost = (double)rounds * ((double)f.r * nt + 6.0) * tile +
-                        (f.r < 8 ? 0.02 * (8 / f.r) : 0.0);  // partial-plane traffic
-    if (best < 0 || cost < best_cost) {
-      best = v;
-      best_cost = cost;
-    }
-  }
-  return best;
+  if (M % 64 || batch < 1 || K < 64 || K > 3000) return -1;
+  if (K <= 256) return N % 64 == 0 ? 5 : -1;
+  return N % 128 == 0 ? 2 : -1;
 }
 
 int64_t dw_res_groups(int v) { return v >= 0 && v < kNumResForms ? 8 / kResForms[v].r : 0; }
@@ -409,7 +411,8 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
     return hipErrorInvalidValue;
   // delta' and col' (or the input planes' rearrangement): one block row per
   // operand row, 65535 rows a launch
-  const unsigned gx = (unsigned)((rowlen + RCH - 1) / RCH);
+  const int ch = (int)std::min<int64_t>(RCH, (rowlen + 255) / 256 * 256);
+  const unsigned gx = (unsigned)((rowlen + ch - 1) / ch);
   auto rows_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
     for (int64_t r0 = 0; r0 < nrows; r0 += 65535) {
       launch(dim3(gx, (unsigned)std::min<int64_t>(nrows - r0, 65535)), (int)r0);
@@ -419,20 +422,20 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   };
   if (hipError_t e = rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
         hipLaunchKernelGGL(res_permute_kernel, gr, dim3(256), 0, s, d.delta, d.M * d.K, d.dA,
-                           d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0);
+                           d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0, ch);
       });
       e != hipSuccess)
     return e;
   if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
         if (d.direct) {
           hipLaunchKernelGGL(res_permute_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                             d.N * rowlen, (int)d.N, (int)d.K, (int)K4, r0);
+                             d.N * rowlen, (int)d.N, (int)d.K, (int)K4, r0, ch);
         } else {
           const ConvGeom& g = d.g;
           hipLaunchKernelGGL(im2col_res_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
                              d.N * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
                              (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX, (int)g.ow,
-                             (int)d.K, (int)d.N, (int)K4, r0);
+                             (int)d.K, (int)d.N, (int)K4, r0, ch);
         }
       });
       e != hipSuccess)
