@@ -384,14 +384,14 @@ const char* dw_res_name(int v) { return v >= 0 && v < kNumResForms ? kResForms[v
 int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 3) / 4 * 4; }
 
 // Measured per YOLOv3 layer (scripts/dw_res_prof.py under a kernel trace,
-// batch 8; profiles/r04_dw_res_forms/, r04_dw_res_forms_v2.jsonl): the 64 x
-// 128 tile with residue
-// pairs (4 group planes) on the 52^2 and 26^2 output planes (52^2 3x3: 133 us
-// against 184 for dw_tile; 26^2: 140 against 171 for the residue-register
-// kernel), the 64 x 64 tile with all 8 residues (one plane: the group
-// partials of a 1024 x 4608 output would cost more to add than the product
-// saves) on the 13^2 planes (198 against 241); on larger planes the
-// rearranged im2col copy costs more than the product saves.  -1: none.
+// batch 8; profiles/r04_dw_res_forms/, r04_dw_res_forms_v2.jsonl): the
+// 64 x 128 tile with residue pairs (4 group planes) on the 52^2 and 26^2
+// output planes (52^2 3x3: 133 us against 184 for dw_tile; 26^2: 140
+// against 171 for the residue-register kernel), the 64 x 64 tile with all 8
+// residues (one plane: the group partials of a 1024 x 4608 output would cost
+// more to add than the product saves) on the 13^2 planes (198 against 241);
+// on larger planes the rearranged im2col copy costs more than the product
+// saves.  -1: none.
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
   if (M % 64 || batch < 1 || K < 64 || K > 3000) return -1;
   if (K <= 256) return N % 64 == 0 ? 5 : -1;
