@@ -246,6 +246,7 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
       else if constexpr (R == 4) v = X[i][j];
       else v = X[i][j] + Y[i][j];  // (s0 + s1) + (s2 + s3)
       const int col = n0 + wn * (BN / 2) + 32 * j + l31;
+      if (col >= p.N) continue;  // (padded col rows)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int row = m0 + wm * (BM / 2) + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
@@ -352,8 +353,8 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
 
 template <int BM, int BN, int R>
 hipError_t launch_res(const ResArgs& a, int64_t batch, hipStream_t s) {
-  if (a.M % BM || a.N % BN) return hipErrorInvalidValue;
-  const int64_t tiles = (int64_t)(a.M / BM) * (a.N / BN);
+  if (a.M % BM) return hipErrorInvalidValue;
+  const int64_t tiles = (int64_t)(a.M / BM) * ((a.N + BN - 1) / BN);
   hipLaunchKernelGGL((dw_res_kernel<BM, BN, R>), dim3((unsigned)tiles, 8 / R, (unsigned)batch),
                      dim3(256), 0, s, a);
   return hipGetLastError();
@@ -370,6 +371,8 @@ struct ResForm {
 const ResForm kResForms[] = {
     TNS_RES(128, 128, 2), TNS_RES(128, 128, 4), TNS_RES(64, 128, 2),
     TNS_RES(64, 128, 4),  TNS_RES(64, 64, 4),   TNS_RES(64, 64, 8),
+    // one residue a block (8 group planes): the long-k layers with few outputs
+    TNS_RES(64, 64, 1),   TNS_RES(128, 64, 1),  TNS_RES(128, 128, 1),
 };
 #undef TNS_RES
 constexpr int kNumResForms = sizeof(kResForms) / sizeof(kResForms[0]);
@@ -394,8 +397,16 @@ int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 3) / 4 * 4; }
 // saves.  -1: none.
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
   if (M % 64 || batch < 1 || K < 64 || K > 3000) return -1;
-  if (K <= 256) return N % 64 == 0 ? 5 : -1;
-  return N % 128 == 0 ? 2 : -1;
+  if (K <= 256) return 5;
+  return N % 128 == 0 ? 2 : 4;
+}
+
+// col' rows per image: N rounded up to the form's column tile (the rows past
+// N are never written; they only feed output columns that are not stored)
+int64_t dw_res_b_rows(int v, int64_t N) {
+  if (v < 0 || v >= kNumResForms) return N;
+  const int64_t bn = kResForms[v].bn;
+  return (N + bn - 1) / bn * bn;
 }
 
 int64_t dw_res_groups(int v) { return v >= 0 && v < kNumResForms ? 8 / kResForms[v].r : 0; }
@@ -403,9 +414,10 @@ int64_t dw_res_groups(int v) { return v >= 0 && v < kNumResForms ? 8 / kResForms
 hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   if (v < 0 || v >= kNumResForms) return hipErrorInvalidValue;
   const ResForm& f = kResForms[v];
-  if (d.M % f.bm || d.N % f.bn || d.K <= 0 || d.batch <= 0 || d.batch > 65535)
+  if (d.M % f.bm || d.N <= 0 || d.K <= 0 || d.batch <= 0 || d.batch > 65535)
     return hipErrorInvalidValue;
   const int64_t K4 = dw_res_k4(d.K), rowlen = 8 * K4;
+  const int64_t npad = dw_res_b_rows(v, d.N);  // col' rows per image (tile multiple)
   if (rowlen * 4 * 8 > 0x7fffffffLL || d.M * d.N > 0x7fffffffLL || d.batch * d.N > 0x7fffffffLL ||
       d.batch * d.M > 0x7fffffffLL)
     return hipErrorInvalidValue;
@@ -429,11 +441,11 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
         if (d.direct) {
           hipLaunchKernelGGL(res_permute_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                             d.N * rowlen, (int)d.N, (int)d.K, (int)K4, r0, ch);
+                             npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0, ch);
         } else {
           const ConvGeom& g = d.g;
           hipLaunchKernelGGL(im2col_res_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                             d.N * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
+                             npad * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
                              (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX, (int)g.ow,
                              (int)d.K, (int)d.N, (int)K4, r0, ch);
         }
@@ -450,7 +462,7 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   a.K4 = (int)K4;
   a.G = 8 / f.r;
   a.strideA = d.M * rowlen;
-  a.strideB = d.N * rowlen;
+  a.strideB = npad * rowlen;
   a.strideP = (int64_t)a.G * d.M * d.N;
   if (hipError_t e = f.fn(a, d.batch, s); e != hipSuccess) return e;
   const int64_t mn = d.M * d.N;

@@ -1670,7 +1670,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   if (g_nt_sdot && g_dw_res != -2 && g_dw_tile < 0 && batch <= 65535 && i_k >= 64) {
     if (g_dw_res >= 0)
       dwr = (int)g_dw_res;
-    else if (kSize == 3 && i_m * i_n >= 256 * 1152)
+    else if (kSize == 3)
       dwr = dw_res_pick(i_m, i_n, i_k, batch);
     if (dwr >= 0) dwv = -1;
   }
@@ -1723,7 +1723,8 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
       d.direct = !needs_col; d.alpha = 1.0f;
       const int64_t rowlen = 8 * dw_res_k4(i_k);
       if (int r = ensure_scratch(c, SLOT_RES_A, batch * i_m * rowlen + 32, &d.dA)) return r;
-      if (int r = ensure_scratch(c, SLOT_RES_B, batch * i_n * rowlen + 32, &d.dB)) return r;
+      if (int r = ensure_scratch(c, SLOT_RES_B, batch * dw_res_b_rows(dwr, i_n) * rowlen + 32, &d.dB))
+        return r;
       if (int r = ensure_scratch(c, SLOT_DW, batch * dw_res_groups(dwr) * i_m * i_n, &d.part))
         return r;
       OpTimer t(c, TNS_OP_GEMM);

@@ -241,7 +241,8 @@ hipError_t launch_col2im(const ConvGeom& g, const float* col, int64_t colStride,
 // the same product as residue chains run in sequence over residue-major
 // copies of delta and the im2col matrix (dw_res.hip), then added to
 // weight_updates image by image; scratch: dA batch*M*8*K4 (+32), dB
-// batch*N*8*K4 (+32), part batch*groups*M*N floats (K4 = dw_res_k4(K))
+// batch*dw_res_b_rows(v, N)*8*K4 (+32), part batch*groups*M*N floats
+// (K4 = dw_res_k4(K))
 struct DwResArgs {
   ConvGeom g;
   const float* x;        // input images, xStride floats apart
@@ -257,6 +258,7 @@ int dw_res_count();
 const char* dw_res_name(int v);
 int64_t dw_res_k4(int64_t K);
 int64_t dw_res_groups(int v);
+int64_t dw_res_b_rows(int v, int64_t N);  // dB rows per image
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch);
 hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s);
 
