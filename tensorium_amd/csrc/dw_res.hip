@@ -282,23 +282,28 @@ __global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restric
 }
 
 // Residue-major rearrangement: dst[row][r][i] = v(row, r + 8 i) for i < K4,
-// v(row, p) = 0 for p >= K.  A block takes CH consecutive p of one row (CH a
-// multiple of 256 up to 2048, by row length; grid.y = row from row0, grid.x =
-// chunk): coalesced reads into LDS, then each residue's CH/8 consecutive i
-// written as one run (LDS row stride 264: both phases conflict-free).
+// v(row, p) = 0 for p >= K.  A block takes CH consecutive p of one row (CH =
+// 256 .. 2048 by row length; grid.y = row from row0, grid.x = chunk): all of
+// a thread's reads issued together, coalesced, into LDS, then each residue's
+// CH/8 consecutive i written as one run (LDS row stride 264: both phases
+// conflict-free).
 constexpr int RCH = 2048, RLD = 264;
 
-template <class Src>
-__device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, int K4, int ch) {
+template <int CH, class Src>
+__device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, int K4) {
   __shared__ float t[8 * RLD];
-  const int tid = threadIdx.x, base = (int)blockIdx.x * ch;
-  for (int j = 0; j < ch / 256; ++j) {
+  const int tid = threadIdx.x, base = (int)blockIdx.x * CH;
+  float v[CH / 256];  // all of a thread's loads in flight before the stores
+#pragma unroll
+  for (int j = 0; j < CH / 256; ++j) v[j] = src(base + tid + 256 * j, j);
+#pragma unroll
+  for (int j = 0; j < CH / 256; ++j) {
     const int pl = tid + 256 * j;
-    t[(pl & 7) * RLD + (pl >> 3)] = src(base + pl, j);
+    t[(pl & 7) * RLD + (pl >> 3)] = v[j];
   }
   __syncthreads();
-  if (tid < ch / 8) {
-    const int i = (int)blockIdx.x * (ch / 8) + tid;
+  if (tid < CH / 8) {
+    const int i = (int)blockIdx.x * (CH / 8) + tid;
     if (i < K4) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) drow[(int64_t)r * K4 + i] = t[r * RLD + tid];
@@ -306,35 +311,37 @@ __device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, i
   }
 }
 
+template <int CH>
 __global__ __launch_bounds__(256) void res_permute_kernel(const float* __restrict__ src,
                                                           int64_t srcImg, float* __restrict__ dst,
                                                           int64_t dstImg, int rows, int K, int K4,
-                                                          int row0, int ch) {
+                                                          int row0) {
   const int ra = row0 + (int)blockIdx.y;
   const int b = ra / rows, row = ra - b * rows;
   const float* s = src + b * srcImg + (int64_t)row * K;
-  res_chunk([&](int pp, int) { return pp < K ? s[pp] : 0.0f; },
-            dst + b * dstImg + (int64_t)row * 8 * K4, K4, ch);
+  res_chunk<CH>([&](int pp, int) { return pp < K ? s[pp] : 0.0f; },
+                dst + b * dstImg + (int64_t)row * 8 * K4, K4);
 }
 
 // the im2col matrix (rows n = (c, kr, kc), columns = output pixels; the
 // reference's sim2Col, ntensors.pas:11415-11532) written residue-major; a
 // thread's pixels p0 + 256 j walk the output plane by a fixed (rows,
 // columns) step, one division per thread
+template <int CH>
 __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict__ x, int64_t xImg,
                                                          float* __restrict__ dst, int64_t dstImg,
                                                          int H, int W, int kH, int kW, int sY,
                                                          int sX, int pH, int pW, int dY, int dX,
                                                          int oW, int HWo, int rows, int K4,
-                                                         int row0, int ch) {
+                                                         int row0) {
   const int ra = row0 + (int)blockIdx.y;
   const int b = ra / rows, n = ra - b * rows;
   const int taps = kH * kW, c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
   const float* xc = x + b * xImg + (int64_t)c * H * W;
-  const int p0 = (int)blockIdx.x * ch + (int)threadIdx.x;
+  const int p0 = (int)blockIdx.x * CH + (int)threadIdx.x;
   const int dy = 256 / oW, dx = 256 - dy * oW;
   int oy = p0 / oW, ox = p0 - oy * oW;
-  res_chunk(
+  res_chunk<CH>(
       [&](int pp, int j) {
         if (j > 0) {  // pp = p0 + 256 j: advance the pixel by 256
           ox += dx;
@@ -348,7 +355,7 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
         const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
         return ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? xc[iy * W + ix] : 0.0f;
       },
-      dst + b * dstImg + (int64_t)n * 8 * K4, K4, ch);
+      dst + b * dstImg + (int64_t)n * 8 * K4, K4);
 }
 
 template <int BM, int BN, int R>
@@ -423,8 +430,15 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
     return hipErrorInvalidValue;
   // delta' and col' (or the input planes' rearrangement): one block row per
   // operand row, 65535 rows a launch
-  const int ch = (int)std::min<int64_t>(RCH, (rowlen + 255) / 256 * 256);
-  const unsigned gx = (unsigned)((rowlen + ch - 1) / ch);
+  // chunk of a block: the largest of 2048 .. 256 that pads the row by at
+  // most an eighth
+  int chs = 256;
+  for (int c = RCH; c > 256; c /= 2)
+    if (((rowlen + c - 1) / c * c - rowlen) * 8 <= rowlen) {
+      chs = c;
+      break;
+    }
+  const unsigned gx = (unsigned)((rowlen + chs - 1) / chs);
   auto rows_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
     for (int64_t r0 = 0; r0 < nrows; r0 += 65535) {
       launch(dim3(gx, (unsigned)std::min<int64_t>(nrows - r0, 65535)), (int)r0);
@@ -432,23 +446,36 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
     }
     return hipSuccess;
   };
+  auto by_chunk = [&](auto&& f) {
+    switch (chs) {
+      case 256: f(std::integral_constant<int, 256>{}); break;
+      case 512: f(std::integral_constant<int, 512>{}); break;
+      case 1024: f(std::integral_constant<int, 1024>{}); break;
+      default: f(std::integral_constant<int, 2048>{}); break;
+    }
+  };
   if (hipError_t e = rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
-        hipLaunchKernelGGL(res_permute_kernel, gr, dim3(256), 0, s, d.delta, d.M * d.K, d.dA,
-                           d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0, ch);
+        by_chunk([&](auto c) {
+          hipLaunchKernelGGL((res_permute_kernel<decltype(c)::value>), gr, dim3(256), 0, s, d.delta,
+                             d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0);
+        });
       });
       e != hipSuccess)
     return e;
   if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
-        if (d.direct) {
-          hipLaunchKernelGGL(res_permute_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                             npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0, ch);
-        } else {
-          const ConvGeom& g = d.g;
-          hipLaunchKernelGGL(im2col_res_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                             npad * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
-                             (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX, (int)g.ow,
-                             (int)d.K, (int)d.N, (int)K4, r0, ch);
-        }
+        by_chunk([&](auto c) {
+          constexpr int C = decltype(c)::value;
+          if (d.direct) {
+            hipLaunchKernelGGL((res_permute_kernel<C>), gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+                               npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0);
+          } else {
+            const ConvGeom& g = d.g;
+            hipLaunchKernelGGL((im2col_res_kernel<C>), gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+                               npad * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
+                               (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX,
+                               (int)g.ow, (int)d.K, (int)d.N, (int)K4, r0);
+          }
+        });
       });
       e != hipSuccess)
     return e;
