@@ -443,7 +443,7 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
 // dependent add), and the staging waves keep one tile of loads in flight in
 // registers while the chain wave works, three LDS buffers deep (a tile is
 // loaded at the top of tile t, written after the barrier that ends t, read
-// in tile t+2; round 4: loaded a tile earlier still, two register sets).  The loop bodies of the two roles are separate, so no staging
+// in tile t+2).  The loop bodies of the two roles are separate, so no staging
 // register is carried around a loop edge (hipcc copies such registers right
 // after their loads and waits there).  Same terms, same order: bit-identical.
 template <int MODE>
@@ -480,12 +480,8 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
       // float4 staging where the block is 16-byte aligned (nb8 % 8 == 0: a
       // float4 is wholly inside or outside the full 8-blocks)
       const bool v4 = ((reinterpret_cast<uintptr_t>(pa) | (TWO ? reinterpret_cast<uintptr_t>(pb) : 0)) & 15) == 0;
-      // two register sets: tile j is loaded into set j & 1 at the top of
-      // tile j-3 and stored after the barrier that ends tile j-2 (two tiles
-      // of load latency covered); the loop is unrolled by two so each set
-      // keeps one role per body
-      float ra0[E], rb0[TWO ? E : 1], ra1[E], rb1[TWO ? E : 1];
-      auto load = [&](int t, float (&ra)[E], float (&rb)[TWO ? E : 1]) {
+      float ra[E], rb[TWO ? E : 1];
+      auto load = [&](int t) {
         const int64_t t0 = (int64_t)t * TILE;
         if (v4) {
 #pragma unroll
@@ -510,7 +506,7 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
             }
         }
       };
-      auto store = [&](int buf, const float (&ra)[E], const float (&rb)[TWO ? E : 1]) {
+      auto store = [&](int buf) {
 #pragma unroll
         for (int u = 0; u < E / 4; ++u)
 #pragma unroll
@@ -532,25 +528,16 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
             }
           }
       };
-      if (ntile > 0) {
-        load(0, ra0, rb0);
-        store(0, ra0, rb0);
+      for (int t = 0; t < 2 && t < ntile; ++t) {
+        load(t);
+        store(t);
       }
-      if (ntile > 1) {
-        load(1, ra1, rb1);
-        store(1, ra1, rb1);
-      }
-      if (ntile > 2) load(2, ra0, rb0);
       __syncthreads();
-      auto body = [&](int t, float (&la)[E], float (&lb)[TWO ? E : 1], const float (&sa)[E],
-                      const float (&sb)[TWO ? E : 1]) {
-        if (t + 3 < ntile) load(t + 3, la, lb);
+      for (int t = 0; t < ntile; ++t) {
+        const bool more = t + 2 < ntile;
+        if (more) load(t + 2);
         __syncthreads();
-        if (t + 2 < ntile) store((t + 2) % NBUF, sa, sb);
-      };
-      for (int t = 0; t < ntile; t += 2) {
-        body(t, ra1, rb1, ra0, rb0);
-        if (t + 1 < ntile) body(t + 1, ra0, rb0, ra1, rb1);
+        if (more) store((t + 2) % NBUF);
       }
     } else {
       __syncthreads();
