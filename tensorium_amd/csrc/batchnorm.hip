@@ -549,44 +549,91 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
           const float* row =
               ((MODE == CH_VDELTA && grp == 1) ? &V[buf][0] : &U[buf][0]) + l * LDT;
           const float* rowb = TWO ? &V[buf][0] + l * LDT : row;
-          float va[16], wa[16], vb[16], wb[16], vc[16], wc[16];
-          auto rd = [&](int q, float (&v)[16], float (&w)[16]) {
-#pragma unroll
-            for (int z = 0; z < 16; z += 4) {
-              const float4 x4 = *reinterpret_cast<const float4*>(row + q + z);
-              v[z] = x4.x; v[z + 1] = x4.y; v[z + 2] = x4.z; v[z + 3] = x4.w;
-              if constexpr (MODE == CH_DOT) {
-                const float4 y4 = *reinterpret_cast<const float4*>(rowb + q + z);
-                w[z] = y4.x; w[z + 1] = y4.y; w[z + 2] = y4.z; w[z + 3] = y4.w;
-              }
+          // groups of 16 terms read by ds_read_b128 issued as inline asm
+          // with explicit counted waits: hipcc's own waits at the loop
+          // header assumed only the newest reads pending and drained the
+          // whole ring there (lgkmcnt 3..0 before the first group's adds),
+          // exposing the LDS latency once per loop trip.  One stream: a
+          // ring of three register sets, a group's reads issued right after
+          // the group two ahead of it is consumed (lgkmcnt(8) = the two
+          // newer sets in flight); two streams (CH_DOT): two sets of 8 reads
+          // (lgkmcnt(8) = the newer set).  The waits take the sets as
+          // operands, so no add moves above them and no register of a set
+          // in flight is reused.  Rows have 72 floats of slack: the ring may
+          // read up to 47 terms past cnt.
+          typedef float f4 __attribute__((ext_vector_type(4)));
+          const unsigned ra_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)row;
+          const unsigned rb_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)rowb;
+          auto rd = [&](int q, f4 (&v)[4], f4 (&w)[4]) {
+            const unsigned a = ra_lds + 4u * (unsigned)q;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(v[0]) : "v"(a));
+            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(v[1]) : "v"(a));
+            asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(v[2]) : "v"(a));
+            asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(v[3]) : "v"(a));
+            if constexpr (MODE == CH_DOT) {
+              const unsigned b = rb_lds + 4u * (unsigned)q;
+              asm volatile("ds_read_b128 %0, %1" : "=v"(w[0]) : "v"(b));
+              asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(w[1]) : "v"(b));
+              asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(w[2]) : "v"(b));
+              asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(w[3]) : "v"(b));
             }
           };
-          auto add16 = [&](const float (&v)[16], const float (&w)[16]) {
+          // wait until at most 8 reads are pending, with the set as operand
+          auto wait8 = [&](f4 (&v)[4], f4 (&w)[4]) {
+            if constexpr (MODE == CH_DOT)
+              asm volatile("s_waitcnt lgkmcnt(8)"
+                           : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(w[0]),
+                             "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+            else
+              asm volatile("s_waitcnt lgkmcnt(8)"
+                           : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+          };
+          auto add16 = [&](const f4 (&v)[4], const f4 (&w)[4]) {
 #pragma unroll
             for (int z = 0; z < 16; ++z) {
-              if constexpr (MODE == CH_DOT) acc = fmaf(v[z], w[z], acc);
-              else acc = acc + v[z];
+              if constexpr (MODE == CH_DOT) acc = fmaf(v[z >> 2][z & 3], w[z >> 2][z & 3], acc);
+              else acc = acc + v[z >> 2][z & 3];
             }
           };
-          // groups of 16 terms in a ring of three register sets: a group's
-          // reads go out right after the group two ahead of it is consumed
-          // (32 dependent adds of cover for the LDS latency; with two sets
-          // only 16, and the chain waited on its reads at every group)
-          // (unconditional: they may read the row's slack past cnt)
-          const int full = cnt - cnt % 48;
-          rd(0, va, wa);
-          rd(16, vb, wb);
-          rd(32, vc, wc);
-          for (int q = 0; q < full; q += 48) {
-            add16(va, wa);
-            __builtin_amdgcn_sched_barrier(0);
-            rd(q + 48, va, wa);
-            add16(vb, wb);
-            __builtin_amdgcn_sched_barrier(0);
-            rd(q + 64, vb, wb);
-            add16(vc, wc);
-            __builtin_amdgcn_sched_barrier(0);
-            rd(q + 80, vc, wc);
+          f4 va[4], wa[4], vb[4], wb[4], vc[4], wc[4];
+          int full;
+          if constexpr (MODE == CH_DOT) {
+            full = cnt - cnt % 32;
+            rd(0, va, wa);
+            rd(16, vb, wb);
+            for (int q = 0; q < full; q += 32) {
+              wait8(va, wa);
+              add16(va, wa);
+              rd(q + 32, va, wa);
+              wait8(vb, wb);
+              add16(vb, wb);
+              rd(q + 48, vb, wb);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(va[3]), "+v"(wa[0]),
+                           "+v"(wa[1]), "+v"(wa[2]), "+v"(wa[3]), "+v"(vb[0]), "+v"(vb[1]),
+                           "+v"(vb[2]), "+v"(vb[3]), "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]),
+                           "+v"(wb[3]));
+          } else {
+            full = cnt - cnt % 48;
+            rd(0, va, wa);
+            rd(16, vb, wb);
+            rd(32, vc, wc);
+            for (int q = 0; q < full; q += 48) {
+              wait8(va, wa);
+              add16(va, wa);
+              rd(q + 48, va, wa);
+              wait8(vb, wb);
+              add16(vb, wb);
+              rd(q + 64, vb, wb);
+              wait8(vc, wc);
+              add16(vc, wc);
+              rd(q + 80, vc, wc);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(va[3]), "+v"(vb[0]),
+                           "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]), "+v"(vc[0]), "+v"(vc[1]),
+                           "+v"(vc[2]), "+v"(vc[3]));
           }
           for (int q = full; q < cnt; ++q) {
             if constexpr (MODE == CH_DOT) acc = fmaf(row[q], rowb[q], acc);
