@@ -11,4 +11,5 @@ for L in 11 28 45 9 3 1 4 6; do
   (cd /tmp && timeout -k 10 150 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/dwres3/l$L -o l$L --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/dw_res_prof.py --layer $L > $GRAFT_REPO_ROOT/gpurun_out/dwres3/l$L.json 2> $GRAFT_REPO_ROOT/gpurun_out/dwres3/l$L.err) || exit $?
   echo "layer $L ok"; cat gpurun_out/dwres3/l$L.json
 done
+bash scripts/gpu_r4_b5.sh || exit $?
 bash scripts/gpu_r4_evidence.sh
