@@ -890,6 +890,9 @@ const TileInfo4 kTiles4DX[] = {
     TNS_CT4DX(64, 64, 4, 2, 32, 0, false, 3, 0, 0),    // 4
     TNS_CT4DX(128, 48, 8, 1, 64, 1, true, 2, 0, 0),    // 5
     // (128 x 176: the running sums take it past 256 VGPRs — spills; not built)
+    // eight waves over the narrower row counts of the 26^2 / 13^2 planes
+    TNS_CT4DX(64, 96, 4, 2, 32, 0, false, 3, 0, 0),    // 6
+    TNS_CT4DX(32, 96, 2, 4, 64, 1, true, 2, 1, 2),     // 7
 };
 constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4DX
