@@ -12,4 +12,6 @@ for L in 11 28 45 9 3 1 4 6; do
   echo "layer $L ok"; cat gpurun_out/dwres3/l$L.json
 done
 bash scripts/gpu_r4_b5.sh || exit $?
+timeout -k 10 300 python scripts/bwd_sweep.py --what dx --layers 28,45,11,6,43 > gpurun_out/bwd_dx2.json 2> gpurun_out/bwd_dx2.err || exit $?
+echo "bwd dx sweep ok"
 bash scripts/gpu_r4_evidence.sh
