@@ -13,7 +13,7 @@
 // waves, or 8 accumulator sets per wave), which holds the output tile to 32 x
 // 64 (sgemm_sdot.hip) or 16 x 80 per wave (dw_tile.hip).  Here the operands
 // are first rearranged residue-major, X'[row][r][i] = X[row][r + 8 i] (zero
-// for r + 8 i >= K, rows padded to K4 = 4-aligned K1 = ceil(K / 8)), so the
+// for r + 8 i >= K, rows padded to K4 = 32-aligned K1 = ceil(K / 8)), so the
 // chain of residue r is a plain ascending-k product over a contiguous slice:
 //
 //   * a block owns a BM x BN output tile (2 x 2 waves, 32x32x2 MFMA tiles,
@@ -41,6 +41,7 @@ namespace tns {
 namespace {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 constexpr int RBK = 32;  // k per tile
 
@@ -111,20 +112,25 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
     }
   };
 
-  // fragments of step s (k = 2s + h): row R at chunk (k >> 2) ^ ((R >> 1) & 7);
-  // the wave's rows start at multiples of 32, so (R >> 1) & 7 = (l31 >> 1) & 7
+  // fragments of step group q (steps 4q .. 4q+3, k = 8q + h + 2j): the
+  // rearranged rows hold each 32-k block as [h][q][j] (kperm), so a lane's
+  // four steps are one 16-byte chunk, 4h + q, at slot (4h + q) ^ ((R >> 1) &
+  // 7); the wave's rows start at multiples of 32, so (R >> 1) & 7 =
+  // (l31 >> 1) & 7
   const int swz = (l31 >> 1) & 7;
-  const int a_row = (wm * (BM / 2) + l31) * RBK + h;
-  const int b_row = A_T + (wn * (BN / 2) + l31) * RBK + h;
+  const int a_row = (wm * (BM / 2) + l31) * RBK;
+  const int b_row = A_T + (wn * (BN / 2) + l31) * RBK;
   struct Frag {
-    float a[TI], b[TJ];
+    floatx4 a[TI], b[TJ];
   };
-  auto frag = [&](const float* st, int s, Frag& f) {
-    const int ka = 4 * ((s >> 1) ^ swz) + 2 * (s & 1);
+  auto frag = [&](const float* st, int q, Frag& f) {
+    const int ka = 4 * ((4 * h + q) ^ swz);
 #pragma unroll
-    for (int i = 0; i < TI; ++i) f.a[i] = st[a_row + 32 * RBK * i + ka];
+    for (int i = 0; i < TI; ++i)
+      f.a[i] = *reinterpret_cast<const floatx4*>(st + a_row + 32 * RBK * i + ka);
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) f.b[j] = st[b_row + 32 * RBK * j + ka];
+    for (int j = 0; j < TJ; ++j)
+      f.b[j] = *reinterpret_cast<const floatx4*>(st + b_row + 32 * RBK * j + ka);
   };
   floatx16 acc[TI][TJ];
   auto zero = [&](floatx16 (&x)[TI][TJ]) {
@@ -138,23 +144,27 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   zero(acc);
   auto mma = [&](const Frag& f) {
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+    for (int st = 0; st < 4; ++st)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][st], f.b[j][st], acc[i][j], 0,
+                                                           0, 0);
   };
-  // steps 0 .. steps-2 of a k-tile (16 steps, or `steps`, even, for a
-  // chain's last tile) from fragments f0 = step 0; leaves the last step's
-  // fragments in f1 (its MFMAs are issued by the caller, after the barrier)
+  // step groups 0 .. groups-2 of a k-tile (4 groups, or `groups`, 2 or 4,
+  // for a chain's last tile: the rest is zero padding) from fragments f0 =
+  // group 0; leaves the last group's fragments in f1 (its MFMAs are issued
+  // by the caller, after the barrier)
   Frag f0, f1;
-  auto compute = [&](const float* st, int steps) {
+  auto compute = [&](const float* st, int groups) {
 #pragma unroll
-    for (int s = 0; s < RBK / 2; s += 2) {
-      if (s < steps) {  // (wave-uniform)
-        frag(st, s + 1, f1);
+    for (int q = 0; q < RBK / 8; q += 2) {
+      if (q < groups) {  // (wave-uniform)
+        frag(st, q + 1, f1);
         mma(f0);
-        if (s + 2 < steps) {
-          frag(st, s + 2, f0);
+        if (q + 2 < groups) {
+          frag(st, q + 2, f0);
           mma(f1);
         }
       }
@@ -189,7 +199,9 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   };
 
   const int nt = (p.K1 + RBK - 1) / RBK;
-  const int last_steps = 2 * ((p.K1 - (nt - 1) * RBK + 3) / 4);  // covers the last tile's k, even
+  // the last tile's step groups: its k rounded up to 16 (K4 is a multiple of
+  // 32, so the rest of the tile is zero)
+  const int last_groups = 2 * ((p.K1 - (nt - 1) * RBK + 15) / 16);
   const int T = R * nt;
   // the barrier that publishes tile t+1 sits before tile t's last step: tile
   // t+1's first fragments are read under that step's MFMAs, and the DMA of
@@ -219,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   }
   for (int t = 0; t < T; ++t) {
     const int kt = t - (t / nt) * nt;
-    compute(smem + (t & 1) * STAGE, kt == nt - 1 ? last_steps : RBK / 2);
+    compute(smem + (t & 1) * STAGE, kt == nt - 1 ? last_groups : RBK / 8);
     if (t + 1 < T) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1
       __syncthreads();  // every wave's; every read of tile t complete
@@ -289,6 +301,13 @@ __global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restric
 // conflict-free).
 constexpr int RCH = 2048, RLD = 264;
 
+// position of chain element i in its row: each 32-element block stored as
+// [h][q][j] for element 32 b + 8 q + h + 2 j (the kernel's step groups)
+__device__ __forceinline__ int kperm(int i) {
+  const int k = i & 31;
+  return (i & ~31) | ((k & 1) << 4) | ((k >> 3) << 2) | ((k >> 1) & 3);
+}
+
 template <int CH, class Src>
 __device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, int K4) {
   __shared__ float t[8 * RLD];
@@ -306,7 +325,7 @@ __device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, i
     const int i = (int)blockIdx.x * (CH / 8) + tid;
     if (i < K4) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) drow[(int64_t)r * K4 + i] = t[r * RLD + tid];
+      for (int r = 0; r < 8; ++r) drow[(int64_t)r * K4 + kperm(i)] = t[r * RLD + tid];
     }
   }
 }
@@ -391,7 +410,7 @@ int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 16384
 int dw_res_count() { return kNumResForms; }
 const char* dw_res_name(int v) { return v >= 0 && v < kNumResForms ? kResForms[v].name : ""; }
 
-int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 3) / 4 * 4; }
+int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 31) / 32 * 32; }
 
 // Measured per YOLOv3 layer (scripts/dw_res_prof.py under a kernel trace,
 // batch 8; profiles/r04_dw_res_forms/, r04_dw_res_forms_v2.jsonl): the
