@@ -33,7 +33,7 @@ def per_dispatch(d: Path):
             k = r["Kernel_Name"]
             if "tns::" not in k:
                 continue
-            short = k.split("(")[0][:160]
+            short = k.replace("(anonymous namespace)::", "").split("(")[0][:160]
             did = f.parent.name + ":" + r["Dispatch_Id"]
             names[did] = short
             per[(did, r["Counter_Name"])] += float(r["Counter_Value"])

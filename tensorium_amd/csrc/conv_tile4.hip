@@ -889,10 +889,10 @@ const TileInfo4 kTiles4DX[] = {
     TNS_CT4DX(128, 96, 8, 1, 64, 1, true, 2, 0, 0),    // 3
     TNS_CT4DX(64, 64, 4, 2, 32, 0, false, 3, 0, 0),    // 4
     TNS_CT4DX(128, 48, 8, 1, 64, 1, true, 2, 0, 0),    // 5
-    // (128 x 176: the running sums take it past 256 VGPRs — spills; not built)
-    // eight waves over the narrower row counts of the 26^2 / 13^2 planes
-    TNS_CT4DX(64, 96, 4, 2, 32, 0, false, 3, 0, 0),    // 6
-    TNS_CT4DX(32, 96, 2, 4, 64, 1, true, 2, 1, 2),     // 7
+    // (128 x 176: the running sums take it past 256 VGPRs — spills; not built.
+    // Eight-wave 64 x 96 / 32 x 96 forms for the 26^2 / 13^2 row counts
+    // measured no better than these: 26^2 0.369 / 0.378 ms a call against
+    // 0.352 for TN + col2im, 13^2 0.446 / 0.453 against 0.424 — not built)
 };
 constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4DX
@@ -996,7 +996,8 @@ bool dx3_fits(int v, int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, 
 // by plane size.  Measured per YOLOv3 layer (scripts/bwd_sweep.py --what dx,
 // whole backward calls at batch 8, profiles/r04_bwd_dx_forms.json): ahead of the
 // col = W^T . delta product + col2im on the 104^2 planes (64 x 64 tiles,
-// 0.453 -> 0.413 ms a call) and the 52^2 planes (128 x 96, 0.365 -> 0.336);
+// 0.453 -> 0.413 ms a call) and the 52^2 planes (64 x 176: 0.385 -> 0.368 in
+// a second sweep, profiles/r04_bwd_dx_forms2.json);
 // level on 26^2 (0.339 vs 0.341) and behind on 13^2 (0.44 -> 0.49 and
 // worse: too few pixels per filter tap for the per-tap tiles), so not there
 int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
@@ -1006,7 +1007,7 @@ int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t 
   if (N >= 50000)
     v = 4;
   else if (N >= 16384)
-    v = C % 128 == 0 ? 3 : 0;
+    v = 0;
   return v >= 0 && dx3_fits(v, batch, C, H, W, F, ks, pad, oh, ow) ? v : -1;
 }
 

@@ -413,22 +413,21 @@ const char* dw_res_name(int v) { return v >= 0 && v < kNumResForms ? kResForms[v
 int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 31) / 32 * 32; }
 
 // Measured per YOLOv3 layer (scripts/dw_res_prof.py under a kernel trace,
-// batch 8; profiles/r04_dw_res_forms/, r04_dw_res_forms_v2.jsonl): the
-// 64 x 128 tile with residue pairs (4 group planes) on the 52^2 and 26^2
-// output planes (52^2 3x3: 133 us against 184 for dw_tile; 26^2: 140
-// against 171 for the residue-register kernel), the 64 x 64 tile with all 8
-// residues (one plane: the group partials of a 1024 x 4608 output would cost
-// more to add than the product saves) on the 13^2 planes (198 against 241);
-// on larger planes the rearranged im2col copy costs more than the product
-// saves.  -1: none.
+// batch 8; profiles/r04_dw_res_forms*): one residue a block (8 group planes,
+// no fold) runs the fastest product wherever the planes give enough blocks —
+// 128 x 64 tiles at 52^2: 117 us against 182 for dw_tile; on the long-k
+// layers (104^2: 153 us against 216 for the sdot kernel + its im2col's 107)
+// the whole call gains 13-24 %; the 13^2 planes keep all 8 residues in one
+// 64 x 64 block (one partial plane: the group partials of a 1024 x 4608
+// output cost more to add than the product saves; 0.274 against 0.305 ms a
+// call).  -1: none applies.
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
-  if (M % 64 || batch < 1 || K < 64 || K > 3000) return -1;
+  (void)N;
+  if (M % 64 || batch < 1 || K < 64) return -1;
   if (K <= 256) return 5;
-  return N % 128 == 0 ? 2 : 4;
+  return M % 128 == 0 ? 7 : 6;
 }
 
-// col' rows per image: N rounded up to the form's column tile (the rows past
-// N are never written; they only feed output columns that are not stored)
 int64_t dw_res_b_rows(int v, int64_t N) {
   if (v < 0 || v >= kNumResForms) return N;
   const int64_t bn = kResForms[v].bn;
@@ -449,14 +448,11 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
     return hipErrorInvalidValue;
   // delta' and col' (or the input planes' rearrangement): one block row per
   // operand row, 65535 rows a launch
-  // chunk of a block: the largest of 2048 .. 256 that pads the row by at
-  // most an eighth
-  int chs = 256;
-  for (int c = RCH; c > 256; c /= 2)
-    if (((rowlen + c - 1) / c * c - rowlen) * 8 <= rowlen) {
-      chs = c;
-      break;
-    }
+  // chunk of a block: 2048, or the row rounded up to 256 when shorter (a
+  // block's loads are its latency: small chunks measured slower even where
+  // the 2048-chunk leaves a partial last block; 52^2 rows: 83 us with 256,
+  // 46 us with 2048)
+  const int chs = rowlen >= RCH ? RCH : rowlen > 512 ? 1024 : rowlen > 256 ? 512 : 256;
   const unsigned gx = (unsigned)((rowlen + chs - 1) / chs);
   auto rows_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
     for (int64_t r0 = 0; r0 < nrows; r0 += 65535) {
