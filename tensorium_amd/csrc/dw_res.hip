@@ -413,19 +413,24 @@ const char* dw_res_name(int v) { return v >= 0 && v < kNumResForms ? kResForms[v
 int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 31) / 32 * 32; }
 
 // Measured per YOLOv3 layer (scripts/dw_res_prof.py under a kernel trace,
-// batch 8; profiles/r04_dw_res_forms*): one residue a block (8 group planes,
-// no fold) runs the fastest product wherever the planes give enough blocks —
-// 128 x 64 tiles at 52^2: 117 us against 182 for dw_tile; on the long-k
-// layers (104^2: 153 us against 216 for the sdot kernel + its im2col's 107)
-// the whole call gains 13-24 %; the 13^2 planes keep all 8 residues in one
-// 64 x 64 block (one partial plane: the group partials of a 1024 x 4608
-// output cost more to add than the product saves; 0.274 against 0.305 ms a
-// call).  -1: none applies.
+// whole backward calls without state.delta at batch 8; profiles/
+// r04_dw_res_forms4*), against the kernels before (dw_tile at 52^2, the
+// residue-register kernel at 26^2 / 13^2, im2col + the sdot kernel on the
+// long-k planes):
+//   k <= 1024 (26^2, 13^2 planes): all 8 residues in one 64 x 64 block, one
+//     partial plane (26^2 0.221 -> 0.191 ms, 13^2 0.309 -> 0.275); the
+//     one-residue forms make 8 planes of these large outputs to add, and the
+//     26^2 product runs 0.26-0.27 with them;
+//   k <= 4096 (52^2): one residue a block, 128 x 64 (0.213 -> 0.194);
+//   longer k (104^2, 208^2 planes): one residue a block, 64 x 64 (104^2
+//   0.379 -> 0.267, 208^2 0.560 -> 0.434).
+// -1: none applies (filters not a multiple of 64, k < 64).
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
   (void)N;
   if (M % 64 || batch < 1 || K < 64) return -1;
-  if (K <= 256) return 5;
-  return M % 128 == 0 ? 7 : 6;
+  if (K <= 1024) return 5;
+  if (K <= 4096) return M % 128 == 0 ? 7 : 6;
+  return 6;
 }
 
 int64_t dw_res_b_rows(int v, int64_t N) {
