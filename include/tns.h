@@ -569,9 +569,12 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * tile over residue-major copies of delta and the im2col matrix, folded in
  * sdot's order, then added to weight_updates image by image (dw_res.hip; the
  * copies and the per-group partial planes live in the context's scratch);
- * by shape on the 3x3 layers with large outputs; -2 = off; v >= 0 forces form
- * v of tns_conv_dw_res_count() (same bits; ignored while TNS_OPT_DW_TILE
- * forces a tile).
+ * by shape on the 3x3 layers with >= 64 filters; -2 = off; v >= 0 forces
+ * form v of tns_conv_dw_res_count() (same bits; ignored while
+ * TNS_OPT_DW_TILE forces a tile).  Memory: the residue-major copies (about
+ * the im2col matrix plus delta) and the group planes live in the context's
+ * scratch, allocated IN ADDITION to the caller's workspace (which then holds
+ * nothing for dW); -2 bounds the backward's dW memory to the workspace.
  * TNS_OPT_BWD_OVERLAP (default 1): the conv backward runs the dW product and
  * the state.delta chain (which read delta and write disjoint outputs)
  * concurrently, the latter on a side stream of the context that the
