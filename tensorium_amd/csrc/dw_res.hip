@@ -377,6 +377,60 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
       dst + b * dstImg + (int64_t)n * 8 * K4, K4);
 }
 
+// Rows of at most 256 elements (the 13^2 planes): eight rows a block, a
+// thread's element of each (eight loads in flight), written straight to its
+// rearranged place — a block writes its rows whole, so the lines complete in
+// L2 without the LDS transpose
+__global__ __launch_bounds__(256) void res_permute_short_kernel(
+    const float* __restrict__ src, int64_t srcImg, float* __restrict__ dst, int64_t dstImg,
+    int rows, int K, int K4, int row0, int total) {
+  const int pp = threadIdx.x;
+  if (pp >= 8 * K4) return;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ra = row0 + 8 * (int)blockIdx.y + j;
+    const int b = ra / rows, row = ra - b * rows;
+    v[j] = (ra < total && pp < K) ? src[b * srcImg + (int64_t)row * K + pp] : 0.0f;
+  }
+  const int off = (pp & 7) * K4 + kperm(pp >> 3);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ra = row0 + 8 * (int)blockIdx.y + j;
+    if (ra >= total) break;
+    const int b = ra / rows, row = ra - b * rows;
+    dst[b * dstImg + (int64_t)row * 8 * K4 + off] = v[j];
+  }
+}
+
+__global__ __launch_bounds__(256) void im2col_res_short_kernel(
+    const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int H,
+    int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
+    int rows, int K4, int row0, int total) {
+  const int pp = threadIdx.x;
+  if (pp >= 8 * K4) return;
+  const int oy = pp / oW, ox = pp - oy * oW, taps = kH * kW;
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ra = row0 + 8 * (int)blockIdx.y + j;
+    const int b = ra / rows, n = ra - b * rows;
+    const int c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
+    const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
+    v[j] = (ra < total && pp < HWo && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+               ? x[b * xImg + ((int64_t)c * H + iy) * W + ix]
+               : 0.0f;
+  }
+  const int off = (pp & 7) * K4 + kperm(pp >> 3);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int ra = row0 + 8 * (int)blockIdx.y + j;
+    if (ra >= total) break;
+    const int b = ra / rows, n = ra - b * rows;
+    dst[b * dstImg + (int64_t)n * 8 * K4 + off] = v[j];
+  }
+}
+
 template <int BM, int BN, int R>
 hipError_t launch_res(const ResArgs& a, int64_t batch, hipStream_t s) {
   if (a.M % BM) return hipErrorInvalidValue;
@@ -474,31 +528,62 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       default: f(std::integral_constant<int, 2048>{}); break;
     }
   };
-  if (hipError_t e = rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
-        by_chunk([&](auto c) {
-          hipLaunchKernelGGL((res_permute_kernel<decltype(c)::value>), gr, dim3(256), 0, s, d.delta,
-                             d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0);
+  if (rowlen <= 256) {
+    auto short_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
+      const int64_t groups = (nrows + 7) / 8;
+      for (int64_t g0 = 0; g0 < groups; g0 += 65535) {
+        launch(dim3(1, (unsigned)std::min<int64_t>(groups - g0, 65535)), (int)(8 * g0), (int)nrows);
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+      }
+      return hipSuccess;
+    };
+    if (hipError_t e = short_launch(d.batch * d.M, [&](dim3 gr, int r0, int tot) {
+          hipLaunchKernelGGL(res_permute_short_kernel, gr, dim3(256), 0, s, d.delta, d.M * d.K,
+                             d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0, tot);
         });
-      });
-      e != hipSuccess)
-    return e;
-  if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
-        by_chunk([&](auto c) {
-          constexpr int C = decltype(c)::value;
+        e != hipSuccess)
+      return e;
+    if (hipError_t e = short_launch(d.batch * d.N, [&](dim3 gr, int r0, int tot) {
           if (d.direct) {
-            hipLaunchKernelGGL((res_permute_kernel<C>), gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                               npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0);
+            hipLaunchKernelGGL(res_permute_short_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+                               npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0, tot);
           } else {
             const ConvGeom& g = d.g;
-            hipLaunchKernelGGL((im2col_res_kernel<C>), gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+            hipLaunchKernelGGL(im2col_res_short_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
                                npad * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
                                (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX,
-                               (int)g.ow, (int)d.K, (int)d.N, (int)K4, r0);
+                               (int)g.ow, (int)d.K, (int)d.N, (int)K4, r0, tot);
           }
         });
-      });
-      e != hipSuccess)
-    return e;
+        e != hipSuccess)
+      return e;
+  } else {
+    if (hipError_t e = rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
+          by_chunk([&](auto c) {
+            hipLaunchKernelGGL((res_permute_kernel<decltype(c)::value>), gr, dim3(256), 0, s, d.delta,
+                               d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0);
+          });
+        });
+        e != hipSuccess)
+      return e;
+    if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
+          by_chunk([&](auto c) {
+            constexpr int C = decltype(c)::value;
+            if (d.direct) {
+              hipLaunchKernelGGL((res_permute_kernel<C>), gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+                                 npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0);
+            } else {
+              const ConvGeom& g = d.g;
+              hipLaunchKernelGGL((im2col_res_kernel<C>), gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
+                                 npad * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
+                                 (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX,
+                                 (int)g.ow, (int)d.K, (int)d.N, (int)K4, r0);
+            }
+          });
+        });
+        e != hipSuccess)
+      return e;
+  }
   ResArgs a{};
   a.A = d.dA;
   a.B = d.dB;
