@@ -466,13 +466,7 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
   const bool chainwave = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;
   const int st = tid - 64;  // staging thread index (waves 1..3)
   const int l = tid & 7, grp = tid >> 3;
-  // wave 0: lanes 0-7 run the chains; lanes 8-15 read each chain's next
-  // four terms (of the first stream, for CH_DOT) for it — a row_ror:8 DPP
-  // operand hands them to the add / fmac — and CH_VDELTA's second chain set
-  // sits at lanes 16-23 with its readers at 24-31
-  const bool chain = grp == 0 || (MODE == CH_VDELTA && grp == 2);
-  constexpr bool DPP = true;
-  const bool reader = MODE == CH_VDELTA ? tid < 32 : tid < 16;
+  const bool chain = grp == 0 || (MODE == CH_VDELTA && grp == 1);
   const int64_t nb8 = (bs >> 3) << 3;
   const int ntile = (int)((nb8 + TILE - 1) / TILE);
   const int tail = (int)(bs & 7);
@@ -548,14 +542,13 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
     } else {
       __syncthreads();
       for (int t = 0; t < ntile; ++t) {
-        if (reader) {
+        if (chain) {
           const int64_t rem = nb8 - (int64_t)t * TILE;
           const int cnt = (int)((rem < TILE ? rem : TILE) >> 3);
           const int buf = t % NBUF;
-          const int sub = DPP ? (tid >> 3) & 1 : 0;  // a reader lane's four-term offset
           const float* row =
-              ((MODE == CH_VDELTA && tid >= 16) ? &V[buf][0] : &U[buf][0]) + l * LDT + 4 * sub;
-          const float* rowb = TWO ? &V[buf][0] + l * LDT : row;  // (no reader offset)
+              ((MODE == CH_VDELTA && grp == 1) ? &V[buf][0] : &U[buf][0]) + l * LDT;
+          const float* rowb = TWO ? &V[buf][0] + l * LDT : row;
           // groups of 16 terms read by ds_read_b128 issued as inline asm
           // with explicit counted waits: hipcc's own waits at the loop
           // header assumed only the newest reads pending and drained the
@@ -571,22 +564,8 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
           typedef float f4 __attribute__((ext_vector_type(4)));
           const unsigned ra_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)row;
           const unsigned rb_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)rowb;
-          // (one stream: a group's 16 terms are two reads, the own lanes'
-          // terms 0-3 and 8-11, the readers' 4-7 and 12-15)
           auto rd = [&](int q, f4 (&v)[4], f4 (&w)[4]) {
             const unsigned a = ra_lds + 4u * (unsigned)q;
-            if constexpr (DPP) {
-              asm volatile("ds_read_b128 %0, %1" : "=v"(v[0]) : "v"(a));
-              asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(v[1]) : "v"(a));
-              if constexpr (MODE == CH_DOT) {  // the own lanes' 16 second-stream terms
-                const unsigned b = rb_lds + 4u * (unsigned)q;
-                asm volatile("ds_read_b128 %0, %1" : "=v"(w[0]) : "v"(b));
-                asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(w[1]) : "v"(b));
-                asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(w[2]) : "v"(b));
-                asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(w[3]) : "v"(b));
-              }
-              return;
-            }
             asm volatile("ds_read_b128 %0, %1" : "=v"(v[0]) : "v"(a));
             asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(v[1]) : "v"(a));
             asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(v[2]) : "v"(a));
@@ -601,43 +580,15 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
           };
           // wait until at most 8 reads are pending, with the set as operand
           auto wait8 = [&](f4 (&v)[4], f4 (&w)[4]) {
-            if constexpr (MODE == CH_DOT)  // (six reads a group, two groups: the newer in flight)
-              asm volatile("s_waitcnt lgkmcnt(6)"
-                           : "+v"(v[0]), "+v"(v[1]), "+v"(w[0]), "+v"(w[1]), "+v"(w[2]),
-                             "+v"(w[3]));
-            else  // (two reads a group: the two newer groups in flight)
-              asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(v[0]), "+v"(v[1]));
+            if constexpr (MODE == CH_DOT)
+              asm volatile("s_waitcnt lgkmcnt(8)"
+                           : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(w[0]),
+                             "+v"(w[1]), "+v"(w[2]), "+v"(w[3]));
+            else
+              asm volatile("s_waitcnt lgkmcnt(8)"
+                           : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
           };
           auto add16 = [&](const f4 (&v)[4], const f4 (&w)[4]) {
-            if constexpr (MODE == CH_DOT) {
-#pragma unroll
-              for (int h = 0; h < 2; ++h) {
-#pragma unroll
-                for (int z = 0; z < 4; ++z) acc = fmaf(v[h][z], w[2 * h][z], acc);
-#pragma unroll
-                for (int z = 0; z < 4; ++z) {  // dpp(v) * w + acc, one rounding
-                  const float x = v[h][z], y = w[2 * h + 1][z];
-                  asm volatile("v_fmac_f32_dpp %0, %1, %2 row_ror:8 row_mask:0xf bank_mask:0xf"
-                               : "+v"(acc)
-                               : "v"(x), "v"(y));
-                }
-              }
-              return;
-            } else if constexpr (DPP) {
-#pragma unroll
-              for (int h = 0; h < 2; ++h) {
-#pragma unroll
-                for (int z = 0; z < 4; ++z) acc = acc + v[h][z];
-#pragma unroll
-                for (int z = 0; z < 4; ++z) {  // row_ror:8 — lane l gets lane l + 8's term
-                  const float x = v[h][z];
-                  asm volatile("v_add_f32_dpp %0, %1, %0 row_ror:8 row_mask:0xf bank_mask:0xf"
-                               : "+v"(acc)
-                               : "v"(x));
-                }
-              }
-              return;
-            }
 #pragma unroll
             for (int z = 0; z < 16; ++z) {
               if constexpr (MODE == CH_DOT) acc = fmaf(v[z >> 2][z & 3], w[z >> 2][z & 3], acc);
@@ -659,9 +610,10 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
               rd(q + 48, vb, wb);
             }
             asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(va[0]), "+v"(va[1]), "+v"(wa[0]), "+v"(wa[1]), "+v"(wa[2]),
-                           "+v"(wa[3]), "+v"(vb[0]), "+v"(vb[1]), "+v"(wb[0]), "+v"(wb[1]),
-                           "+v"(wb[2]), "+v"(wb[3]));
+                         : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(va[3]), "+v"(wa[0]),
+                           "+v"(wa[1]), "+v"(wa[2]), "+v"(wa[3]), "+v"(vb[0]), "+v"(vb[1]),
+                           "+v"(vb[2]), "+v"(vb[3]), "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]),
+                           "+v"(wb[3]));
           } else {
             full = cnt - cnt % 48;
             rd(0, va, wa);
@@ -679,10 +631,11 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
               rd(q + 80, vc, wc);
             }
             asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(va[0]), "+v"(va[1]), "+v"(vb[0]), "+v"(vb[1]), "+v"(vc[0]),
-                           "+v"(vc[1]));
+                         : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(va[3]), "+v"(vb[0]),
+                           "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]), "+v"(vc[0]), "+v"(vc[1]),
+                           "+v"(vc[2]), "+v"(vc[3]));
           }
-          for (int q = full; q < cnt; ++q) {  // (own lanes: row has no reader offset)
+          for (int q = full; q < cnt; ++q) {
             if constexpr (MODE == CH_DOT) acc = fmaf(row[q], rowb[q], acc);
             else acc = acc + row[q];
           }
@@ -691,7 +644,7 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
       }
     }
     if (tid < 64) {  // lane-order epilogues (as block_chains)
-      const bool lanes_form = MODE == CH_SRSS || (MODE == CH_VDELTA && grp == 2);
+      const bool lanes_form = MODE == CH_SRSS || (MODE == CH_VDELTA && grp == 1);
       if constexpr (MODE == CH_DOT) {
         if (tail && grp == 0) {
           const float xa = l < tail ? pa[nb8 + l] : 0.0f;
