@@ -889,6 +889,7 @@ const TileInfo4 kTiles4DX[] = {
     TNS_CT4DX(128, 96, 8, 1, 64, 1, true, 2, 0, 0),    // 3
     TNS_CT4DX(64, 64, 4, 2, 32, 0, false, 3, 0, 0),    // 4
     TNS_CT4DX(128, 48, 8, 1, 64, 1, true, 2, 0, 0),    // 5
+    TNS_CT4DX(32, 176, 2, 4, 64, 1, true, 2, 3, 3),    // 6: 32-channel planes (208^2)
     // (128 x 176: the running sums take it past 256 VGPRs — spills; not built.
     // Eight-wave 64 x 96 / 32 x 96 forms for the 26^2 / 13^2 row counts
     // measured no better than these: 26^2 0.369 / 0.378 ms a call against
@@ -1004,7 +1005,9 @@ int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t 
                         int64_t pad) {
   const int64_t N = batch * H * W, oh = H + 2 * pad - ks + 1, ow = W + 2 * pad - ks + 1;
   int v = -1;
-  if (N >= 50000)
+  if (C % 64 && N >= 50000)
+    v = 6;
+  else if (N >= 50000)
     v = 4;
   else if (N >= 16384)
     v = 0;

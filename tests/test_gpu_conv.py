@@ -244,7 +244,7 @@ def test_conv_backward_dx_tiles(hip, torch_cuda, ora):
 
 
 DX3_CASES = [(2, 64, 13, 64, 3, 1, 1, 9), (2, 128, 11, 96, 3, 1, 1, 1), (3, 64, 9, 128, 3, 1, 0, 9),
-             (1, 128, 20, 128, 3, 1, 1, 4), (2, 64, 6, 64, 3, 1, 2, 9)]
+             (1, 128, 20, 128, 3, 1, 1, 4), (2, 64, 6, 64, 3, 1, 2, 9), (2, 32, 15, 64, 3, 1, 1, 9)]
 
 
 def test_conv_backward_dx_conv_forms(hip, torch_cuda, ora):
