@@ -952,8 +952,12 @@ const char* conv_tile4_ta_name(int v) { return v >= 0 && v < kNumTiles4T ? kTile
 // of the TN GEMM on the 13^2 planes only (1x1 layers 0.222 -> 0.155 ms per
 // 7 calls, 3x3 1.197 -> 1.180); behind it on the 26^2 .. 104^2 planes, whose
 // TN tiles balance better (26^2 3x3 1.48 -> 1.65 with the 128 x 96 form).
+// Round 4 (scripts/bwd_sweep.py --what dx, profiles/r04_bwd_dx_forms2.json:
+// whole backward calls with state.delta): the 64 x 96 form ahead of 128 x 48
+// on the 13^2 planes (layer 45 0.440 -> 0.397 ms, stride-2 layer 43 0.450 ->
+// 0.407).
 int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K) {
-  if (K % 64 == 0 && M % 128 == 0 && N < 4096) return 2;
+  if (K % 32 == 0 && M % 64 == 0 && N < 4096) return 4;
   return -1;
 }
 
