@@ -1670,7 +1670,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   if (g_nt_sdot && g_dw_res != -2 && g_dw_tile < 0 && batch <= 65535 && i_k >= 64) {
     if (g_dw_res >= 0)
       dwr = (int)g_dw_res;
-    else if (kSize == 3 || kSize == 1)
+    else if (kSize == 3)  // (1x1 layers: behind the sdot kernels, 0.048 -> 0.058 ms at 52^2)
       dwr = dw_res_pick(i_m, i_n, i_k, batch);
     if (dwr >= 0) dwv = -1;
   }
