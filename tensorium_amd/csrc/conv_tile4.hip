@@ -953,18 +953,21 @@ const char* conv_tile4_ta_name(int v) { return v >= 0 && v < kNumTiles4T ? kTile
 // 7 calls, 3x3 1.197 -> 1.180); behind it on the 26^2 .. 104^2 planes, whose
 // TN tiles balance better (26^2 3x3 1.48 -> 1.65 with the 128 x 96 form).
 // Round 4 (scripts/bwd_sweep.py --what dx, whole backward calls with
-// state.delta; profiles/r04_bwd_dx_forms2.json, r04_bwd_sweep_start.json):
-// 3x3 layers (M = 9 C) on the 13^2 planes take the 64 x 96 form (layer 45
-// 0.440 -> 0.397 ms, stride-2 layer 43 0.450 -> 0.407); the 1x1 layers (M =
-// C, the product added into state.delta in the epilogue) 128 x 48 on the
-// 13^2 planes and 64 x 64 on the 26^2 / 52^2 ones (0.080 -> 0.071 ms at 26^2,
-// 0.080 -> 0.078 at 52^2, against the TN GEMM).
-int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K) {
-  if (M <= 1024) {  // 1x1 layers
+// state.delta; profiles/r04_bwd_dx_forms2.json, r04_bwd_dx_forms4.json):
+// 3x3 layers on the 13^2 planes take the 64 x 96 form (layer 45 0.440 ->
+// 0.397 ms, stride-2 layer 43 0.450 -> 0.407), the stride-2 208^2 -> 104^2
+// layer 64 x 64 (0.552 -> 0.501); the 1x1 layers (the product added into
+// state.delta in the epilogue) 128 x 48 on the 13^2 planes (0.087 -> 0.080)
+// and 64 x 64 on the 26^2 / 52^2 ones (0.079 -> 0.075 at 26^2).
+int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K, int64_t ks) {
+  if (ks == 1) {
     if (N >= 4096) return (M % 64 == 0 && K % 32 == 0) ? 7 : -1;
     return (K % 64 == 0 && M % 128 == 0) ? 2 : -1;
   }
-  if (K % 32 == 0 && M % 64 == 0 && N < 4096) return 4;
+  if (K % 32 == 0 && M % 64 == 0) {
+    if (N < 4096) return 4;
+    if (N >= 50000) return 8;
+  }
   return -1;
 }
 

@@ -1815,7 +1815,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     bool done = false;
     float* col = dx_direct ? state_delta : dx_ws;
     if (g_dx_tile != -2) {
-      const int dv = g_dx_tile >= 0 ? (int)g_dx_tile : conv_tile4_dx_pick(i_n, batch * i_k, i_m);
+      const int dv = g_dx_tile >= 0 ? (int)g_dx_tile : conv_tile4_dx_pick(i_n, batch * i_k, i_m, kSize);
       if (dv >= 0) {
         OpTimer t(c, TNS_OP_GEMM);
         const hipError_t e = launch_conv_tile4_dx(dv, weights, delta, col, batch, C, kSize,

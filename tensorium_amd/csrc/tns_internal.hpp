@@ -143,7 +143,7 @@ hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStrea
 // conv_tile4_dx_pick = -1 where none applies
 int conv_tile4_ta_count();
 const char* conv_tile4_ta_name(int v);
-int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K);
+int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K, int64_t ks);
 hipError_t launch_conv_tile4_dx(int v, const float* w, const float* delta, float* col,
                                 int64_t batch, int64_t C, int64_t ks, int64_t F, int64_t oh,
                                 int64_t ow, hipStream_t s, bool add_into = false);
