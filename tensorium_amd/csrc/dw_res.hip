@@ -61,6 +61,10 @@ struct ResArgs {
   float* P;        // [batch][G][M][N]
   int M, N, K1, K4, G;
   int64_t strideA, strideB, strideP;
+  // (IF) every image in one block: weight_updates [M][N] += ALPHA * dot_b
+  float* W;
+  float alpha;
+  int batch;
 };
 
 // R residues per block: the residue of position rho in group g, in sdot's
@@ -71,9 +75,15 @@ __device__ __forceinline__ int residue_of(int g, int rho) {
   return (R / 2) * g + (rho >> 1) + 4 * (rho & 1);
 }
 
-template <int BM, int BN, int R>
+// IF: the block runs every image in turn (grid.z = 1, R = 8) and adds
+// ALPHA * dot of each to the weight_updates tile it holds in registers, in
+// image order — no partial planes and no second pass (the 13^2 planes, whose
+// 1024 x 4608 partials per image cost more to write and re-read than the
+// product)
+template <int BM, int BN, int R, bool IF = false>
 __global__ __launch_bounds__(256, 2) void dw_res_kernel(
     ResArgs p) {
+  static_assert(!IF || R == 8, "image folding needs the whole dot in the block");
   constexpr int TI = BM / 64, TJ = BN / 64;  // 32x32 tiles of a wave (2 x 2 waves)
   constexpr int A_T = BM * RBK, STAGE = (BM + BN) * RBK;  // floats
   constexpr int GA = BM / 8, GT = (BM + BN) / 8, GPW = GT / 4;  // DMA row groups
@@ -85,7 +95,7 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   const int tiles_m = p.M / BM;
   const int m0 = (int)(blockIdx.x % tiles_m) * BM, n0 = (int)(blockIdx.x / tiles_m) * BN;
   const int g = blockIdx.y;
-  const int64_t img = blockIdx.z;
+  const int64_t img = IF ? 0 : blockIdx.z;
   const int64_t ld = 8LL * p.K4;  // row stride, floats
   const float* A = p.A + img * p.strideA + (int64_t)m0 * ld;
   const float* B = p.B + img * p.strideB + (int64_t)n0 * ld;
@@ -98,16 +108,18 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   const unsigned voff1 =
       (unsigned)(arow * ld * 4) + 16u * (unsigned)((lane & 7) ^ (((arow >> 1) & 7) ^ 4));
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem;
-  auto issue = [&](int residue, int kt, int st) {
+  auto issue = [&](int residue, int kt, int st, int b) {
     const int64_t koff = (int64_t)residue * p.K4 + (int64_t)kt * RBK;
+    const float* Ab = IF ? A + b * p.strideA : A;
+    const float* Bb = IF ? B + b * p.strideB : B;
     const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
 #pragma unroll
     for (int u = 0; u < GPW; ++u) {
       const int q = wid * GPW + u;
       if (q < GA)
-        dma16(A + (int64_t)(8 * q) * ld + koff, (q & 1) ? voff1 : voff0, sb + (unsigned)(q * 1024));
+        dma16(Ab + (int64_t)(8 * q) * ld + koff, (q & 1) ? voff1 : voff0, sb + (unsigned)(q * 1024));
       else
-        dma16(B + (int64_t)(8 * (q - GA)) * ld + koff, ((q - GA) & 1) ? voff1 : voff0,
+        dma16(Bb + (int64_t)(8 * (q - GA)) * ld + koff, ((q - GA) & 1) ? voff1 : voff0,
               sb + (unsigned)(A_T * 4 + (q - GA) * 1024));
     }
   };
@@ -202,22 +214,43 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   // the last tile's step groups: its k rounded up to 16 (K4 is a multiple of
   // 32, so the rest of the tile is zero)
   const int last_groups = 2 * ((p.K1 - (nt - 1) * RBK + 15) / 16);
-  const int T = R * nt;
+  const int TI1 = R * nt;                // tiles of one image
+  const int T = IF ? p.batch * TI1 : TI1;
   // the barrier that publishes tile t+1 sits before tile t's last step: tile
   // t+1's first fragments are read under that step's MFMAs, and the DMA of
   // tile t+2 (into tile t's stage, every read of which completed before the
   // barrier) goes out a whole tile ahead of its use
-  auto tile_of = [&](int t, int& res, int& kt) {
-    res = residue_of<R>(g, t / nt);
-    kt = t - (t / nt) * nt;
+  auto tile_of = [&](int t, int& res, int& kt, int& b) {
+    b = IF ? t / TI1 : 0;
+    const int u = t - b * TI1;
+    res = residue_of<R>(g, u / nt);
+    kt = u - (u / nt) * nt;
   };
+  // (IF) the weight_updates tile, accumulated image by image
+  floatx16 Wt[IF ? TI : 1][IF ? TJ : 1];
+  auto w_at = [&](int i, int j, int e, int& row, int& col) {
+    col = n0 + wn * (BN / 2) + 32 * j + l31;
+    row = m0 + wm * (BM / 2) + 32 * i + 8 * (e >> 2) + 4 * h + (e & 3);
+  };
+  if constexpr (IF) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          int row, col;
+          w_at(i, j, e, row, col);
+          Wt[i][j][e] = col < p.N ? p.W[(int64_t)row * p.N + col] : 0.0f;
+        }
+  }
   {
-    int r0, k0;
-    tile_of(0, r0, k0);
-    issue(r0, k0, 0);
+    int r0, k0, b0;
+    tile_of(0, r0, k0, b0);
+    issue(r0, k0, 0, b0);
     if (T > 1) {
-      tile_of(1, r0, k0);
-      issue(r0, k0, 1);
+      tile_of(1, r0, k0, b0);
+      issue(r0, k0, 1, b0);
       // (this wave's DMA of tile 0 landed: the newer GPW may stay in flight)
       if constexpr (GPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       else if constexpr (GPW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
@@ -230,20 +263,46 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
     frag(smem, 0, f0);
   }
   for (int t = 0; t < T; ++t) {
-    const int kt = t - (t / nt) * nt;
+    int rt, kt, bt;
+    tile_of(t, rt, kt, bt);
+    const int u = t - bt * TI1;  // tile within its image
     compute(smem + (t & 1) * STAGE, kt == nt - 1 ? last_groups : RBK / 8);
     if (t + 1 < T) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of tile t+1
       __syncthreads();  // every wave's; every read of tile t complete
       if (t + 2 < T) {
-        int r2, k2;
-        tile_of(t + 2, r2, k2);
-        issue(r2, k2, t & 1);
+        int r2, k2, b2;
+        tile_of(t + 2, r2, k2, b2);
+        issue(r2, k2, t & 1, b2);
       }
       frag(smem + ((t + 1) & 1) * STAGE, 0, f0);
     }
     mma(f1);  // the tile's last step
-    if (kt == nt - 1) fold(t / nt);
+    if (kt == nt - 1) fold(u / nt);
+    if constexpr (IF) {
+      if (u == TI1 - 1) {  // image bt done: C := C + ALPHA * dot, (s0+s1)+(s2+s3)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            const floatx16 dot = X[i][j] + Y[i][j];
+            Wt[i][j] = Wt[i][j] + p.alpha * dot;
+          }
+      }
+    }
+  }
+  if constexpr (IF) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          int row, col;
+          w_at(i, j, e, row, col);
+          if (col < p.N) p.W[(int64_t)row * p.N + col] = Wt[i][j][e];
+        }
+    return;
   }
 
   // ---- the group's partial plane -------------------------------------------
@@ -431,12 +490,12 @@ __global__ __launch_bounds__(256) void im2col_res_short_kernel(
   }
 }
 
-template <int BM, int BN, int R>
+template <int BM, int BN, int R, bool IF = false>
 hipError_t launch_res(const ResArgs& a, int64_t batch, hipStream_t s) {
   if (a.M % BM) return hipErrorInvalidValue;
   const int64_t tiles = (int64_t)(a.M / BM) * ((a.N + BN - 1) / BN);
-  hipLaunchKernelGGL((dw_res_kernel<BM, BN, R>), dim3((unsigned)tiles, 8 / R, (unsigned)batch),
-                     dim3(256), 0, s, a);
+  hipLaunchKernelGGL((dw_res_kernel<BM, BN, R, IF>),
+                     dim3((unsigned)tiles, 8 / R, IF ? 1u : (unsigned)batch), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -444,17 +503,23 @@ struct ResForm {
   int bm, bn, r;
   hipError_t (*fn)(const ResArgs&, int64_t, hipStream_t);
   const char* name;
+  bool fold_images;  // (IF) weight_updates accumulated in the block
 };
 #define TNS_RES(BMv, BNv, Rv) \
-  {BMv, BNv, Rv, launch_res<BMv, BNv, Rv>, "dw_res<" #BMv "x" #BNv ",r" #Rv ">"}
+  {BMv, BNv, Rv, launch_res<BMv, BNv, Rv>, "dw_res<" #BMv "x" #BNv ",r" #Rv ">", false}
+#define TNS_RESI(BMv, BNv) \
+  {BMv, BNv, 8, launch_res<BMv, BNv, 8, true>, "dw_res<" #BMv "x" #BNv ",r8,images>", true}
 // (R = 8 on the 128-wide tiles: four live accumulator sets spill)
 const ResForm kResForms[] = {
     TNS_RES(128, 128, 2), TNS_RES(128, 128, 4), TNS_RES(64, 128, 2),
     TNS_RES(64, 128, 4),  TNS_RES(64, 64, 4),   TNS_RES(64, 64, 8),
     // one residue a block (8 group planes): the long-k layers with few outputs
     TNS_RES(64, 64, 1),   TNS_RES(128, 64, 1),  TNS_RES(128, 128, 1),
+    // every image in one block (no partial planes)
+    TNS_RESI(64, 64),
 };
 #undef TNS_RES
+#undef TNS_RESI
 constexpr int kNumResForms = sizeof(kResForms) / sizeof(kResForms[0]);
 
 int blocks_for(int64_t n) { return (int)std::min<int64_t>((n + 255) / 256, 16384); }
@@ -482,6 +547,7 @@ int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 31) / 32 * 32; }
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
   (void)N;
   if (M % 64 || batch < 1 || K < 64) return -1;
+  if (K <= 256) return 9;
   if (K <= 1024) return 5;
   if (K <= 4096) return M % 128 == 0 ? 7 : 6;
   return 6;
@@ -493,7 +559,9 @@ int64_t dw_res_b_rows(int v, int64_t N) {
   return (N + bn - 1) / bn * bn;
 }
 
-int64_t dw_res_groups(int v) { return v >= 0 && v < kNumResForms ? 8 / kResForms[v].r : 0; }
+int64_t dw_res_groups(int v) {
+  return v >= 0 && v < kNumResForms && !kResForms[v].fold_images ? 8 / kResForms[v].r : 0;
+}
 
 hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   if (v < 0 || v >= kNumResForms) return hipErrorInvalidValue;
@@ -596,7 +664,11 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   a.strideA = d.M * rowlen;
   a.strideB = npad * rowlen;
   a.strideP = (int64_t)a.G * d.M * d.N;
+  a.W = d.weight_updates;
+  a.alpha = d.alpha;
+  a.batch = (int)d.batch;
   if (hipError_t e = f.fn(a, d.batch, s); e != hipSuccess) return e;
+  if (f.fold_images) return hipSuccess;  // (weight_updates written by the product)
   const int64_t mn = d.M * d.N;
   hipLaunchKernelGGL(dw_res_accumulate_kernel, dim3(blocks_for(mn)), dim3(256), 0, s,
                      d.weight_updates, d.part, mn, a.G, a.strideP, (int)d.batch, d.alpha);
