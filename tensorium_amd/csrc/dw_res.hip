@@ -462,6 +462,46 @@ __global__ __launch_bounds__(256) void res_permute_short_kernel(
   }
 }
 
+// The rearranged im2col matrix by input plane: a block stages one image's
+// channel plane in LDS (read once, coalesced), then writes that channel's
+// kH*kW col' rows from it — each row's residue slices as runs of
+// consecutive i (the row-chunk kernel above reads every plane element once
+// per tap from L2).  Planes of at most PLANE_MAX floats.
+constexpr int PLANE_MAX = 16384;
+__global__ __launch_bounds__(256) void im2col_res_plane_kernel(
+    const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int C,
+    int H, int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
+    int K4, float inv_ow) {
+  __shared__ float plane[PLANE_MAX];
+  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const float* xc = x + b * xImg + (int64_t)c * H * W;
+  for (int e = tid; e < H * W; e += 256) plane[e] = xc[e];
+  __syncthreads();
+  const int taps = kH * kW;
+  float* drow0 = dst + b * dstImg + (int64_t)c * taps * 8 * K4;
+  for (int t = 0; t < taps; ++t) {
+    const int kr = t / kW, kc = t - kr * kW;
+    float* drow = drow0 + (int64_t)t * 8 * K4;
+    for (int r = 0; r < 8; ++r) {
+      for (int i = tid; i < K4; i += 256) {
+        const int pp = r + 8 * i;
+        float v = 0.0f;
+        if (pp < HWo) {
+          // oy = pp / oW: the float estimate (pp < 2^24, exact operands) is
+          // off by at most one either way; corrected
+          int oy = (int)((float)pp * inv_ow);
+          oy += (oy + 1) * oW <= pp;
+          oy -= oy * oW > pp;
+          const int ox = pp - oy * oW;
+          const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
+          if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) v = plane[iy * W + ix];
+        }
+        drow[(int64_t)r * K4 + kperm(i)] = v;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void im2col_res_short_kernel(
     const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int H,
     int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
@@ -596,7 +636,26 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       default: f(std::integral_constant<int, 2048>{}); break;
     }
   };
-  if (rowlen <= 256) {
+  auto delta_rows = [&]() {
+    return rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
+      by_chunk([&](auto c) {
+        hipLaunchKernelGGL((res_permute_kernel<decltype(c)::value>), gr, dim3(256), 0, s, d.delta,
+                           d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0);
+      });
+    });
+  };
+  // (the col' rows by input plane where a plane fits the block's LDS)
+  const bool by_plane = !d.direct && rowlen > 256 && d.g.H * d.g.W <= PLANE_MAX &&
+                        d.batch <= 65535 && d.g.C <= 0x7fffffff && d.K < (1 << 24);
+  if (by_plane) {
+    if (hipError_t e = delta_rows(); e != hipSuccess) return e;
+    hipLaunchKernelGGL(im2col_res_plane_kernel, dim3((unsigned)d.g.C, (unsigned)d.batch),
+                       dim3(256), 0, s, d.x, d.xStride, d.dB, npad * rowlen, (int)d.g.C,
+                       (int)d.g.H, (int)d.g.W, (int)d.g.kH, (int)d.g.kW, (int)d.g.sY, (int)d.g.sX,
+                       (int)d.g.padH, (int)d.g.padW, (int)d.g.dY, (int)d.g.dX, (int)d.g.ow,
+                       (int)d.K, (int)K4, 1.0f / (float)d.g.ow);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+  } else if (rowlen <= 256) {
     auto short_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
       const int64_t groups = (nrows + 7) / 8;
       for (int64_t g0 = 0; g0 < groups; g0 += 65535) {
@@ -626,14 +685,7 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
         e != hipSuccess)
       return e;
   } else {
-    if (hipError_t e = rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
-          by_chunk([&](auto c) {
-            hipLaunchKernelGGL((res_permute_kernel<decltype(c)::value>), gr, dim3(256), 0, s, d.delta,
-                               d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0);
-          });
-        });
-        e != hipSuccess)
-      return e;
+    if (hipError_t e = delta_rows(); e != hipSuccess) return e;
     if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
           by_chunk([&](auto c) {
             constexpr int C = decltype(c)::value;
