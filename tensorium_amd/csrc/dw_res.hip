@@ -462,42 +462,49 @@ __global__ __launch_bounds__(256) void res_permute_short_kernel(
   }
 }
 
-// The rearranged im2col matrix by input plane: a block stages one image's
-// channel plane in LDS (read once, coalesced), then writes that channel's
-// kH*kW col' rows from it — each row's residue slices as runs of
-// consecutive i (the row-chunk kernel above reads every plane element once
-// per tap from L2).  Planes of at most PLANE_MAX floats.
+// The rearranged im2col matrix by input band: a block stages the input rows
+// under one band of L output pixels of one image's channel plane in LDS
+// (read once, coalesced), then writes that band of the channel's kH*kW col'
+// rows from it — per tap and residue a run of L/8 consecutive i (the
+// row-chunk kernel above reads every plane element once per tap from L2).
+// L is a multiple of 256 (whole kperm blocks), the band's input rows at most
+// PLANE_MAX floats.
 constexpr int PLANE_MAX = 16384;
-__global__ __launch_bounds__(256) void im2col_res_plane_kernel(
-    const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int C,
-    int H, int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
-    int K4, float inv_ow) {
+__global__ __launch_bounds__(256) void im2col_res_band_kernel(
+    const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int H,
+    int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
+    int K4, int L, float inv_ow) {
   __shared__ float plane[PLANE_MAX];
-  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int band = blockIdx.x, c = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
+  const int p0 = band * L, p1 = min(p0 + L, 8 * K4);
+  // input rows under output rows oy0..oy1 (the last pixel clamped to the plane)
+  const int oy0 = min(p0, HWo - 1) / oW, oy1 = (min(p1, HWo) - 1) / oW;
+  const int iy0 = oy0 * sY - pH, nrows = (oy1 - oy0) * sY + (kH - 1) * dY + 1;
   const float* xc = x + b * xImg + (int64_t)c * H * W;
-  for (int e = tid; e < H * W; e += 256) plane[e] = xc[e];
+  for (int e = tid; e < nrows * W; e += 256) {
+    const int ry = e / W, iy = iy0 + ry;
+    plane[e] = (unsigned)iy < (unsigned)H ? xc[iy * W + (e - ry * W)] : 0.0f;
+  }
   __syncthreads();
-  const int taps = kH * kW;
+  const int taps = kH * kW, i0 = p0 >> 3, i1 = p1 >> 3;
   float* drow0 = dst + b * dstImg + (int64_t)c * taps * 8 * K4;
-  for (int t = 0; t < taps; ++t) {
-    const int kr = t / kW, kc = t - kr * kW;
-    float* drow = drow0 + (int64_t)t * 8 * K4;
-    for (int r = 0; r < 8; ++r) {
-      for (int i = tid; i < K4; i += 256) {
-        const int pp = r + 8 * i;
-        float v = 0.0f;
-        if (pp < HWo) {
-          // oy = pp / oW: the float estimate (pp < 2^24, exact operands) is
-          // off by at most one either way; corrected
-          int oy = (int)((float)pp * inv_ow);
-          oy += (oy + 1) * oW <= pp;
-          oy -= oy * oW > pp;
-          const int ox = pp - oy * oW;
-          const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
-          if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) v = plane[iy * W + ix];
-        }
-        drow[(int64_t)r * K4 + kperm(i)] = v;
+  for (int tr = 0; tr < taps * 8; ++tr) {
+    const int t = tr >> 3, r = tr & 7, kr = t / kW, kc = t - kr * kW;
+    float* drow = drow0 + (int64_t)t * 8 * K4 + (int64_t)r * K4;
+    for (int i = i0 + tid; i < i1; i += 256) {
+      const int pp = r + 8 * i;
+      float v = 0.0f;
+      if (pp < HWo) {
+        // oy = pp / oW: the float estimate (pp < 2^24, exact operands) is
+        // off by at most one either way; corrected
+        int oy = (int)((float)pp * inv_ow);
+        oy += (oy + 1) * oW <= pp;
+        oy -= oy * oW > pp;
+        const int ox = pp - oy * oW;
+        const int ry = (oy - oy0) * sY + kr * dY, ix = ox * sX - pW + kc * dX;
+        if ((unsigned)ix < (unsigned)W) v = plane[ry * W + ix];
       }
+      drow[kperm(i)] = v;
     }
   }
 }
@@ -644,16 +651,25 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       });
     });
   };
-  // (the col' rows by input plane where a plane fits the block's LDS)
-  const bool by_plane = !d.direct && rowlen > 256 && d.g.H * d.g.W <= PLANE_MAX &&
-                        d.batch <= 65535 && d.g.C <= 0x7fffffff && d.K < (1 << 24);
-  if (by_plane) {
+  // (the col' rows by input band: the largest band of whole 256-pixel
+  // blocks, at most 4096 pixels, whose input rows fit the block's LDS)
+  int band = 0;
+  if (!d.direct && rowlen > 256 && d.K < (1 << 24) && d.g.C <= 65535) {
+    const ConvGeom& g = d.g;
+    for (int L = 4096; L >= 256 && !band; L -= 256) {
+      const int64_t orows = (L + g.ow - 1) / g.ow + 1;
+      if (((orows - 1) * g.sY + (g.kH - 1) * g.dY + 1) * g.W <= PLANE_MAX) band = L;
+    }
+  }
+  if (band) {
     if (hipError_t e = delta_rows(); e != hipSuccess) return e;
-    hipLaunchKernelGGL(im2col_res_plane_kernel, dim3((unsigned)d.g.C, (unsigned)d.batch),
-                       dim3(256), 0, s, d.x, d.xStride, d.dB, npad * rowlen, (int)d.g.C,
-                       (int)d.g.H, (int)d.g.W, (int)d.g.kH, (int)d.g.kW, (int)d.g.sY, (int)d.g.sX,
-                       (int)d.g.padH, (int)d.g.padW, (int)d.g.dY, (int)d.g.dX, (int)d.g.ow,
-                       (int)d.K, (int)K4, 1.0f / (float)d.g.ow);
+    const ConvGeom& g = d.g;
+    hipLaunchKernelGGL(im2col_res_band_kernel,
+                       dim3((unsigned)((rowlen + band - 1) / band), (unsigned)g.C, (unsigned)d.batch),
+                       dim3(256), 0, s, d.x, d.xStride, d.dB, npad * rowlen, (int)g.H, (int)g.W,
+                       (int)g.kH, (int)g.kW, (int)g.sY, (int)g.sX, (int)g.padH, (int)g.padW,
+                       (int)g.dY, (int)g.dX, (int)g.ow, (int)d.K, (int)K4, band,
+                       1.0f / (float)g.ow);
     if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   } else if (rowlen <= 256) {
     auto short_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {

@@ -382,7 +382,8 @@ def test_conv_backward_dw_tiles(hip, torch_cuda, ora):
 
 DWR_CASES = [(3, 128, 11, 128, 3, 1, 1, 9), (2, 64, 13, 64, 3, 1, 1, 9), (2, 64, 20, 128, 3, 2, 1, 1),
              (1, 128, 26, 256, 3, 1, 1, 9), (2, 64, 9, 64, 1, 1, 0, 4), (9, 64, 12, 64, 3, 1, 1, 9),
-             (2, 128, 10, 128, 3, 1, 1, 9, 2), (1, 32, 48, 64, 3, 1, 1, 9), (2, 3, 20, 64, 3, 1, 1, 1)]
+             (2, 128, 10, 128, 3, 1, 1, 9, 2), (1, 32, 48, 64, 3, 1, 1, 9), (2, 3, 20, 64, 3, 1, 1, 1),
+             (1, 16, 72, 64, 3, 1, 1, 9), (2, 16, 144, 64, 3, 2, 1, 1)]
 
 
 def test_conv_backward_dw_res_forms(hip, torch_cuda, ora):
@@ -391,8 +392,8 @@ def test_conv_backward_dw_res_forms(hip, torch_cuda, ora):
     over residue-major copies of delta and the im2col matrix, folded in sdot's
     order, images added in order): weight_updates (and state.delta, bias)
     bit-exact against the reference's per-image im2col + beta = 1 sdot loop;
-    k = 100 .. 2304 pixels (chains of 13 .. 288 terms: ragged last k-tiles),
-    stride 2, dilation 2, a 1x1 layer (the input planes rearranged), batch 9,
+    k = 100 .. 5184 pixels (chains of 13 .. 648 terms: ragged last k-tiles;
+    the col' rows in one or two input bands), stride 2, dilation 2, a 1x1 layer (the input planes rearranged), batch 9,
     col rows off the column tile (N = 27, 288, 576: padded rows); forms whose
     row tile does not divide the filters report UNSUPPORTED."""
     from tensorium_amd._abi import TnsError
