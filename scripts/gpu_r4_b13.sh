@@ -1,12 +1,12 @@
 #!/bin/bash
 # Round-4 batch 13: col' rows by input plane (dw_res): conv tests, the dW
-# kernels on layers 6 / 9 / 11 / 28 under a kernel trace, the bench.
+# kernels on layers 3 / 4 / 6 / 9 / 11 / 28 under a kernel trace, the bench.
 set -u
 mkdir -p gpurun_out/dwres7
 timeout -k 10 400 python -u -m pytest tests/test_gpu_conv.py -x -q --timeout 120 --timeout-method thread > gpurun_out/b13_tests.log 2>&1
 rc=$?; echo "conv tests rc=$rc"; tail -2 gpurun_out/b13_tests.log; [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
-for L in 6 9 11 28; do
+for L in 3 4 6 9 11 28; do
   (cd /tmp && timeout -k 10 150 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/dwres7/l$L -o l$L --output-format csv -- python3 $GRAFT_REPO_ROOT/scripts/dw_res_prof.py --layer $L > $GRAFT_REPO_ROOT/gpurun_out/dwres7/l$L.json 2> $GRAFT_REPO_ROOT/gpurun_out/dwres7/l$L.err) || exit $?
   echo "layer $L ok"; cat gpurun_out/dwres7/l$L.json | cut -c1-400
 done
