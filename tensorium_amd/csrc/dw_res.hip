@@ -584,7 +584,9 @@ int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 31) / 32 * 32; }
 // residue-register kernel at 26^2 / 13^2, im2col + the sdot kernel on the
 // long-k planes):
 //   k <= 1024 (26^2, 13^2 planes): all 8 residues in one 64 x 64 block, one
-//     partial plane (26^2 0.221 -> 0.191 ms, 13^2 0.309 -> 0.275); the
+//     partial plane (26^2 0.221 -> 0.191 ms, 13^2 0.309 -> 0.275; the
+//     image-folded form, no partial planes, runs the 13^2 layers in 0.289
+//     against 0.269, profiles/r04_dw_res_forms6); the
 //     one-residue forms make 8 planes of these large outputs to add, and the
 //     26^2 product runs 0.26-0.27 with them;
 //   k <= 4096 (52^2): one residue a block, 128 x 64 (0.213 -> 0.194);
@@ -594,7 +596,6 @@ int64_t dw_res_k4(int64_t K) { return ((K + 7) / 8 + 31) / 32 * 32; }
 int dw_res_pick(int64_t M, int64_t N, int64_t K, int64_t batch) {
   (void)N;
   if (M % 64 || batch < 1 || K < 64) return -1;
-  if (K <= 256) return 9;
   if (K <= 1024) return 5;
   if (K <= 4096) return M % 128 == 0 ? 7 : 6;
   return 6;
