@@ -465,16 +465,16 @@ __global__ __launch_bounds__(256) void res_permute_short_kernel(
 // The rearranged im2col matrix by input band: a block stages the input rows
 // under one band of L output pixels of one image's channel plane in LDS
 // (read once, coalesced), then writes that band of the channel's kH*kW col'
-// rows from it — per tap and residue a run of L/8 consecutive i (the
-// row-chunk kernel above reads every plane element once per tap from L2).
-// L is a multiple of 256 (whole kperm blocks), the band's input rows at most
-// PLANE_MAX floats.
-constexpr int PLANE_MAX = 16384;
+// rows from it — per tap and residue a run of L/8 consecutive i, the runs
+// dealt to the threads as one flat range (the row-chunk kernel above reads
+// every plane element once per tap from L2).  L is a multiple of 256 (whole
+// kperm blocks); the LDS holds the band's input rows (dynamic, sized by the
+// host to the largest band).
 __global__ __launch_bounds__(256) void im2col_res_band_kernel(
     const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int H,
     int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
     int K4, int L, float inv_ow) {
-  __shared__ float plane[PLANE_MAX];
+  extern __shared__ float plane[];
   const int band = blockIdx.x, c = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
   const int p0 = band * L, p1 = min(p0 + L, 8 * K4);
   // input rows under output rows oy0..oy1 (the last pixel clamped to the plane)
@@ -486,25 +486,29 @@ __global__ __launch_bounds__(256) void im2col_res_band_kernel(
     plane[e] = (unsigned)iy < (unsigned)H ? xc[iy * W + (e - ry * W)] : 0.0f;
   }
   __syncthreads();
-  const int taps = kH * kW, i0 = p0 >> 3, i1 = p1 >> 3;
-  float* drow0 = dst + b * dstImg + (int64_t)c * taps * 8 * K4;
-  for (int tr = 0; tr < taps * 8; ++tr) {
+  const int i0 = p0 >> 3, ni = (p1 - p0) >> 3, runs = kH * kW * 8;
+  float* drow0 = dst + b * dstImg + (int64_t)c * kH * kW * 8 * K4;
+  // thread's position in the flat range (run tr, i = i0 + j), advanced by 256
+  int tr = tid / ni, j = tid - tr * ni;
+  while (tr < runs) {
     const int t = tr >> 3, r = tr & 7, kr = t / kW, kc = t - kr * kW;
-    float* drow = drow0 + (int64_t)t * 8 * K4 + (int64_t)r * K4;
-    for (int i = i0 + tid; i < i1; i += 256) {
-      const int pp = r + 8 * i;
-      float v = 0.0f;
-      if (pp < HWo) {
-        // oy = pp / oW: the float estimate (pp < 2^24, exact operands) is
-        // off by at most one either way; corrected
-        int oy = (int)((float)pp * inv_ow);
-        oy += (oy + 1) * oW <= pp;
-        oy -= oy * oW > pp;
-        const int ox = pp - oy * oW;
-        const int ry = (oy - oy0) * sY + kr * dY, ix = ox * sX - pW + kc * dX;
-        if ((unsigned)ix < (unsigned)W) v = plane[ry * W + ix];
-      }
-      drow[kperm(i)] = v;
+    const int i = i0 + j, pp = r + 8 * i;
+    float v = 0.0f;
+    if (pp < HWo) {
+      // oy = pp / oW: the float estimate (pp < 2^24, exact operands) is off
+      // by at most one either way; corrected
+      int oy = (int)((float)pp * inv_ow);
+      oy += (oy + 1) * oW <= pp;
+      oy -= oy * oW > pp;
+      const int ox = pp - oy * oW;
+      const int ry = (oy - oy0) * sY + kr * dY, ix = ox * sX - pW + kc * dX;
+      if ((unsigned)ix < (unsigned)W) v = plane[ry * W + ix];
+    }
+    drow0[(int64_t)tr * K4 + kperm(i)] = v;  // (t * 8 + r) * K4: tap t's residue r
+    j += 256;
+    while (j >= ni) {
+      j -= ni;
+      ++tr;
     }
   }
 }
@@ -653,13 +657,16 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
     });
   };
   // (the col' rows by input band: the largest band of whole 256-pixel
-  // blocks, at most 4096 pixels, whose input rows fit the block's LDS)
+  // blocks, at most 4096 pixels, whose input rows take at most 24 KB of LDS,
+  // so that several blocks share a CU)
   int band = 0;
+  size_t band_lds = 0;
   if (!d.direct && rowlen > 256 && d.K < (1 << 24) && d.g.C <= 65535) {
     const ConvGeom& g = d.g;
-    for (int L = 4096; L >= 256 && !band; L -= 256) {
+    for (int64_t L = std::min<int64_t>(4096, rowlen); L >= 256 && !band; L -= 256) {
       const int64_t orows = (L + g.ow - 1) / g.ow + 1;
-      if (((orows - 1) * g.sY + (g.kH - 1) * g.dY + 1) * g.W <= PLANE_MAX) band = L;
+      const int64_t bytes = ((std::min(orows, g.oh) - 1) * g.sY + (g.kH - 1) * g.dY + 1) * g.W * 4;
+      if (bytes <= 24 * 1024) band = (int)L, band_lds = (size_t)bytes;
     }
   }
   if (band) {
@@ -667,7 +674,7 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
     const ConvGeom& g = d.g;
     hipLaunchKernelGGL(im2col_res_band_kernel,
                        dim3((unsigned)((rowlen + band - 1) / band), (unsigned)g.C, (unsigned)d.batch),
-                       dim3(256), 0, s, d.x, d.xStride, d.dB, npad * rowlen, (int)g.H, (int)g.W,
+                       dim3(256), band_lds, s, d.x, d.xStride, d.dB, npad * rowlen, (int)g.H, (int)g.W,
                        (int)g.kH, (int)g.kW, (int)g.sY, (int)g.sX, (int)g.padH, (int)g.padW,
                        (int)g.dY, (int)g.dX, (int)g.ow, (int)d.K, (int)K4, band,
                        1.0f / (float)g.ow);
