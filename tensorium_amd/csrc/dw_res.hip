@@ -93,7 +93,17 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid >> 1, wn = wid & 1, l31 = lane & 31, h = lane >> 5;
   const int tiles_m = p.M / BM;
-  const int m0 = (int)(blockIdx.x % tiles_m) * BM, n0 = (int)(blockIdx.x / tiles_m) * BN;
+  // XCD-contiguous tiles (blocks go to the 8 XCDs round-robin): each XCD
+  // takes one contiguous run of the m-fastest tile list — a few column tiles
+  // with every row tile — so its L2 holds those col' rows while delta'
+  // streams past, instead of every XCD streaming all of col'
+  int tile;
+  {
+    const int nb = (int)gridDim.x, bid = (int)blockIdx.x;
+    const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
+    tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  }
+  const int m0 = (tile % tiles_m) * BM, n0 = (tile / tiles_m) * BN;
   const int g = blockIdx.y;
   const int64_t img = IF ? 0 : blockIdx.z;
   const int64_t ld = 8LL * p.K4;  // row stride, floats
@@ -164,7 +174,7 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[i][st], f.b[j][st], acc[i][j], 0,
                                                            0, 0);
   };
-  // step groups 0 .. groups-2 of a k-tile (4 groups, or `groups`, 2 or 4,
+  // step groups 0 .. groups-2 of a k-tile (4 groups, or `groups`, 1 .. 4,
   // for a chain's last tile: the rest is zero padding) from fragments f0 =
   // group 0; leaves the last group's fragments in f1 (its MFMAs are issued
   // by the caller, after the barrier)
@@ -172,13 +182,15 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   auto compute = [&](const float* st, int groups) {
 #pragma unroll
     for (int q = 0; q < RBK / 8; q += 2) {
-      if (q < groups) {  // (wave-uniform)
+      if (q + 1 < groups) {  // (wave-uniform)
         frag(st, q + 1, f1);
         mma(f0);
         if (q + 2 < groups) {
           frag(st, q + 2, f0);
           mma(f1);
         }
+      } else if (q + 1 == groups) {
+        f1 = f0;  // (an odd count: group q is the last)
       }
     }
   };
@@ -211,9 +223,11 @@ __global__ __launch_bounds__(256, 2) void dw_res_kernel(
   };
 
   const int nt = (p.K1 + RBK - 1) / RBK;
-  // the last tile's step groups: its k rounded up to 16 (K4 is a multiple of
-  // 32, so the rest of the tile is zero)
-  const int last_groups = 2 * ((p.K1 - (nt - 1) * RBK + 15) / 16);
+  // the last tile's step groups: its k rounded up to 8 (K4 is a multiple of
+  // 32, so the rest of the tile is zero; the chain's masked tail element,
+  // i = K1 - 1, is always run: sdot's one fma(0, 0, lane) on the residues
+  // past K, and the further zero steps of the group leave the lane as it is)
+  const int last_groups = (p.K1 - (nt - 1) * RBK + 7) / 8;
   const int TI1 = R * nt;                // tiles of one image
   const int T = IF ? p.batch * TI1 : TI1;
   // the barrier that publishes tile t+1 sits before tile t's last step: tile
