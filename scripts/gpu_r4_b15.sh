@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 batch 15: dw_res last k-tile by 8, XCD-contiguous tiles (+ the band kernel):
+# Round-4 batch 15: dw_res last k-tile by 8, XCD-contiguous tiles, 16-byte col' writes:
 # kernels on layers 3 / 4 / 6 / 9 / 11 / 28 under a kernel trace, the bench.
 set -u
 mkdir -p gpurun_out/dwres9

@@ -394,11 +394,22 @@ __device__ __forceinline__ void res_chunk(Src&& src, float* __restrict__ drow, i
     t[(pl & 7) * RLD + (pl >> 3)] = v[j];
   }
   __syncthreads();
-  if (tid < CH / 8) {
-    const int i = (int)blockIdx.x * (CH / 8) + tid;
-    if (i < K4) {
+  // written as 16-byte pieces: piece a of a 32-element block holds elements
+  // e = (a >> 2) + 8 (a & 3) + 2 b, b = 0..3 (kperm); a residue's CH/8
+  // elements are CH/32 consecutive pieces
+  constexpr int PIECES = CH / 32;  // per residue
+  const int i0 = (int)blockIdx.x * (CH / 8);
 #pragma unroll
-      for (int r = 0; r < 8; ++r) drow[(int64_t)r * K4 + kperm(i)] = t[r * RLD + tid];
+  for (int u = 0; u < (8 * PIECES + 255) / 256; ++u) {
+    const int idx = tid + 256 * u;
+    if (8 * PIECES % 256 == 0 || idx < 8 * PIECES) {
+      const int r = idx / PIECES, pc = idx - r * PIECES, kb = pc >> 3, a = pc & 7;
+      if (i0 + 32 * kb < K4) {
+        const int e = 32 * kb + (a >> 2) + 8 * (a & 3);
+        const float* tr = t + r * RLD + e;
+        *reinterpret_cast<float4*>(drow + (int64_t)r * K4 + i0 + 4 * pc) =
+            make_float4(tr[0], tr[2], tr[4], tr[6]);
+      }
     }
   }
 }
@@ -473,57 +484,6 @@ __global__ __launch_bounds__(256) void res_permute_short_kernel(
     if (ra >= total) break;
     const int b = ra / rows, row = ra - b * rows;
     dst[b * dstImg + (int64_t)row * 8 * K4 + off] = v[j];
-  }
-}
-
-// The rearranged im2col matrix by input band: a block stages the input rows
-// under one band of L output pixels of one image's channel plane in LDS
-// (read once, coalesced), then writes that band of the channel's kH*kW col'
-// rows from it — per tap and residue a run of L/8 consecutive i, the runs
-// dealt to the threads as one flat range (the row-chunk kernel above reads
-// every plane element once per tap from L2).  L is a multiple of 256 (whole
-// kperm blocks); the LDS holds the band's input rows (dynamic, sized by the
-// host to the largest band).
-__global__ __launch_bounds__(256) void im2col_res_band_kernel(
-    const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int H,
-    int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
-    int K4, int L, float inv_ow) {
-  extern __shared__ float plane[];
-  const int band = blockIdx.x, c = blockIdx.y, b = blockIdx.z, tid = threadIdx.x;
-  const int p0 = band * L, p1 = min(p0 + L, 8 * K4);
-  // input rows under output rows oy0..oy1 (the last pixel clamped to the plane)
-  const int oy0 = min(p0, HWo - 1) / oW, oy1 = (min(p1, HWo) - 1) / oW;
-  const int iy0 = oy0 * sY - pH, nrows = (oy1 - oy0) * sY + (kH - 1) * dY + 1;
-  const float* xc = x + b * xImg + (int64_t)c * H * W;
-  for (int e = tid; e < nrows * W; e += 256) {
-    const int ry = e / W, iy = iy0 + ry;
-    plane[e] = (unsigned)iy < (unsigned)H ? xc[iy * W + (e - ry * W)] : 0.0f;
-  }
-  __syncthreads();
-  const int i0 = p0 >> 3, ni = (p1 - p0) >> 3, runs = kH * kW * 8;
-  float* drow0 = dst + b * dstImg + (int64_t)c * kH * kW * 8 * K4;
-  // thread's position in the flat range (run tr, i = i0 + j), advanced by 256
-  int tr = tid / ni, j = tid - tr * ni;
-  while (tr < runs) {
-    const int t = tr >> 3, r = tr & 7, kr = t / kW, kc = t - kr * kW;
-    const int i = i0 + j, pp = r + 8 * i;
-    float v = 0.0f;
-    if (pp < HWo) {
-      // oy = pp / oW: the float estimate (pp < 2^24, exact operands) is off
-      // by at most one either way; corrected
-      int oy = (int)((float)pp * inv_ow);
-      oy += (oy + 1) * oW <= pp;
-      oy -= oy * oW > pp;
-      const int ox = pp - oy * oW;
-      const int ry = (oy - oy0) * sY + kr * dY, ix = ox * sX - pW + kc * dX;
-      if ((unsigned)ix < (unsigned)W) v = plane[ry * W + ix];
-    }
-    drow0[(int64_t)tr * K4 + kperm(i)] = v;  // (t * 8 + r) * K4: tap t's residue r
-    j += 256;
-    while (j >= ni) {
-      j -= ni;
-      ++tr;
-    }
   }
 }
 
@@ -670,30 +630,7 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       });
     });
   };
-  // (the col' rows by input band: the largest band of whole 256-pixel
-  // blocks, at most 4096 pixels, whose input rows take at most 24 KB of LDS,
-  // so that several blocks share a CU)
-  int band = 0;
-  size_t band_lds = 0;
-  if (!d.direct && rowlen > 256 && d.K < (1 << 24) && d.g.C <= 65535) {
-    const ConvGeom& g = d.g;
-    for (int64_t L = std::min<int64_t>(4096, rowlen); L >= 256 && !band; L -= 256) {
-      const int64_t orows = (L + g.ow - 1) / g.ow + 1;
-      const int64_t bytes = ((std::min(orows, g.oh) - 1) * g.sY + (g.kH - 1) * g.dY + 1) * g.W * 4;
-      if (bytes <= 24 * 1024) band = (int)L, band_lds = (size_t)bytes;
-    }
-  }
-  if (band) {
-    if (hipError_t e = delta_rows(); e != hipSuccess) return e;
-    const ConvGeom& g = d.g;
-    hipLaunchKernelGGL(im2col_res_band_kernel,
-                       dim3((unsigned)((rowlen + band - 1) / band), (unsigned)g.C, (unsigned)d.batch),
-                       dim3(256), band_lds, s, d.x, d.xStride, d.dB, npad * rowlen, (int)g.H, (int)g.W,
-                       (int)g.kH, (int)g.kW, (int)g.sY, (int)g.sX, (int)g.padH, (int)g.padW,
-                       (int)g.dY, (int)g.dX, (int)g.ow, (int)d.K, (int)K4, band,
-                       1.0f / (float)g.ow);
-    if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
-  } else if (rowlen <= 256) {
+  if (rowlen <= 256) {
     auto short_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
       const int64_t groups = (nrows + 7) / 8;
       for (int64_t g0 = 0; g0 < groups; g0 += 65535) {
