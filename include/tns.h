@@ -586,7 +586,15 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * (which then holds dW's col matrix only); if that allocation fails, or the
  * side stream cannot be created, the call runs in sequence within the
  * caller's workspace instead of failing.  Set 0 to bound the backward's
- * memory to the workspace. */
+ * memory to the workspace.  2 = pipelined: each call enqueues its dW on the
+ * side stream (behind the earlier calls' dW) and returns without joining it;
+ * the next call of ANY other entry point (and tns_hip_finish) first makes the
+ * context's stream wait for the side stream.  The dW of layer L then runs
+ * under the following calls' derive / state.delta work — the caller must not
+ * modify a pending call's input, delta or weight_updates by other means (work
+ * enqueued on the stream outside this API, or host writes) before such a
+ * join; a backward pass of the layers below reads none of them.  Same
+ * results; state.delta always gets its own col buffer (the memory note above). */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,

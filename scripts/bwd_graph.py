@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """The bench's 75-layer YOLOv3 conv backward (batch 8, bench.py
-bench_conv_backward) timed four ways: per-call launches with the dW / dX
-overlap on and off, and the same call sequence captured once into a HIP graph
-and replayed (overlap on / off).  The graph replays the very kernels the calls
+bench_conv_backward) timed five ways: per-call launches with the dW / dX
+overlap on (1), off (0) and pipelined (2: each dW left on the side stream),
+and the same call sequence captured once into a HIP graph and replayed
+(overlap 1 / 0).  The graph replays the very kernels the calls
 launch, with the same arguments; the replay's weight_updates, bias_updates
 and state.delta are checked bit-identical to the per-call pass from the same
 starting state.  One JSON line.
@@ -60,21 +61,24 @@ def main():
             for t, v in zip([t for t in L[4:] if t is not None], sv):
                 t.copy_(v)
 
-    def timed(fn):
+    def timed(fn, join=False):
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(cap)
         for _ in range(a.steps):
             fn()
+        if join:  # the pipelined schedule's last dW products inside the region
+            hip.finish()
         e1.record(cap)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / a.steps
 
     row = {"layers": len(specs), "batch": B, "steps": a.steps}
     with torch.cuda.stream(cap):
-        for ov in (True, False):  # every scratch buffer and the side stream exist
+        for ov in (1, 0, 2):  # every scratch buffer and the side stream exist
             hip.setBwdOverlap(ov)
             step()
+            hip.finish()
         torch.cuda.synchronize()
         graphs = {}
         for ov in (True, False):
@@ -97,13 +101,24 @@ def main():
             got = state()
             same = all(torch.equal(p, q) for r1, r2 in zip(ref, got) for p, q in zip(r1, r2))
             row[f"graph_overlap{int(ov)}_bit_identical"] = bool(same)
-        times = {k: [] for k in ("calls_overlap1", "calls_overlap0", "graph_overlap1",
-                                 "graph_overlap0")}
+        # the pipelined schedule (2) per call against the same reference
+        restore(snap)
+        hip.setBwdOverlap(2)
+        step()
+        hip.finish()
+        torch.cuda.synchronize()
+        got = state()
+        row["calls_overlap2_bit_identical"] = bool(
+            all(torch.equal(p, q) for r1, r2 in zip(ref, got) for p, q in zip(r1, r2)))
+        times = {k: [] for k in ("calls_overlap1", "calls_overlap0", "calls_overlap2",
+                                 "graph_overlap1", "graph_overlap0")}
         for _ in range(a.rounds):
             for ov in (True, False):
                 hip.setBwdOverlap(ov)
                 times[f"calls_overlap{int(ov)}"].append(timed(step))
                 times[f"graph_overlap{int(ov)}"].append(timed(graphs[ov].replay))
+            hip.setBwdOverlap(2)
+            times["calls_overlap2"].append(timed(step, join=True))
         hip.setBwdOverlap(True)
     for k, v in times.items():
         row[k + "_ms"] = round(min(v), 3)

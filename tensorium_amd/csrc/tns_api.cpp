@@ -84,6 +84,10 @@ struct tns_ctx {
   // stream while the dW product runs on `stream` (fork / join events)
   hipStream_t aux_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // TNS_OPT_BWD_OVERLAP = 2: dW products left running on aux_stream past the
+  // call's return; the next call of any other entry point joins them first
+  bool side_pending = false;
+  hipStream_t home_stream = nullptr;  // the context's stream while `stream` is aux
   // implicit-GEMM conv k-tables, one per (C, H, W, kH, kW, dY, dX)
   std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int*> ktabs;
 };
@@ -101,6 +105,7 @@ int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
     if (c->scratch[slot]) {
       hipStreamSynchronize(c->stream);
       if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+      if (c->home_stream) hipStreamSynchronize(c->home_stream);
       hipFree(c->scratch[slot]);
       c->scratch[slot] = nullptr;
       c->scratch_elems[slot] = 0;
@@ -155,9 +160,22 @@ struct OpTimer {
   }
 };
 
-int check_ctx(tns_ctx* c) {
-  if (!c) return set_error(TNS_ERR_ARG, "null tns_ctx");
+// the dW products a pipelined conv backward (TNS_OPT_BWD_OVERLAP = 2) left
+// on the side stream: the context's stream waits for them from here on
+int join_side(tns_ctx* c) {
+  if (!c->side_pending) return TNS_OK;
+  c->side_pending = false;
+  hipError_t e = hipEventRecord(c->ev_join, c->aux_stream);
+  if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_join, 0);
+  if (e != hipSuccess) return set_error(TNS_ERR_HIP, "backward join: %s", hipGetErrorString(e));
   return TNS_OK;
+}
+
+// every entry point: the context exists, and earlier calls' side-stream work
+// is ordered before whatever this call enqueues
+int check_ctx(tns_ctx* c, bool join = true) {
+  if (!c) return set_error(TNS_ERR_ARG, "null tns_ctx");
+  return join ? join_side(c) : TNS_OK;
 }
 
 int hip_status(hipError_t e, const char* what) {
@@ -585,7 +603,7 @@ int tns_set_option(int32_t opt, int64_t value) {
       g_dx_fused = value < 0 ? 1 : (value > 2 ? 2 : value);
       return TNS_OK;
     case TNS_OPT_BWD_OVERLAP:
-      g_bwd_overlap = value ? 1 : 0;
+      g_bwd_overlap = value <= 0 ? 0 : (value >= 2 ? 2 : 1);
       return TNS_OK;
     case TNS_OPT_DW_TILE:
       if (value >= dw_tile_count()) return set_error(TNS_ERR_ARG, "no dW tile %lld", (long long)value);
@@ -638,6 +656,7 @@ int tns_hip_destroy(tns_ctx* c) {
   if (!c) return TNS_OK;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
   for (int i = 0; i < tns_ctx::kSlots; ++i)
     if (c->scratch[i]) hipFree(c->scratch[i]);
   for (auto& kv : c->ktabs) hipFree(kv.second);
@@ -1583,7 +1602,10 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
                        const float* output, float* delta, float* bias_updates,
                        float* weight_updates, float* workspace, float* state_delta,
                        const ConvBN& bn) {
-  if (int r = check_ctx(c)) return r;
+  // (pipelined mode: this call's dW queues behind the pending ones on the
+  // side stream; its other work touches none of their operands)
+  const bool pipe = g_bwd_overlap == 2 && !c->telemetry && ensure_side_stream(c);
+  if (int r = check_ctx(c, !pipe)) return r;
   if (!act_supported(activation))
     return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
   // delta / output are [batch][filters][outH*outW] with the layer's outH =
@@ -1691,7 +1713,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // side stream (fork / join events), each with its own col buffer —
   // nothing changes in either result.  Telemetry times ops one by one, so it
   // keeps them in sequence.
-  bool overlap = state_delta && g_bwd_overlap && !c->telemetry && ensure_side_stream(c);
+  bool overlap = !pipe && state_delta && g_bwd_overlap && !c->telemetry && ensure_side_stream(c);
   const bool dw_col = needs_col && dwv < 0 && dwr < 0;  // dW reads an im2col matrix
   // state.delta's own col buffer when both chains need one at once (the
   // overlap's extra memory, tns.h); if it cannot be had, the sequential
@@ -1702,8 +1724,12 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     tns_clear_error();
     overlap = false;
   }
+  // (pipelined: state.delta's chain always has its own col buffer — the
+  // pending dW products may still read the shared one)
+  if (pipe && dx_col)
+    if (int r = ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) return r;
   float* ws = workspace;
-  if (!ws && (dw_col || (dx_col && !(overlap && dw_col))))
+  if (!ws && (dw_col || (dx_col && !dx_ws && !(overlap && dw_col))))
     if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws)) return r;
   if (!dx_ws) dx_ws = ws;  // col buffer of state.delta's chain
   // scratch of the fused state.delta kernel, sized before any fork (a growth
@@ -1839,6 +1865,23 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
                       "col2im launch");
   };
 
+  if (pipe) {
+    // dW enqueued on the side stream behind the earlier calls' (fork: after
+    // this call's derive / bias sums), state.delta's chain on the context's
+    // stream; no join — the side stream's work is joined by the next call of
+    // any other entry point (tns.h TNS_OPT_BWD_OVERLAP)
+    TNS_HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
+    TNS_HIP_TRY(hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+    hipStream_t main = c->stream;
+    c->home_stream = main;
+    c->stream = c->aux_stream;
+    const int rw = run_dw();
+    c->stream = main;
+    c->home_stream = nullptr;
+    c->side_pending = true;
+    if (rw) return rw;
+    return state_delta ? run_dx() : TNS_OK;
+  }
   if (!overlap) {
     if (int r = run_dw()) return r;
     return state_delta ? run_dx() : TNS_OK;

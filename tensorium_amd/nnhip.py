@@ -355,10 +355,14 @@ class TNNHip:
         """Implicit transposed-convolution forms of the backward's state.delta."""
         return int(self.lib.tns_conv_dx_conv_count())
 
-    def setBwdOverlap(self, on: bool = True):
-        """Conv backward: dW and state.delta concurrently on two streams (1)
-        or in sequence (0); same results; process-wide."""
-        check(self.lib.tns_set_option(10, 1 if on else 0))
+    def setBwdOverlap(self, mode=True):
+        """Conv backward: dW and state.delta concurrently on two streams,
+        joined before the call returns (1 / True), in sequence (0 / False), or
+        pipelined (2: each call's dW left running on the side stream behind
+        the earlier ones, joined by the next call of any other entry point);
+        same results; process-wide."""
+        m = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
+        check(self.lib.tns_set_option(10, m))
 
     def convDwTiles(self) -> int:
         """Implicit-im2col dW tiles of the conv backward."""

@@ -311,6 +311,45 @@ def test_conv_backward_overlap_matches_sequential(hip, torch_cuda, ora, idx):
             assert np.array_equal(a, r)
 
 
+def test_conv_backward_pipelined_chain(hip, torch_cuda):
+    """TNS_OPT_BWD_OVERLAP = 2 over a chain of YOLOv3 layers (43 .. 46, run
+    in backward order, each layer's state.delta the delta of the layer below
+    and its input that layer's output): every call's dW is left running on
+    the side stream while the next calls' derive / bias sums / state.delta
+    work proceeds; every delta, bias / weight update and the chain's
+    state.delta bit-identical to the sequential schedule (0)."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    specs = [yolov3_conv_table()[i] for i in (43, 44, 45, 46)]
+    B = 8
+    rng = np.random.default_rng(4346)
+    x0 = rng.uniform(0, 1, (B, specs[0].c, specs[0].h, specs[0].h)).astype(np.float32)
+    outs = [rng.uniform(-1, 1, (B, s.filters, s.out_h, s.out_h)).astype(np.float32) for s in specs]
+    deltas = [rng.uniform(-1, 1, o.shape).astype(np.float32) for o in outs]
+    sd0 = np.zeros_like(x0)
+    ws = [rng.uniform(-0.1, 0.1, (s.filters, s.K)).astype(np.float32) for s in specs]
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    got = {}
+    try:
+        for mode in (0, 2):
+            hip.setBwdOverlap(mode)
+            X, O, D, W = t(x0), [t(o) for o in outs], [t(d) for d in deltas], [t(w) for w in ws]
+            SD = t(sd0)
+            BU = [torch_cuda.zeros(s.filters, device="cuda") for s in specs]
+            WU = [torch_cuda.zeros(s.filters, s.K, device="cuda") for s in specs]
+            for j in range(len(specs) - 1, -1, -1):
+                s = specs[j]
+                inp = X if j == 0 else O[j - 1]
+                sd = SD if j == 0 else D[j - 1]
+                hip.convBackward(B, s.c, s.h, s.h, inp, W[j], s.filters, s.size, s.stride, s.pad,
+                                 1, s.activation, O[j], D[j], BU[j], WU[j], None, sd)
+            hip.finish()
+            got[mode] = [a.cpu().numpy() for a in D + BU + WU + [SD]]
+    finally:
+        hip.setBwdOverlap(True)
+    for a, b in zip(got[0], got[2]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("idx", [3, 10, 11, 27, 28, 44, 45, 58])
 def test_conv_backward_dx_yolov3_batch8(hip, torch_cuda, ora, idx):
     """state.delta at YOLOv3 layer shapes, batch 8, on the default path (the
