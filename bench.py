@@ -498,15 +498,26 @@ def bench_conv_backward(torch, hip, ctx, rank, steps=2):
             hip.convBackward(batch, s.c, s.h, s.h, x, w, s.filters, s.size, s.stride, s.pad, 1,
                              s.activation, out, delta, bu, wu, ws, sd)
 
-    step()
-    torch.cuda.synchronize()
-    ctx.barrier()
-    t0 = time.perf_counter()
-    for _ in range(steps):
+    def timed_pass(mode):
+        # TNS_OPT_BWD_OVERLAP: 2 = pipelined (each layer's dW left running on
+        # the context's side stream under the next layers' work; the device
+        # synchronize below waits for all of it), 1 = dW and state.delta
+        # concurrent within each call, joined before it returns
+        hip.setBwdOverlap(mode)
         step()
-    torch.cuda.synchronize()
-    ctx.barrier()
-    wall = ctx.max((time.perf_counter() - t0) / steps)
+        torch.cuda.synchronize()
+        ctx.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        return ctx.max((time.perf_counter() - t0) / steps)
+
+    wall_joined = timed_pass(1)
+    wall = timed_pass(2)
+    hip.setBwdOverlap(1)
+    hip.finish()
     from tensorium_amd._abi import TNS_OP_GEMM, TNS_OP_IM2COL, TNS_OP_COL2IM
     hip.setTelemetry(True)
     step()
@@ -518,6 +529,9 @@ def bench_conv_backward(torch, hip, ctx, rank, steps=2):
     del layers, ws
     torch.cuda.empty_cache()
     return {"layers": len(specs), "batch_per_gpu": batch, "ms_per_batch": round(wall * 1e3, 3),
+            "schedule": "pipelined (TNS_OPT_BWD_OVERLAP = 2: each layer's dW on the side "
+                        "stream under the following layers' work)",
+            "ms_per_batch_joined": round(wall_joined * 1e3, 3),
             "gflop_per_batch": round(gflop, 2), "tflops": round(gflop / wall / 1e3, 2),
             "images_per_s_total": round(ctx.world * batch / wall, 1),
             "telemetry_split": split}
