@@ -1604,7 +1604,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
                        const ConvBN& bn) {
   // (pipelined mode: this call's dW queues behind the pending ones on the
   // side stream; its other work touches none of their operands)
-  const bool pipe = g_bwd_overlap == 2 && !c->telemetry && ensure_side_stream(c);
+  bool pipe = g_bwd_overlap == 2 && !c->telemetry && ensure_side_stream(c);
   if (int r = check_ctx(c, !pipe)) return r;
   if (!act_supported(activation))
     return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
@@ -1726,8 +1726,14 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   }
   // (pipelined: state.delta's chain always has its own col buffer — the
   // pending dW products may still read the shared one)
-  if (pipe && dx_col)
-    if (int r = ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) return r;
+  // (if that buffer cannot be had: the pending dW joined, this call in
+  // sequence within the caller's workspace)
+  if (pipe && dx_col && ensure_scratch(c, SLOT_COL_DX, batch * colSize, &dx_ws)) {
+    tns_clear_error();
+    dx_ws = nullptr;
+    pipe = false;
+    if (int r = join_side(c)) return r;
+  }
   float* ws = workspace;
   if (!ws && (dw_col || (dx_col && !dx_ws && !(overlap && dw_col))))
     if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws)) return r;
