@@ -302,7 +302,11 @@ __global__ void vssum_k(int64_t n, const float* __restrict__ a, float* __restric
 // first 8 (or 16) lanes of wave 0 run the lane chains out of LDS.  The block
 // results go to part[block] (block = g*N + i, memory order) and a per-channel
 // pass adds them in group order.
-enum ChainMode { CH_SUM = 0, CH_SRSS = 1, CH_VDELTA = 2, CH_DOT = 3 };
+// CH_DSUM: CH_SUM over delta * f'(output) — the conv backward's Derivative
+// fused into its bias sums: a = delta (each derived term also written back
+// through wa), b = output, act = the activation; the same product as
+// derive4_kernel, the same chains as CH_SUM
+enum ChainMode { CH_SUM = 0, CH_SRSS = 1, CH_VDELTA = 2, CH_DOT = 3, CH_DSUM = 4 };
 
 template <int MODE, int NT, int E>
 __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
@@ -310,9 +314,11 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
                                                    const float* __restrict__ mu_arr,
                                                    int64_t nblocks, int64_t N, int64_t bs,
                                                    int quirk, float* __restrict__ part0,
-                                                   float* __restrict__ part1) {
+                                                   float* __restrict__ part1, int act,
+                                                   float* wa) {
   constexpr int TILE = NT * E;
   constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;  // two LDS streams
+  constexpr bool LB = TWO || MODE == CH_DSUM;                // b loaded
   // tiles stored lane-major: element e of the tile at (e & 7) * LDT + e / 8,
   // so a chain lane's consecutive terms are contiguous (ds_read_b128 reads
   // four); rows padded by 8 floats (conflict-free staging stores)
@@ -328,23 +334,29 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
   for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
     const int64_t i = blk % N;
     const float* pa = a + blk * bs;
-    const float* pb = TWO ? b + blk * bs : nullptr;
+    const float* pb = LB ? b + blk * bs : nullptr;
+    float* pw = MODE == CH_DSUM ? wa + blk * bs : nullptr;
     const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA) ? mu_arr[i] : 0.0f;
-    float ra[E], rb[TWO ? E : 1];
+    float ra[E], rb[LB ? E : 1];
     auto load = [&](int t) {
       const int64_t base = (int64_t)t * TILE + tid;
 #pragma unroll
       for (int u = 0; u < E; ++u) {
         const int64_t k = base + NT * u;
         ra[u] = k < nb8 ? pa[k] : 0.0f;
-        if constexpr (TWO) rb[u] = k < nb8 ? pb[k] : 0.0f;
+        if constexpr (LB) rb[u] = k < nb8 ? pb[k] : 0.0f;
       }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int t) {
 #pragma unroll
       for (int u = 0; u < E; ++u) {
         const int e = ((tid + NT * u) & 7) * LDT + ((tid + NT * u) >> 3);
-        if constexpr (MODE == CH_SUM) {
+        if constexpr (MODE == CH_DSUM) {
+          const float d = ra[u] * grad_apply(rb[u], act);
+          U[buf][e] = d;
+          const int64_t k = (int64_t)t * TILE + tid + NT * u;
+          if (k < nb8) pw[k] = d;
+        } else if constexpr (MODE == CH_SUM) {
           U[buf][e] = ra[u];
         } else if constexpr (MODE == CH_SRSS) {  // srss: vsubps (mean - a), vmulps
           const float d = mu - ra[u];
@@ -361,7 +373,7 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
     float acc = 0.0f;
     if (ntile > 0) {
       load(0);
-      store(0);
+      store(0, 0);
     }
     __syncthreads();
     for (int t = 0; t < ntile; ++t) {
@@ -395,7 +407,7 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
           else acc = acc + row[q];
         }
       }
-      if (t + 1 < ntile) store((t + 1) & 1);
+      if (t + 1 < ntile) store((t + 1) & 1, t + 1);
       __syncthreads();
     }
     if (tid < 64) {  // lane-order epilogues (8-lane groups of wave 0)
@@ -425,8 +437,15 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
       const float h = x0 + __shfl_down(x0, 1, 8);
       float r = h + __shfl_down(h, 2, 8);
       if (l == 0 && chain) {
-        if (!lanes_form && MODE != CH_DOT)
+        if constexpr (MODE == CH_DSUM) {
+          for (int k = 0; k < tail; ++k) {
+            const float d = pa[nb8 + k] * grad_apply(pb[nb8 + k], act);
+            pw[nb8 + k] = d;
+            r = r + d;
+          }
+        } else if (!lanes_form && MODE != CH_DOT) {
           for (int k = 0; k < tail; ++k) r = r + pa[nb8 + k];
+        }
         if (grp == 0) part0[blk] = r;
         else part1[blk] = r;
       }
@@ -452,9 +471,11 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
                                                        const float* __restrict__ mu_arr,
                                                        int64_t nblocks, int64_t N, int64_t bs,
                                                        int quirk, float* __restrict__ part0,
-                                                       float* __restrict__ part1) {
+                                                       float* __restrict__ part1, int act,
+                                                       float* wa) {
   constexpr int SNT = 192, E = 32, TILE = SNT * E, NBUF = 3;
   constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;
+  constexpr bool LB = TWO || MODE == CH_DSUM;
   // lane-major rows (a chain's terms contiguous), LDT = 8 mod 32 for
   // conflict-free staging stores, and 72 floats of slack past a row's last
   // term: the chain loop reads up to 47 terms past its last full group
@@ -473,14 +494,15 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
   for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
     const int64_t i = blk % N;
     const float* pa = a + blk * bs;
-    const float* pb = TWO ? b + blk * bs : nullptr;
+    const float* pb = LB ? b + blk * bs : nullptr;
+    float* pw = MODE == CH_DSUM ? wa + blk * bs : nullptr;
     const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA) ? mu_arr[i] : 0.0f;
     float acc = 0.0f;
     if (!chainwave) {
       // float4 staging where the block is 16-byte aligned (nb8 % 8 == 0: a
       // float4 is wholly inside or outside the full 8-blocks)
-      const bool v4 = ((reinterpret_cast<uintptr_t>(pa) | (TWO ? reinterpret_cast<uintptr_t>(pb) : 0)) & 15) == 0;
-      float ra[E], rb[TWO ? E : 1];
+      const bool v4 = ((reinterpret_cast<uintptr_t>(pa) | (LB ? reinterpret_cast<uintptr_t>(pb) : 0)) & 15) == 0;
+      float ra[E], rb[LB ? E : 1];
       auto load = [&](int t) {
         const int64_t t0 = (int64_t)t * TILE;
         if (v4) {
@@ -490,7 +512,7 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
             const bool in = k < nb8;
             const float4 x = in ? *reinterpret_cast<const float4*>(pa + k) : float4{0, 0, 0, 0};
             ra[4 * u] = x.x; ra[4 * u + 1] = x.y; ra[4 * u + 2] = x.z; ra[4 * u + 3] = x.w;
-            if constexpr (TWO) {
+            if constexpr (LB) {
               const float4 y = in ? *reinterpret_cast<const float4*>(pb + k) : float4{0, 0, 0, 0};
               rb[4 * u] = y.x; rb[4 * u + 1] = y.y; rb[4 * u + 2] = y.z; rb[4 * u + 3] = y.w;
             }
@@ -502,11 +524,11 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
             for (int c = 0; c < 4; ++c) {
               const int64_t k = t0 + 4 * (st + SNT * u) + c;
               ra[4 * u + c] = k < nb8 ? pa[k] : 0.0f;
-              if constexpr (TWO) rb[4 * u + c] = k < nb8 ? pb[k] : 0.0f;
+              if constexpr (LB) rb[4 * u + c] = k < nb8 ? pb[k] : 0.0f;
             }
         }
       };
-      auto store = [&](int buf) {
+      auto store = [&](int buf, int t) {
 #pragma unroll
         for (int u = 0; u < E / 4; ++u)
 #pragma unroll
@@ -514,7 +536,12 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
             const int ee = 4 * (st + SNT * u) + c;
             const int e = (ee & 7) * LDT + (ee >> 3);
             const float va = ra[4 * u + c];
-            if constexpr (MODE == CH_SUM) {
+            if constexpr (MODE == CH_DSUM) {
+              const float d = va * grad_apply(rb[4 * u + c], act);
+              U[buf][e] = d;
+              const int64_t k = (int64_t)t * TILE + ee;
+              if (k < nb8) pw[k] = d;
+            } else if constexpr (MODE == CH_SUM) {
               U[buf][e] = va;
             } else if constexpr (MODE == CH_SRSS) {  // srss: vsubps (mean - a), vmulps
               const float d = mu - va;
@@ -530,14 +557,14 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
       };
       for (int t = 0; t < 2 && t < ntile; ++t) {
         load(t);
-        store(t);
+        store(t, t);
       }
       __syncthreads();
       for (int t = 0; t < ntile; ++t) {
         const bool more = t + 2 < ntile;
         if (more) load(t + 2);
         __syncthreads();
-        if (more) store((t + 2) % NBUF);
+        if (more) store((t + 2) % NBUF, t + 2);
       }
     } else {
       __syncthreads();
@@ -666,8 +693,15 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
       const float h = x0 + __shfl_down(x0, 1, 8);
       float r = h + __shfl_down(h, 2, 8);
       if (l == 0 && chain) {
-        if (!lanes_form && MODE != CH_DOT)
+        if constexpr (MODE == CH_DSUM) {
+          for (int k = 0; k < tail; ++k) {
+            const float d = pa[nb8 + k] * grad_apply(pb[nb8 + k], act);
+            pw[nb8 + k] = d;
+            r = r + d;
+          }
+        } else if (!lanes_form && MODE != CH_DOT) {
           for (int k = 0; k < tail; ++k) r = r + pa[nb8 + k];
+        }
         if (grp == 0) part0[blk] = r;
         else part1[blk] = r;
       }
@@ -705,18 +739,19 @@ __global__ void chains_finish(const float* __restrict__ part0, const float* __re
 
 template <int MODE>
 hipError_t run_chains(const float* a, const float* b, const float* mu, int64_t groups, int64_t N,
-                      int64_t bs, int quirk, float* part0, float* part1, hipStream_t s) {
+                      int64_t bs, int quirk, float* part0, float* part1, hipStream_t s,
+                      int act = 0, float* wa = nullptr) {
   const int64_t nblocks = groups * N;
   const unsigned grid = (unsigned)(nblocks < (1 << 20) ? nblocks : (1 << 20));
   if (bs >= 16384)
     hipLaunchKernelGGL((block_chains_ws<MODE>), dim3(grid), dim3(256), 0, s, a, b, mu, nblocks,
-                       N, bs, quirk, part0, part1);
+                       N, bs, quirk, part0, part1, act, wa);
   else if (bs >= 4096)
     hipLaunchKernelGGL((block_chains<MODE, 256, 16>), dim3(grid), dim3(256), 0, s, a, b, mu,
-                       nblocks, N, bs, quirk, part0, part1);
+                       nblocks, N, bs, quirk, part0, part1, act, wa);
   else
     hipLaunchKernelGGL((block_chains<MODE, 64, 8>), dim3(grid), dim3(64), 0, s, a, b, mu, nblocks,
-                       N, bs, quirk, part0, part1);
+                       N, bs, quirk, part0, part1, act, wa);
   return hipGetLastError();
 }
 
@@ -1076,6 +1111,24 @@ hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t
   }
   if (!use_chains(bs, part)) return launch_backward_bias(dst, N, src, bs, groups, 1, s);
   if (hipError_t e = run_chains<CH_SUM>(src, nullptr, nullptr, groups, N, bs, 0, part, nullptr, s))
+    return e;
+  return run_finish<FIN_ADD>(part, nullptr, groups, N, bs, nullptr, dst, nullptr, s);
+}
+
+// Derivative() then addSums(delta) of the conv backward (nConvolutionLayer.pas:
+// 583-598) in one pass: each term delta * f'(output) written back and summed
+// in the chains of launch_add_sums — the same values and sums as the two
+// launches (which remain the path where the chains do not apply)
+hipError_t launch_derive_add_sums(float* dst, float* delta, const float* output, int act,
+                                  int64_t groups, int64_t N, int64_t bs, float* part,
+                                  hipStream_t s) {
+  if (N <= 0 || groups <= 0 || bs <= 0) return hipSuccess;
+  if (act == TNS_acLINEAR || bs == 1 || !use_chains(bs, part)) {
+    if (hipError_t e = launch_derive(output, groups * N * bs, act, delta, s)) return e;
+    return launch_add_sums(dst, delta, groups, N, bs, part, s);
+  }
+  if (hipError_t e = run_chains<CH_DSUM>(delta, output, nullptr, groups, N, bs, 0, part, nullptr, s,
+                                         act, delta))
     return e;
   return run_finish<FIN_ADD>(part, nullptr, groups, N, bs, nullptr, dst, nullptr, s);
 }

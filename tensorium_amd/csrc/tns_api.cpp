@@ -1633,13 +1633,13 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   if (bn.scales && (!bn.x || !bn.x_norm || !bn.mean || !bn.variance || !bn.scale_updates ||
                     !bn.mean_delta || !bn.variance_delta))
     return set_error(TNS_ERR_ARG, "conv_backward: null batch-norm operand");
-  // Derivative(): delta *= f'(output)
-  if (int r = hip_status(launch_derive(output, batch * filters * i_k, activation, delta,
-                                       c->stream), "derive launch"))
-    return r;
   float* part;
   if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
   if (bn.scales) {
+    // Derivative(): delta *= f'(output)
+    if (int r = hip_status(launch_derive(output, batch * filters * i_k, activation, delta,
+                                         c->stream), "derive launch"))
+      return r;
     // batchNormBack: scale_updates.addDots(x_norm, delta); delta.forwardScale
     // (scales); MeansAndVarsDelta; normalizeDelta — and no bias_updates term
     // (nConvolutionLayer.pas:601-604)
@@ -1659,9 +1659,11 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
                                                   c->stream), "normalizeDelta launch"))
       return r;
   } else {
-    // bias_updates.addSums(delta)
-    if (int r = hip_status(launch_add_sums(bias_updates, delta, batch, filters, i_k, part,
-                                           c->stream), "addSums launch"))
+    // Derivative(): delta *= f'(output), then bias_updates.addSums(delta) —
+    // one pass (each derived term written back as it enters the sums' chains)
+    if (int r = hip_status(launch_derive_add_sums(bias_updates, delta, output, activation, batch,
+                                                  filters, i_k, part, c->stream),
+                           "derive + addSums launch"))
       return r;
   }
   // state.input.im2Col(...) — a 1x1/s1/p0 col matrix is the input itself

@@ -319,6 +319,10 @@ hipError_t launch_add_dots(float* dst, const float* a, const float* b, int64_t g
                            int64_t bs, float* part, hipStream_t s);
 hipError_t launch_add_sums(float* dst, const float* src, int64_t groups, int64_t N, int64_t bs,
                            float* part, hipStream_t s);
+// Derivative (delta *= f'(output)) fused into addSums' chains (same bits)
+hipError_t launch_derive_add_sums(float* dst, float* delta, const float* output, int act,
+                                  int64_t groups, int64_t N, int64_t bs, float* part,
+                                  hipStream_t s);
 hipError_t launch_mean_var_delta(const float* delta, const float* x, const float* mean,
                                  const float* var, int64_t groups, int64_t N, int64_t bs,
                                  float* mean_delta, float* var_delta, int quirk, float* part,
