@@ -138,14 +138,17 @@ __global__ __launch_bounds__(NT) void conv_dx_col2im_kernel(DxArgs p) {
   }
 }
 
-// Wt[t][f][c] = W[f][c*K2 + t]
+// Wt[s][f][c] = W[f][c*K2 + tap(s)], tap(s) = nibble s of `order` (K2 <= 16;
+// the identity order 0xfedcba9876543210 for tap-major weights)
 __global__ __launch_bounds__(256) void transpose_taps_kernel(const float* w, float* wt, int F,
-                                                              int C, int K2) {
+                                                              int C, int K2,
+                                                              unsigned long long order) {
   const int64_t n = (int64_t)F * C * K2;
   for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t t = i / ((int64_t)F * C);
-    const int64_t r = i - t * F * C;
+    const int64_t sl = i / ((int64_t)F * C);
+    const int64_t r = i - sl * F * C;
     const int64_t f = r / C, c = r - f * C;
+    const int64_t t = (int64_t)((order >> (4 * sl)) & 15);
     wt[i] = w[f * C * K2 + c * K2 + t];
   }
 }
@@ -170,15 +173,16 @@ bool conv_dx_fused_fits(int64_t C, int64_t H, int64_t W, int64_t stride, int64_t
          (int64_t)F * C <= 0x7fffffffLL;
 }
 
-// wt[t][f][c] = W[f][c*K2 + t]: the weights tap-major, k-major per tap
+// wt[s][f][c] = W[f][c*K2 + tap(s)]: the weights tap-major (taps in the
+// order given, nibble s = tap of slot s), k-major per tap
 hipError_t launch_transpose_taps(const float* w, float* wt, int64_t F, int64_t C, int64_t K2,
-                                 hipStream_t s) {
+                                 hipStream_t s, unsigned long long order) {
   const int64_t n = F * C * K2;
   if (n <= 0) return hipSuccess;
-  if (n > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (n > 0x7fffffffLL || K2 > 16) return hipErrorInvalidValue;
   const int64_t tb = std::min<int64_t>((n + 255) / 256, 65536);
   hipLaunchKernelGGL(transpose_taps_kernel, dim3((unsigned)tb), dim3(256), 0, s, w, wt, (int)F,
-                     (int)C, (int)K2);
+                     (int)C, (int)K2, order);
   return hipGetLastError();
 }
 

@@ -204,6 +204,12 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   const int n0 = tn * BN;
   const int N = (int)p.N, K = (int)p.K;
   const int H = p.conv_H, W = p.conv_W, HW = H * W;
+  // (DX) column pixel -> image pixel: itself, or a stride-2 class pixel
+  auto dx_pix = [&](int pix) -> int {
+    if (!p.dx_cls) return pix;
+    const int qy = pix / p.conv_ow, qx = pix - qy * p.conv_ow;
+    return (2 * qy + ((p.dx_cls >> 1) & 1)) * p.dx_imgW + 2 * qx + ((p.dx_cls >> 2) & 1);
+  };
 
   // ---- per-column state: window origin and the 9-bit tap validity mask ----
   // gather lanes: pixel gp of a 16-column fragment, slot component gq
@@ -257,7 +263,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   // (DX) the tile's first filter and its tap t in the forward window's
   // terms: reference tap (kr, kc) = t reads the delta pixel at forward tap
   // (KS-1-kr, KS-1-kc) of a window padded by KS-1-pad
-  const int F_ = G::DX ? K / (KS * KS) : 0;
+  // (a stride-2 pixel class: its dx_taps >> 16 taps)
+  const int F_ = G::DX ? K / (p.dx_cls ? (p.dx_taps >> 16) : KS * KS) : 0;
   int d_f0 = 0, d_t = 0;
   auto advance = [&]() {  // k += BK
     if constexpr (G::DX) {
@@ -308,7 +315,12 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     for (int ii = 0; ii < KI; ++ii) {
       int y = kr_[ii] * dil, z = kc_[ii] * dil, tap = kr_[ii] * KS + kc_[ii], cc = cc_[ii];
       if constexpr (G::DX) {
-        const int fr = KS - 1 - d_t / KS, fc = KS - 1 - d_t % KS;  // wave-uniform
+        int fr = KS - 1 - d_t / KS, fc = KS - 1 - d_t % KS;  // wave-uniform
+        if (p.dx_cls) {
+          const int fb = (p.dx_taps >> (4 * d_t)) & 15;
+          fr = fb / KS;
+          fc = fb - fr * KS;
+        }
         y = fr;
         z = fc;
         tap = fr * KS + fc;
@@ -489,7 +501,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       const int n = n0 + coff * 16 + 16 * j + r16, nc = n < N ? n : N - 1;
       unsigned vb;
       col_geo(n, vb, omask[j]);
-      const int img = nc / p.conv_ohw, pix = nc - img * p.conv_ohw;
+      const int img = nc / p.conv_ohw, pix = dx_pix(nc - img * p.conv_ohw);
       const float* cp = p.C + (int64_t)img * p.strideC + pix + row0 * p.ldc;
 #pragma unroll
       for (int e = 0; e < 4; ++e) rs[j][e] = cp[e * p.ldc];
@@ -498,7 +510,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   auto flush = [&]() {
     if (++fl_cnt < fl_tiles) return;
     fl_cnt = 0;
-    const int bit = KS * KS - 1 - fl_tap++;  // reference tap fl_tap, forward-window bit
+    // reference tap fl_tap's forward-window bit (a class: its tap table)
+    const int bit = p.dx_cls ? (p.dx_taps >> (4 * fl_tap)) & 15 : KS * KS - 1 - fl_tap;
+    ++fl_tap;
 #pragma unroll
     for (int j = 0; j < JW; ++j) {
       const bool ok = __builtin_amdgcn_ubfe(omask[j], bit, 1) != 0;
@@ -705,7 +719,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     for (int j = 0; j < JW; ++j) {
       const int n = n0 + coff * 16 + 16 * j + r16;
       if (n >= N) continue;
-      const int img = n / p.conv_ohw, pix = n - img * p.conv_ohw;
+      const int img = n / p.conv_ohw, pix = dx_pix(n - img * p.conv_ohw);
       float* cp = p.C + (int64_t)img * p.strideC + pix + row0 * p.ldc;
 #pragma unroll
       for (int e = 0; e < 4; ++e) cp[e * p.ldc] = rs[j][e];
@@ -1045,6 +1059,102 @@ hipError_t launch_conv_tile4_dx3(int v, const float* wt, const float* delta, flo
   a.conv_sY = 1; a.conv_sX = 1; a.conv_pH = (int)(ks - 1 - pad); a.conv_pW = (int)(ks - 1 - pad);
   a.conv_bytes = (int)(4 * batch * F * oh * ow);
   return kTiles4DX[v].fn(a, 3, 1, s);
+}
+
+namespace {
+// the taps of output pixel class (py, px) of a stride-2 3x3 layer padded by
+// pad, in scol2im's (kr, kc) order: pixel (iy, ix) = (2 qy + py, 2 qx + px)
+// takes col entry (kr, kc) at delta pixel ((iy + pad - kr) / 2, (ix + pad -
+// kc) / 2) when both differences are even (col2im's stride test) — delta row
+// qy + fr - 1 with fr = (py + pad - kr) / 2 + 1 in 0..2: the forward-window
+// bit fr*3 + fc of a window over the delta planes padded by 1
+int s2_taps(int64_t pad, int py, int px, int* ref, int* fwd) {
+  int n = 0;
+  for (int kr = 0; kr < 3; ++kr) {
+    const int dr = py + (int)pad - kr;
+    if (dr & 1) continue;
+    for (int kc = 0; kc < 3; ++kc) {
+      const int dc = px + (int)pad - kc;
+      if (dc & 1) continue;
+      ref[n] = kr * 3 + kc;
+      fwd[n] = (dr / 2 + 1) * 3 + (dc / 2 + 1);
+      ++n;
+    }
+  }
+  return n;
+}
+
+bool dx3s2_fits(int v, int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t pad,
+                int64_t oh, int64_t ow) {
+  if (v < 0 || v >= kNumTiles4DX || pad < 0 || pad > 2 || H < 2 || W < 2) return false;
+  if (oh != (H + 2 * pad - 3) / 2 + 1 || ow != (W + 2 * pad - 3) / 2 + 1 || oh <= 0 || ow <= 0)
+    return false;
+  if (F % kTiles4DX[v].bk || C % kTiles4DX[v].bm || batch <= 0) return false;
+  return batch * F * oh * ow * 4 <= 0x7fffffffLL && batch * C * H * W <= 0x7fffffffLL &&
+         9 * F * C <= 0x7fffffffLL;
+}
+}  // namespace
+
+unsigned long long conv_tile4_dx3s2_order(int64_t pad) {
+  unsigned long long o = 0;
+  int sl = 0, ref[9], fwd[9];
+  for (int cls = 0; cls < 4; ++cls) {
+    const int n = s2_taps(pad, cls >> 1, cls & 1, ref, fwd);
+    for (int i = 0; i < n; ++i, ++sl) o |= (unsigned long long)ref[i] << (4 * sl);
+  }
+  return o;
+}
+
+// by the pixel count of a class, as the stride-1 forms (conv_tile4_dx3_pick)
+int conv_tile4_dx3s2_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
+                          int64_t pad) {
+  if (ks != 3) return -1;
+  const int64_t N = batch * (H / 2) * (W / 2), oh = (H + 2 * pad - 3) / 2 + 1,
+                ow = (W + 2 * pad - 3) / 2 + 1;
+  int v = -1;
+  if (C % 64 && N >= 50000)
+    v = 6;
+  else if (N >= 50000)
+    v = 4;
+  else if (N >= 16384)
+    v = 0;
+  return v >= 0 && dx3s2_fits(v, batch, C, H, W, F, pad, oh, ow) ? v : -1;
+}
+
+hipError_t launch_conv_tile4_dx3s2(int v, const float* wt, const float* delta, float* im,
+                                   int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F,
+                                   int64_t pad, int64_t oh, int64_t ow, hipStream_t s) {
+  if (!dx3s2_fits(v, batch, C, H, W, F, pad, oh, ow)) return hipErrorInvalidValue;
+  int sl = 0;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int py = cls >> 1, px = cls & 1;
+    int ref[9], fwd[9];
+    const int T = s2_taps(pad, py, px, ref, fwd);
+    const int64_t ohc = (H - py + 1) / 2, owc = (W - px + 1) / 2;
+    if (T == 0 || ohc <= 0 || owc <= 0) {
+      sl += T;
+      continue;
+    }
+    GemmArgs a{};
+    a.M = C; a.N = batch * ohc * owc; a.K = T * F;
+    a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_ZERO;
+    a.A = wt + (int64_t)sl * F * C; a.lda = C; a.strideA = 0;
+    a.B = delta; a.ldb = oh * ow; a.strideB = F * oh * ow;
+    a.C = im; a.ldc = H * W; a.strideC = C * H * W;
+    a.batch = 1; a.epi = EPI_NONE; a.bias = nullptr; a.act = 0;
+    a.conv = 2;
+    // the class's columns over the delta planes: a 3x3 window padded by 1
+    a.conv_H = (int)oh; a.conv_W = (int)ow; a.conv_ow = (int)owc; a.conv_ohw = (int)(ohc * owc);
+    a.conv_sY = 1; a.conv_sX = 1; a.conv_pH = 1; a.conv_pW = 1;
+    a.conv_bytes = (int)(4 * batch * F * oh * ow);
+    a.dx_cls = 1 | py << 1 | px << 2;
+    a.dx_taps = T << 16;
+    for (int i = 0; i < T; ++i) a.dx_taps |= fwd[i] << (4 * i);
+    a.dx_imgW = (int)W;
+    if (hipError_t e = kTiles4DX[v].fn(a, 3, 1, s); e != hipSuccess) return e;
+    sl += T;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_conv_tile4(int v, const GemmArgs& a, int ks, int dil, hipStream_t s) {

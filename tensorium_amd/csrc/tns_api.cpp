@@ -1705,10 +1705,15 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // state.delta of a stride-1 3x3 layer as one implicit transposed
   // convolution (conv_tile4 DX forms: each tap's filter chain added to the
   // pixel in scol2im's order), no col matrix
+  // (stride 2: four such convolutions, one per output pixel parity class,
+  // each over the taps col2im adds to that class)
   int dxc = -1;
-  if (state_delta && !fused_dx && kSize == 3 && stride == 1 && dilation == 1 && g_dx_conv != -2)
+  const bool dxc_s2 = stride == 2;
+  if (state_delta && !fused_dx && kSize == 3 && (stride == 1 || stride == 2) && dilation == 1 &&
+      g_dx_conv != -2)
     dxc = g_dx_conv >= 0 ? (int)g_dx_conv
-                         : conv_tile4_dx3_pick(batch, C, H, W, filters, kSize, padding);
+          : dxc_s2   ? conv_tile4_dx3s2_pick(batch, C, H, W, filters, kSize, padding)
+                     : conv_tile4_dx3_pick(batch, C, H, W, filters, kSize, padding);
   // dW (im2col + sdot or dw_tile, accumulate) and state.delta (TN + col2im
   // or the fused kernel) read delta and write disjoint outputs: with a
   // state.delta they run concurrently, state.delta's chain on the context's
@@ -1838,11 +1843,17 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     // GEMM
     if (dxc >= 0) {
       OpTimer t(c, TNS_OP_GEMM);
-      if (int r = hip_status(launch_transpose_taps(weights, wt, filters, C, kSize * kSize, c->stream),
-                             "weights transpose launch"))
+      if (int r = hip_status(
+              dxc_s2 ? launch_transpose_taps(weights, wt, filters, C, kSize * kSize, c->stream,
+                                             conv_tile4_dx3s2_order(padding))
+                     : launch_transpose_taps(weights, wt, filters, C, kSize * kSize, c->stream),
+              "weights transpose launch"))
         return r;
-      const hipError_t e = launch_conv_tile4_dx3(dxc, wt, delta, state_delta, batch, C, H, W,
-                                                 filters, kSize, padding, g.oh, g.ow, c->stream);
+      const hipError_t e =
+          dxc_s2 ? launch_conv_tile4_dx3s2(dxc, wt, delta, state_delta, batch, C, H, W, filters,
+                                           padding, g.oh, g.ow, c->stream)
+                 : launch_conv_tile4_dx3(dxc, wt, delta, state_delta, batch, C, H, W, filters,
+                                         kSize, padding, g.oh, g.ow, c->stream);
       if (e != hipErrorInvalidValue) return hip_status(e, "dX conv launch");
       return set_error(TNS_ERR_UNSUPPORTED, "dX conv form %d does not fit this layer", dxc);
     }

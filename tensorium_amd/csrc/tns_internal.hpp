@@ -72,6 +72,11 @@ struct GemmArgs {
   int ktab_n;
   int conv_H, conv_W, conv_ow, conv_ohw, conv_sY, conv_sX, conv_pH, conv_pW;
   int conv_bytes;
+  // conv_tile4 DX forms on one pixel class of a stride-2 layer (dx_cls != 0):
+  // columns = the class's pixels (2 qy + py, 2 qx + px) of images dx_imgW
+  // wide (py = dx_cls >> 1 & 1, px = dx_cls >> 2 & 1); k = the class's taps
+  // (count dx_taps >> 16, nibble i = tap i's forward-window bit fr*3 + fc)
+  int dx_cls, dx_taps, dx_imgW;
   // diagnostic builds (-DTNS_GEMM_STAMPS) only: per-block timeline records
   unsigned* stamps;
 };
@@ -160,7 +165,18 @@ hipError_t launch_conv_tile4_dx3(int v, const float* wt, const float* delta, flo
                                  int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F,
                                  int64_t ks, int64_t pad, int64_t oh, int64_t ow, hipStream_t s);
 hipError_t launch_transpose_taps(const float* w, float* wt, int64_t F, int64_t C, int64_t K2,
-                                 hipStream_t s);
+                                 hipStream_t s, unsigned long long order = 0xfedcba9876543210ULL);
+// state.delta of a stride-2 3x3 layer (dilation 1) as four implicit
+// transposed convolutions, one per output pixel class (py, px) = parity of
+// (row, column): each class's taps in scol2im's order, no col matrix.  wt =
+// the weights transposed tap-major in the class order conv_tile4_dx3s2_order
+// (pad) gives; form v of conv_tile4_dx3_count(); pick -1 where none applies
+unsigned long long conv_tile4_dx3s2_order(int64_t pad);
+int conv_tile4_dx3s2_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
+                          int64_t pad);
+hipError_t launch_conv_tile4_dx3s2(int v, const float* wt, const float* delta, float* im,
+                                   int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F,
+                                   int64_t pad, int64_t oh, int64_t ow, hipStream_t s);
 // implicit-GEMM convolution on the ping-pong schedule (conv_pp.hip): same
 // operands and limits as conv_tile; conv_pp_pick = -1 where not measured faster
 int conv_pp_count();

@@ -273,6 +273,34 @@ def test_conv_backward_dx_conv_forms(hip, torch_cuda, ora):
     assert ran >= 2 * nv
 
 
+DX3S2_CASES = [(2, 64, 14, 64, 3, 2, 1, 9), (2, 32, 16, 64, 3, 2, 1, 1), (1, 64, 13, 128, 3, 2, 1, 9),
+               (2, 64, 12, 64, 3, 2, 0, 9), (2, 128, 10, 128, 3, 2, 2, 4), (3, 32, 11, 128, 3, 2, 1, 9)]
+
+
+def test_conv_backward_dx_conv_stride2_forms(hip, torch_cuda, ora):
+    """state.delta of stride-2 3x3 layers as four implicit transposed
+    convolutions, one per output pixel parity class (each over the taps
+    col2im adds to that class, in (kr, kc) order; every DX form forced) —
+    bit-exact against the reference's TN GEMM + scol2im: pads 0, 1, 2, odd
+    and even planes (classes of unequal size), batch 1 .. 3."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convDxConvs()
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setDxConv(v)
+            for i, case in enumerate(DX3S2_CASES):
+                try:
+                    got, ref = _dx_case(hip, torch_cuda, ora, *case, seed=120 + i)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, case)
+    finally:
+        hip.setDxConv(-1)
+    assert ran >= 2 * nv
+
+
 @pytest.mark.parametrize("idx", [2, 28, 45])
 def test_conv_backward_overlap_matches_sequential(hip, torch_cuda, ora, idx):
     """dW and state.delta on two streams (TNS_OPT_BWD_OVERLAP = 1, the
@@ -350,10 +378,11 @@ def test_conv_backward_pipelined_chain(hip, torch_cuda):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("idx", [3, 10, 11, 27, 28, 44, 45, 58])
+@pytest.mark.parametrize("idx", [3, 4, 9, 10, 11, 27, 28, 44, 45, 58])
 def test_conv_backward_dx_yolov3_batch8(hip, torch_cuda, ora, idx):
     """state.delta at YOLOv3 layer shapes, batch 8, on the default path (the
-    k-major-A conv tile where one applies; on the 1x1 layers 10, 27, 44, 58
+    k-major-A conv tile where one applies, the parity-class transposed
+    convolutions on the stride-2 layers 4 and 9; on the 1x1 layers 10, 27, 44, 58
     the product adds into state.delta in its epilogue, col2im's one add per
     pixel): bit-exact."""
     from tensorium_amd.yolo import yolov3_conv_table
