@@ -594,12 +594,15 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * modify a pending call's input, delta or weight_updates by other means (work
  * enqueued on the stream outside this API, or host writes) before such a
  * join; a backward pass of the layers below reads none of them.  Same
- * results; state.delta always gets its own col buffer (the memory note above). */
+ * results; state.delta always gets its own col buffer (the memory note above).
+ * TNS_OPT_DERIVE_SUMS (default 1): the conv backward's Derivative and
+ * addSums (no batch norm) in one pass where the sums' chain kernel applies
+ * (planes under 16384 pixels); 0 = two passes.  Same bits. */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,
        TNS_OPT_DW_TILE = 9, TNS_OPT_BWD_OVERLAP = 10, TNS_OPT_DX_CONV = 11,
-       TNS_OPT_DW_RES = 12 };
+       TNS_OPT_DW_RES = 12, TNS_OPT_DERIVE_SUMS = 13 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

@@ -64,6 +64,7 @@ const
   TNS_OPT_BWD_OVERLAP = 10;
   TNS_OPT_DX_CONV = 11;
   TNS_OPT_DW_RES = 12;
+  TNS_OPT_DERIVE_SUMS = 13;
 
 type
   PTnsCtx = pointer;

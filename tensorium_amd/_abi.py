@@ -37,6 +37,7 @@ TNS_OPT_DW_TILE = 9
 TNS_OPT_BWD_OVERLAP = 10
 TNS_OPT_DX_CONV = 11
 TNS_OPT_DW_RES = 12
+TNS_OPT_DERIVE_SUMS = 13
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 

@@ -1123,7 +1123,11 @@ hipError_t launch_derive_add_sums(float* dst, float* delta, const float* output,
                                   int64_t groups, int64_t N, int64_t bs, float* part,
                                   hipStream_t s) {
   if (N <= 0 || groups <= 0 || bs <= 0) return hipSuccess;
-  if (act == TNS_acLINEAR || bs == 1 || !use_chains(bs, part)) {
+  // (the planes of >= 16384 pixels, whose chain kernel is one block per
+  // plane with three staging waves, keep the separate derivative pass: the
+  // extra read and write stream there outlasts the chains, YOLOv3 layer 0
+  // 0.57 -> 0.68 ms a call)
+  if (act == TNS_acLINEAR || bs == 1 || bs >= 16384 || !use_chains(bs, part)) {
     if (hipError_t e = launch_derive(output, groups * N * bs, act, delta, s)) return e;
     return launch_add_sums(dst, delta, groups, N, bs, part, s);
   }

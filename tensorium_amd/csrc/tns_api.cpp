@@ -41,6 +41,7 @@ static int64_t g_dw_res = -1;
 static int64_t g_dw_tile = -1;
 // conv backward: dW and state.delta concurrently on two streams (TNS_OPT_BWD_OVERLAP)
 static int64_t g_bwd_overlap = 1;
+static int64_t g_derive_sums = 1;
 static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
@@ -616,6 +617,9 @@ int tns_set_option(int32_t opt, int64_t value) {
     case TNS_OPT_DW_RES:
       if (value >= dw_res_count()) return set_error(TNS_ERR_ARG, "no dW res form %lld", (long long)value);
       g_dw_res = value < -1 ? -2 : value;
+      return TNS_OK;
+    case TNS_OPT_DERIVE_SUMS:
+      g_derive_sums = value ? 1 : 0;
       return TNS_OK;
     case TNS_OPT_DX_CONV:
       if (value >= conv_tile4_dx3_count())
@@ -1661,10 +1665,19 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   } else {
     // Derivative(): delta *= f'(output), then bias_updates.addSums(delta) —
     // one pass (each derived term written back as it enters the sums' chains)
-    if (int r = hip_status(launch_derive_add_sums(bias_updates, delta, output, activation, batch,
-                                                  filters, i_k, part, c->stream),
-                           "derive + addSums launch"))
-      return r;
+    if (g_derive_sums) {
+      if (int r = hip_status(launch_derive_add_sums(bias_updates, delta, output, activation, batch,
+                                                    filters, i_k, part, c->stream),
+                             "derive + addSums launch"))
+        return r;
+    } else {
+      if (int r = hip_status(launch_derive(output, batch * filters * i_k, activation, delta,
+                                           c->stream), "derive launch"))
+        return r;
+      if (int r = hip_status(launch_add_sums(bias_updates, delta, batch, filters, i_k, part,
+                                             c->stream), "addSums launch"))
+        return r;
+    }
   }
   // state.input.im2Col(...) — a 1x1/s1/p0 col matrix is the input itself
   const bool needs_col = kSize != 1 || stride != 1 || padding != 0 || dilation != 1;

@@ -339,6 +339,22 @@ def test_conv_backward_overlap_matches_sequential(hip, torch_cuda, ora, idx):
             assert np.array_equal(a, r)
 
 
+@pytest.mark.parametrize("idx", [10, 28, 45])
+def test_conv_backward_derive_sums_separate(hip, torch_cuda, ora, idx):
+    """TNS_OPT_DERIVE_SUMS = 0 (Derivative and addSums as two passes, the
+    form the fused chain pass replaced): state.delta and the whole backward
+    still bit-exact against the oracle."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    spec = yolov3_conv_table()[idx]
+    try:
+        hip.setDeriveSums(False)
+        got, ref = _dx_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,
+                            spec.stride, spec.pad, spec.activation, seed=500 + idx)
+    finally:
+        hip.setDeriveSums(True)
+    assert np.array_equal(got, ref)
+
+
 def test_conv_backward_pipelined_chain(hip, torch_cuda):
     """TNS_OPT_BWD_OVERLAP = 2 over a chain of YOLOv3 layers (43 .. 46, run
     in backward order, each layer's state.delta the delta of the layer below
