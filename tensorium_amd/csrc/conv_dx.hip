@@ -138,8 +138,8 @@ __global__ __launch_bounds__(NT) void conv_dx_col2im_kernel(DxArgs p) {
   }
 }
 
-// Wt[s][f][c] = W[f][c*K2 + tap(s)], tap(s) = nibble s of `order` (K2 <= 16;
-// the identity order 0xfedcba9876543210 for tap-major weights)
+// Wt[s][f][c] = W[f][c*K2 + tap(s)], tap(s) = nibble s of `order` (K2 <= 16),
+// or s itself for order = ~0 (any K2)
 __global__ __launch_bounds__(256) void transpose_taps_kernel(const float* w, float* wt, int F,
                                                               int C, int K2,
                                                               unsigned long long order) {
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void transpose_taps_kernel(const float* w, flo
     const int64_t sl = i / ((int64_t)F * C);
     const int64_t r = i - sl * F * C;
     const int64_t f = r / C, c = r - f * C;
-    const int64_t t = (int64_t)((order >> (4 * sl)) & 15);
+    const int64_t t = order == ~0ULL ? sl : (int64_t)((order >> (4 * sl)) & 15);
     wt[i] = w[f * C * K2 + c * K2 + t];
   }
 }
@@ -174,12 +174,12 @@ bool conv_dx_fused_fits(int64_t C, int64_t H, int64_t W, int64_t stride, int64_t
 }
 
 // wt[s][f][c] = W[f][c*K2 + tap(s)]: the weights tap-major (taps in the
-// order given, nibble s = tap of slot s), k-major per tap
+// order given, nibble s = tap of slot s; ~0 = natural order), k-major per tap
 hipError_t launch_transpose_taps(const float* w, float* wt, int64_t F, int64_t C, int64_t K2,
                                  hipStream_t s, unsigned long long order) {
   const int64_t n = F * C * K2;
   if (n <= 0) return hipSuccess;
-  if (n > 0x7fffffffLL || K2 > 16) return hipErrorInvalidValue;
+  if (n > 0x7fffffffLL || (order != ~0ULL && K2 > 16)) return hipErrorInvalidValue;
   const int64_t tb = std::min<int64_t>((n + 255) / 256, 65536);
   hipLaunchKernelGGL(transpose_taps_kernel, dim3((unsigned)tb), dim3(256), 0, s, w, wt, (int)F,
                      (int)C, (int)K2, order);

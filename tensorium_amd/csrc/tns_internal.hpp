@@ -165,7 +165,7 @@ hipError_t launch_conv_tile4_dx3(int v, const float* wt, const float* delta, flo
                                  int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F,
                                  int64_t ks, int64_t pad, int64_t oh, int64_t ow, hipStream_t s);
 hipError_t launch_transpose_taps(const float* w, float* wt, int64_t F, int64_t C, int64_t K2,
-                                 hipStream_t s, unsigned long long order = 0xfedcba9876543210ULL);
+                                 hipStream_t s, unsigned long long order = ~0ULL);
 // state.delta of a stride-2 3x3 layer (dilation 1) as four implicit
 // transposed convolutions, one per output pixel class (py, px) = parity of
 // (row, column): each class's taps in scol2im's order, no col matrix.  wt =
