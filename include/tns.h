@@ -595,9 +595,11 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * enqueued on the stream outside this API, or host writes) before such a
  * join; a backward pass of the layers below reads none of them.  Same
  * results; state.delta always gets its own col buffer (the memory note above).
- * TNS_OPT_DERIVE_SUMS (default 1): the conv backward's Derivative and
+ * TNS_OPT_DERIVE_SUMS (default 0): 1 = the conv backward's Derivative and
  * addSums (no batch norm) in one pass where the sums' chain kernel applies
- * (planes under 16384 pixels); 0 = two passes.  Same bits. */
+ * (planes under 16384 pixels); 0 = two passes (measured level: 15.06 vs
+ * 15.00 ms a pipelined YOLOv3 pass, profiles/r04_bwd_schedules2.json).  Same
+ * bits. */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,

@@ -111,7 +111,7 @@ def main():
         row["calls_overlap2_bit_identical"] = bool(
             all(torch.equal(p, q) for r1, r2 in zip(ref, got) for p, q in zip(r1, r2)))
         times = {k: [] for k in ("calls_overlap1", "calls_overlap0", "calls_overlap2",
-                                 "calls_overlap2_derive_apart", "graph_overlap1",
+                                 "calls_overlap2_derive_fused", "graph_overlap1",
                                  "graph_overlap0")}
         for _ in range(a.rounds):
             for ov in (True, False):
@@ -120,9 +120,9 @@ def main():
                 times[f"graph_overlap{int(ov)}"].append(timed(graphs[ov].replay))
             hip.setBwdOverlap(2)
             times["calls_overlap2"].append(timed(step, join=True))
-            hip.setDeriveSums(False)
-            times["calls_overlap2_derive_apart"].append(timed(step, join=True))
             hip.setDeriveSums(True)
+            times["calls_overlap2_derive_fused"].append(timed(step, join=True))
+            hip.setDeriveSums(False)
         hip.setBwdOverlap(True)
     for k, v in times.items():
         row[k + "_ms"] = round(min(v), 3)

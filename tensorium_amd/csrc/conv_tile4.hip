@@ -1105,7 +1105,12 @@ unsigned long long conv_tile4_dx3s2_order(int64_t pad) {
   return o;
 }
 
-// by the pixel count of a class, as the stride-1 forms (conv_tile4_dx3_pick)
+// by the pixel count of a class.  Measured on the YOLOv3 stride-2 layers at
+// batch 8 (scripts/bwd_sweep.py --what dx, whole backward calls,
+// profiles/r04_bwd_dx_s2.json) against TN + col2im: 416^2 -> 208^2 (32
+// channels) 0.840 -> 0.788 ms with the 32 x 176 tile, 208^2 -> 104^2 0.495
+// -> 0.456 with 64 x 48; level at 104^2 -> 52^2 (0.384 vs 0.382) and behind
+// on the smaller planes (52^2 -> 26^2 0.319 vs >= 0.356), so not there
 int conv_tile4_dx3s2_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
                           int64_t pad) {
   if (ks != 3) return -1;
@@ -1115,9 +1120,7 @@ int conv_tile4_dx3s2_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_
   if (C % 64 && N >= 50000)
     v = 6;
   else if (N >= 50000)
-    v = 4;
-  else if (N >= 16384)
-    v = 0;
+    v = 2;
   return v >= 0 && dx3s2_fits(v, batch, C, H, W, F, pad, oh, ow) ? v : -1;
 }
 

@@ -41,7 +41,7 @@ static int64_t g_dw_res = -1;
 static int64_t g_dw_tile = -1;
 // conv backward: dW and state.delta concurrently on two streams (TNS_OPT_BWD_OVERLAP)
 static int64_t g_bwd_overlap = 1;
-static int64_t g_derive_sums = 1;
+static int64_t g_derive_sums = 0;
 static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;

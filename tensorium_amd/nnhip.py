@@ -364,10 +364,10 @@ class TNNHip:
         m = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
         check(self.lib.tns_set_option(10, m))
 
-    def setDeriveSums(self, on: bool = True):
+    def setDeriveSums(self, on: bool = False):
         """Conv backward (no batch norm): Derivative fused into addSums'
-        chain pass (1, where it applies) or two passes (0); same results;
-        process-wide."""
+        chain pass (True, where it applies) or two passes (False, the
+        default); same results; process-wide."""
         check(self.lib.tns_set_option(13, 1 if on else 0))
 
     def convDwTiles(self) -> int:

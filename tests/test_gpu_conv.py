@@ -340,19 +340,35 @@ def test_conv_backward_overlap_matches_sequential(hip, torch_cuda, ora, idx):
 
 
 @pytest.mark.parametrize("idx", [10, 28, 45])
-def test_conv_backward_derive_sums_separate(hip, torch_cuda, ora, idx):
-    """TNS_OPT_DERIVE_SUMS = 0 (Derivative and addSums as two passes, the
-    form the fused chain pass replaced): state.delta and the whole backward
-    still bit-exact against the oracle."""
+def test_conv_backward_derive_sums_fused(hip, torch_cuda, ora, idx):
+    """TNS_OPT_DERIVE_SUMS = 1 (Derivative fused into addSums' chain pass,
+    each derived term written back as it is staged): delta, bias_updates,
+    weight_updates and state.delta bit-exact against the oracle."""
     from tensorium_amd.yolo import yolov3_conv_table
     spec = yolov3_conv_table()[idx]
+    batch, C, H, F, k, s, p = 8, spec.c, spec.h, spec.filters, spec.size, spec.stride, spec.pad
+    rng = np.random.default_rng(500 + idx)
+    oh = (H + 2 * p - k) // s + 1
+    x = rng.uniform(-1, 1, (batch, C, H, H)).astype(np.float32)
+    w = rng.uniform(-0.1, 0.1, F * C * k * k).astype(np.float32)
+    out = rng.uniform(-1, 1, (batch, F, oh, oh)).astype(np.float32)
+    d0 = rng.uniform(-1, 1, out.shape).astype(np.float32)
+    bu0 = rng.uniform(-1, 1, F).astype(np.float32)
+    wu0 = rng.uniform(-1, 1, F * C * k * k).astype(np.float32)
+    sd0 = rng.uniform(-1, 1, x.shape).astype(np.float32)
+    rd, rbu, rwu, rsd = d0.copy(), bu0.copy(), wu0.copy(), sd0.copy()
+    ora.conv_backward(x, w, F, k, s, p, spec.activation, out, rd, rbu, rwu, rsd)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    dx, dw, dout, dd, dbu, dwu, dsd = map(t, (x, w, out, d0, bu0, wu0, sd0))
     try:
-        hip.setDeriveSums(False)
-        got, ref = _dx_case(hip, torch_cuda, ora, 8, spec.c, spec.h, spec.filters, spec.size,
-                            spec.stride, spec.pad, spec.activation, seed=500 + idx)
-    finally:
         hip.setDeriveSums(True)
-    assert np.array_equal(got, ref)
+        hip.convBackward(batch, C, H, H, dx, dw, F, k, s, p, 1, spec.activation, dout, dd, dbu,
+                         dwu, None, dsd)
+        hip.finish()
+    finally:
+        hip.setDeriveSums(False)
+    for a, r in zip((dd, dbu, dwu, dsd), (rd, rbu, rwu, rsd)):
+        assert np.array_equal(a.cpu().numpy(), r)
 
 
 def test_conv_backward_pipelined_chain(hip, torch_cuda):
