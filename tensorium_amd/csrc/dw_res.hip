@@ -461,29 +461,30 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
       dst + b * dstImg + (int64_t)n * 8 * K4, K4);
 }
 
-// Rows of at most 256 elements (the 13^2 planes): eight rows a block, a
-// thread's element of each (eight loads in flight), written straight to its
-// rearranged place — a block writes its rows whole, so the lines complete in
-// L2 without the LDS transpose
+// Rows of 256 elements (K4 = 32: the 13^2 planes): eight rows a block, each
+// row's 64 16-byte pieces written straight to their rearranged place — piece
+// a of residue r holds elements i = (a >> 2) + 8 (a & 3) + 2 e, e = 0..3, of
+// kperm's block; a thread two pieces, each four loads and one 16-byte store
+// (a block writes its rows whole, so the lines complete in L2 without the
+// LDS transpose)
 __global__ __launch_bounds__(256) void res_permute_short_kernel(
     const float* __restrict__ src, int64_t srcImg, float* __restrict__ dst, int64_t dstImg,
     int rows, int K, int K4, int row0, int total) {
-  const int pp = threadIdx.x;
-  if (pp >= 8 * K4) return;
-  float v[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int u = 0; u < 2; ++u) {
+    const int idx = (int)threadIdx.x + 256 * u, j = idx >> 6, r = (idx >> 3) & 7, a = idx & 7;
     const int ra = row0 + 8 * (int)blockIdx.y + j;
+    if (ra >= total) continue;
     const int b = ra / rows, row = ra - b * rows;
-    v[j] = (ra < total && pp < K) ? src[b * srcImg + (int64_t)row * K + pp] : 0.0f;
-  }
-  const int off = (pp & 7) * K4 + kperm(pp >> 3);
+    const float* s = src + b * srcImg + (int64_t)row * K;
+    float v[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int ra = row0 + 8 * (int)blockIdx.y + j;
-    if (ra >= total) break;
-    const int b = ra / rows, row = ra - b * rows;
-    dst[b * dstImg + (int64_t)row * 8 * K4 + off] = v[j];
+    for (int e = 0; e < 4; ++e) {
+      const int pp = r + 8 * ((a >> 2) + 8 * (a & 3) + 2 * e);
+      v[e] = pp < K ? s[pp] : 0.0f;
+    }
+    *reinterpret_cast<float4*>(dst + b * dstImg + (int64_t)row * 8 * K4 + r * K4 + 4 * a) =
+        make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
@@ -491,27 +492,27 @@ __global__ __launch_bounds__(256) void im2col_res_short_kernel(
     const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int H,
     int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
     int rows, int K4, int row0, int total) {
-  const int pp = threadIdx.x;
-  if (pp >= 8 * K4) return;
-  const int oy = pp / oW, ox = pp - oy * oW, taps = kH * kW;
-  float v[8];
+  const int taps = kH * kW;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int u = 0; u < 2; ++u) {
+    const int idx = (int)threadIdx.x + 256 * u, j = idx >> 6, r = (idx >> 3) & 7, a = idx & 7;
     const int ra = row0 + 8 * (int)blockIdx.y + j;
+    if (ra >= total) continue;
     const int b = ra / rows, n = ra - b * rows;
     const int c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
-    const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
-    v[j] = (ra < total && pp < HWo && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
-               ? x[b * xImg + ((int64_t)c * H + iy) * W + ix]
-               : 0.0f;
-  }
-  const int off = (pp & 7) * K4 + kperm(pp >> 3);
+    const float* xc = x + b * xImg + (int64_t)c * H * W;
+    float v[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int ra = row0 + 8 * (int)blockIdx.y + j;
-    if (ra >= total) break;
-    const int b = ra / rows, n = ra - b * rows;
-    dst[b * dstImg + (int64_t)n * 8 * K4 + off] = v[j];
+    for (int e = 0; e < 4; ++e) {
+      const int pp = r + 8 * ((a >> 2) + 8 * (a & 3) + 2 * e);
+      const int oy = pp / oW, ox = pp - oy * oW;
+      const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
+      v[e] = (pp < HWo && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                 ? xc[iy * W + ix]
+                 : 0.0f;
+    }
+    *reinterpret_cast<float4*>(dst + b * dstImg + (int64_t)n * 8 * K4 + r * K4 + 4 * a) =
+        make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
