@@ -374,10 +374,12 @@ def test_conv_backward_derive_sums_fused(hip, torch_cuda, ora, idx):
 def test_conv_backward_pipelined_chain(hip, torch_cuda):
     """TNS_OPT_BWD_OVERLAP = 2 over a chain of YOLOv3 layers (43 .. 46, run
     in backward order, each layer's state.delta the delta of the layer below
-    and its input that layer's output): every call's dW is left running on
-    the side stream while the next calls' derive / bias sums / state.delta
-    work proceeds; every delta, bias / weight update and the chain's
-    state.delta bit-identical to the sequential schedule (0)."""
+    and its input that layer's output), two passes: every call's dW is left
+    running on the side stream while the next calls' derive / bias sums /
+    state.delta work proceeds, and pass 2's derivative of a layer waits for
+    pass 1's dW that still reads that delta; every delta, bias / weight
+    update and the chain's state.delta bit-identical to the sequential
+    schedule (0)."""
     from tensorium_amd.yolo import yolov3_conv_table
     specs = [yolov3_conv_table()[i] for i in (43, 44, 45, 46)]
     B = 8
@@ -396,12 +398,13 @@ def test_conv_backward_pipelined_chain(hip, torch_cuda):
             SD = t(sd0)
             BU = [torch_cuda.zeros(s.filters, device="cuda") for s in specs]
             WU = [torch_cuda.zeros(s.filters, s.K, device="cuda") for s in specs]
-            for j in range(len(specs) - 1, -1, -1):
-                s = specs[j]
-                inp = X if j == 0 else O[j - 1]
-                sd = SD if j == 0 else D[j - 1]
-                hip.convBackward(B, s.c, s.h, s.h, inp, W[j], s.filters, s.size, s.stride, s.pad,
-                                 1, s.activation, O[j], D[j], BU[j], WU[j], None, sd)
+            for _ in range(2):  # (pass 2 rewrites the deltas pass 1's dW products read)
+                for j in range(len(specs) - 1, -1, -1):
+                    s = specs[j]
+                    inp = X if j == 0 else O[j - 1]
+                    sd = SD if j == 0 else D[j - 1]
+                    hip.convBackward(B, s.c, s.h, s.h, inp, W[j], s.filters, s.size, s.stride,
+                                     s.pad, 1, s.activation, O[j], D[j], BU[j], WU[j], None, sd)
             hip.finish()
             got[mode] = [a.cpu().numpy() for a in D + BU + WU + [SD]]
     finally:
