@@ -590,10 +590,11 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * side stream (behind the earlier calls' dW) and returns without joining it;
  * the next call of ANY other entry point (and tns_hip_finish) first makes the
  * context's stream wait for the side stream.  The dW of layer L then runs
- * under the following calls' derive / state.delta work — the caller must not
- * modify a pending call's input, delta or weight_updates by other means (work
- * enqueued on the stream outside this API, or host writes) before such a
- * join; a backward pass of the layers below reads none of them.  Same
+ * under the following calls' derive / state.delta work; a later backward
+ * call that writes into a pending dW's delta or input waits for that dW
+ * first.  The caller must not modify a pending call's input, delta or
+ * weight_updates by other means (work enqueued on the stream outside this
+ * API, or host writes) before a join.  Same
  * results; state.delta always gets its own col buffer (the memory note above).
  * TNS_OPT_DERIVE_SUMS (default 0): 1 = the conv backward's Derivative and
  * addSums (no batch norm) in one pass where the sums' chain kernel applies
