@@ -89,14 +89,12 @@ struct tns_ctx {
   // call's return; the next call of any other entry point joins them first
   bool side_pending = false;
   hipStream_t home_stream = nullptr;  // the context's stream while `stream` is aux
-  // the pending dW products' operand ranges (delta, input) and completion
-  // events: a later call's work on `stream` that writes into one waits for it
+  // the pending dW products' operand ranges (delta, input): a later call
+  // whose work on `stream` writes into one joins the side stream first
   struct PendingDw {
     uintptr_t lo[2], hi[2];
-    hipEvent_t ev;
   };
   std::vector<PendingDw> pending;
-  std::vector<hipEvent_t> dw_ev;  // event pool, pending[i] uses dw_ev[i]
   // implicit-GEMM conv k-tables, one per (C, H, W, kH, kW, dY, dX)
   std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int*> ktabs;
 };
@@ -680,7 +678,6 @@ int tns_hip_destroy(tns_ctx* c) {
   if (c->aux_stream) hipStreamDestroy(c->aux_stream);
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->ev_join) hipEventDestroy(c->ev_join);
-  for (hipEvent_t e : c->dw_ev) hipEventDestroy(e);
   for (hipEvent_t e : c->pipe_ev) hipEventDestroy(e);
   delete c;
   return TNS_OK;
@@ -1649,21 +1646,18 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     return set_error(TNS_ERR_ARG, "conv_backward: null batch-norm operand");
   if (pipe) {
     // this call writes delta (in place) and state.delta on the context's
-    // stream: it first waits for the newest pending dW that reads either
-    // (an earlier call on the same layers — the side stream runs in order)
+    // stream: if a pending dW reads either (an earlier call on the same
+    // layers, e.g. the previous pass), the side stream is joined first (no
+    // per-call event: the join is only paid where the ranges meet)
     const uintptr_t w0[2] = {(uintptr_t)delta, (uintptr_t)state_delta};
     const uintptr_t w1[2] = {(uintptr_t)(delta + batch * filters * i_k),
                              (uintptr_t)(state_delta ? state_delta + batch * C * H * W : nullptr)};
-    for (size_t i = c->pending.size(); i-- > 0;) {
-      const tns_ctx::PendingDw& d = c->pending[i];
-      bool hit = false;
+    bool hit = false;
+    for (const tns_ctx::PendingDw& d : c->pending)
       for (int x = 0; x < 2; ++x)
         for (int y = 0; y < 2; ++y) hit |= w0[x] < w1[x] && d.lo[y] < w1[x] && w0[x] < d.hi[y];
-      if (hit) {
-        TNS_HIP_TRY(hipStreamWaitEvent(c->stream, d.ev, 0));
-        break;
-      }
-    }
+    if (hit)
+      if (int r = join_side(c)) return r;
   }
   float* part;
   if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
@@ -1940,26 +1934,13 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     c->home_stream = nullptr;
     c->side_pending = true;
     if (rw) return rw;
-    // the record of this dW: its operands and an event behind it (a full
-    // pool joins everything instead)
-    if (c->pending.size() >= 64) {
-      if (int r = join_side(c)) return r;
-    } else {
-      const size_t k = c->pending.size();
-      if (k == c->dw_ev.size()) {
-        hipEvent_t e = nullptr;
-        TNS_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        c->dw_ev.push_back(e);
-      }
-      TNS_HIP_TRY(hipEventRecord(c->dw_ev[k], c->aux_stream));
-      tns_ctx::PendingDw d;
-      d.lo[0] = (uintptr_t)delta;
-      d.hi[0] = (uintptr_t)(delta + batch * filters * i_k);
-      d.lo[1] = (uintptr_t)input;
-      d.hi[1] = (uintptr_t)(input + batch * C * H * W);
-      d.ev = c->dw_ev[k];
-      c->pending.push_back(d);
-    }
+    // the record of this dW's operands
+    tns_ctx::PendingDw d;
+    d.lo[0] = (uintptr_t)delta;
+    d.hi[0] = (uintptr_t)(delta + batch * filters * i_k);
+    d.lo[1] = (uintptr_t)input;
+    d.hi[1] = (uintptr_t)(input + batch * C * H * W);
+    c->pending.push_back(d);
     return state_delta ? run_dx() : TNS_OK;
   }
   if (!overlap) {
