@@ -1615,6 +1615,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
                        const ConvBN& bn) {
   // (pipelined mode: this call's dW queues behind the pending ones on the
   // side stream; its other work touches none of their operands)
+  if (!c) return check_ctx(c);
   bool pipe = g_bwd_overlap == 2 && !c->telemetry && ensure_side_stream(c);
   if (int r = check_ctx(c, !pipe)) return r;
   if (!act_supported(activation))
