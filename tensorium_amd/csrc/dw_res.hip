@@ -461,42 +461,55 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
       dst + b * dstImg + (int64_t)n * 8 * K4, K4);
 }
 
-// Rows of 256 elements (K4 = 32: the 13^2 planes): eight rows a block, each
-// row's 64 16-byte pieces written straight to their rearranged place — piece
-// a of residue r holds elements i = (a >> 2) + 8 (a & 3) + 2 e, e = 0..3, of
-// kperm's block; a thread two pieces, each four loads and one 16-byte store
-// (a block writes its rows whole, so the lines complete in L2 without the
-// LDS transpose)
+// Rows of up to 1024 elements (K4 = 32 NB, NB <= 4: the 13^2 and 26^2
+// planes): eight rows a block, each row's 64 NB 16-byte pieces written
+// straight to their rearranged place — piece a of kperm block kb of residue r
+// holds elements i = 32 kb + (a >> 2) + 8 (a & 3) + 2 e, e = 0..3; a thread
+// 2 NB pieces, each four loads and one 16-byte store (a block writes its rows
+// whole, so the lines complete in L2 without the LDS transpose)
+struct Piece {
+  int j, r, i0, off;  // row in the block, residue, first element, float offset in the row
+};
+template <int NB>
+__device__ __forceinline__ Piece piece_of(int idx) {
+  constexpr int PR = 64 * NB;  // pieces per row
+  const int j = idx / PR, rem = idx - j * PR, r = rem / (8 * NB), pc = rem - r * (8 * NB);
+  const int kb = pc >> 3, a = pc & 7;
+  return Piece{j, r, 32 * kb + (a >> 2) + 8 * (a & 3), r * 32 * NB + 32 * kb + 4 * a};
+}
+
+template <int NB>
 __global__ __launch_bounds__(256) void res_permute_short_kernel(
     const float* __restrict__ src, int64_t srcImg, float* __restrict__ dst, int64_t dstImg,
     int rows, int K, int K4, int row0, int total) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int idx = (int)threadIdx.x + 256 * u, j = idx >> 6, r = (idx >> 3) & 7, a = idx & 7;
-    const int ra = row0 + 8 * (int)blockIdx.y + j;
+  for (int u = 0; u < 2 * NB; ++u) {
+    const Piece q = piece_of<NB>((int)threadIdx.x + 256 * u);
+    const int ra = row0 + 8 * (int)blockIdx.y + q.j;
     if (ra >= total) continue;
     const int b = ra / rows, row = ra - b * rows;
     const float* s = src + b * srcImg + (int64_t)row * K;
     float v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int pp = r + 8 * ((a >> 2) + 8 * (a & 3) + 2 * e);
+      const int pp = q.r + 8 * (q.i0 + 2 * e);
       v[e] = pp < K ? s[pp] : 0.0f;
     }
-    *reinterpret_cast<float4*>(dst + b * dstImg + (int64_t)row * 8 * K4 + r * K4 + 4 * a) =
+    *reinterpret_cast<float4*>(dst + b * dstImg + (int64_t)row * 8 * K4 + q.off) =
         make_float4(v[0], v[1], v[2], v[3]);
   }
 }
 
+template <int NB>
 __global__ __launch_bounds__(256) void im2col_res_short_kernel(
     const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int H,
     int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
     int rows, int K4, int row0, int total) {
   const int taps = kH * kW;
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int idx = (int)threadIdx.x + 256 * u, j = idx >> 6, r = (idx >> 3) & 7, a = idx & 7;
-    const int ra = row0 + 8 * (int)blockIdx.y + j;
+  for (int u = 0; u < 2 * NB; ++u) {
+    const Piece q = piece_of<NB>((int)threadIdx.x + 256 * u);
+    const int ra = row0 + 8 * (int)blockIdx.y + q.j;
     if (ra >= total) continue;
     const int b = ra / rows, n = ra - b * rows;
     const int c = n / taps, t = n - c * taps, kr = t / kW, kc = t - kr * kW;
@@ -504,14 +517,14 @@ __global__ __launch_bounds__(256) void im2col_res_short_kernel(
     float v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int pp = r + 8 * ((a >> 2) + 8 * (a & 3) + 2 * e);
+      const int pp = q.r + 8 * (q.i0 + 2 * e);
       const int oy = pp / oW, ox = pp - oy * oW;
       const int iy = oy * sY - pH + kr * dY, ix = ox * sX - pW + kc * dX;
       v[e] = (pp < HWo && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
                  ? xc[iy * W + ix]
                  : 0.0f;
     }
-    *reinterpret_cast<float4*>(dst + b * dstImg + (int64_t)n * 8 * K4 + r * K4 + 4 * a) =
+    *reinterpret_cast<float4*>(dst + b * dstImg + (int64_t)n * 8 * K4 + q.off) =
         make_float4(v[0], v[1], v[2], v[3]);
   }
 }
@@ -631,7 +644,16 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       });
     });
   };
-  if (rowlen <= 256) {
+  if (rowlen <= 1024) {
+    const int nb = (int)(K4 / 32);
+    auto by_nb = [&](auto&& f) {
+      switch (nb) {
+        case 1: f(std::integral_constant<int, 1>{}); break;
+        case 2: f(std::integral_constant<int, 2>{}); break;
+        case 3: f(std::integral_constant<int, 3>{}); break;
+        default: f(std::integral_constant<int, 4>{}); break;
+      }
+    };
     auto short_launch = [&](int64_t nrows, auto&& launch) -> hipError_t {
       const int64_t groups = (nrows + 7) / 8;
       for (int64_t g0 = 0; g0 < groups; g0 += 65535) {
@@ -641,22 +663,30 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       return hipSuccess;
     };
     if (hipError_t e = short_launch(d.batch * d.M, [&](dim3 gr, int r0, int tot) {
-          hipLaunchKernelGGL(res_permute_short_kernel, gr, dim3(256), 0, s, d.delta, d.M * d.K,
-                             d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4, r0, tot);
+          by_nb([&](auto c) {
+            hipLaunchKernelGGL((res_permute_short_kernel<decltype(c)::value>), gr, dim3(256), 0, s,
+                               d.delta, d.M * d.K, d.dA, d.M * rowlen, (int)d.M, (int)d.K, (int)K4,
+                               r0, tot);
+          });
         });
         e != hipSuccess)
       return e;
     if (hipError_t e = short_launch(d.batch * d.N, [&](dim3 gr, int r0, int tot) {
-          if (d.direct) {
-            hipLaunchKernelGGL(res_permute_short_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                               npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0, tot);
-          } else {
-            const ConvGeom& g = d.g;
-            hipLaunchKernelGGL(im2col_res_short_kernel, gr, dim3(256), 0, s, d.x, d.xStride, d.dB,
-                               npad * rowlen, (int)g.H, (int)g.W, (int)g.kH, (int)g.kW, (int)g.sY,
-                               (int)g.sX, (int)g.padH, (int)g.padW, (int)g.dY, (int)g.dX,
-                               (int)g.ow, (int)d.K, (int)d.N, (int)K4, r0, tot);
-          }
+          by_nb([&](auto c) {
+            constexpr int NB = decltype(c)::value;
+            if (d.direct) {
+              hipLaunchKernelGGL((res_permute_short_kernel<NB>), gr, dim3(256), 0, s, d.x,
+                                 d.xStride, d.dB, npad * rowlen, (int)d.N, (int)d.K, (int)K4, r0,
+                                 tot);
+            } else {
+              const ConvGeom& g = d.g;
+              hipLaunchKernelGGL((im2col_res_short_kernel<NB>), gr, dim3(256), 0, s, d.x,
+                                 d.xStride, d.dB, npad * rowlen, (int)g.H, (int)g.W, (int)g.kH,
+                                 (int)g.kW, (int)g.sY, (int)g.sX, (int)g.padH, (int)g.padW,
+                                 (int)g.dY, (int)g.dX, (int)g.ow, (int)d.K, (int)d.N, (int)K4,
+                                 r0, tot);
+            }
+          });
         });
         e != hipSuccess)
       return e;

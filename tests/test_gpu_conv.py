@@ -486,7 +486,8 @@ def test_conv_backward_dw_tiles(hip, torch_cuda, ora):
 DWR_CASES = [(3, 128, 11, 128, 3, 1, 1, 9), (2, 64, 13, 64, 3, 1, 1, 9), (2, 64, 20, 128, 3, 2, 1, 1),
              (1, 128, 26, 256, 3, 1, 1, 9), (2, 64, 9, 64, 1, 1, 0, 4), (9, 64, 12, 64, 3, 1, 1, 9),
              (2, 128, 10, 128, 3, 1, 1, 9, 2), (1, 32, 48, 64, 3, 1, 1, 9), (2, 3, 20, 64, 3, 1, 1, 1),
-             (1, 16, 72, 64, 3, 1, 1, 9), (2, 16, 144, 64, 3, 2, 1, 1)]
+             (1, 16, 72, 64, 3, 1, 1, 9), (2, 16, 144, 64, 3, 2, 1, 1), (1, 64, 20, 64, 3, 1, 1, 9),
+             (1, 64, 30, 64, 3, 1, 1, 1)]
 
 
 def test_conv_backward_dw_res_forms(hip, torch_cuda, ora):
