@@ -461,8 +461,8 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
       dst + b * dstImg + (int64_t)n * 8 * K4, K4);
 }
 
-// Rows of up to 1024 elements (K4 = 32 NB, NB <= 4: the 13^2 and 26^2
-// planes): eight rows a block, each row's 64 NB 16-byte pieces written
+// Rows of up to 1024 elements (K4 = 32 NB, NB <= 4; launched for the 13^2
+// planes' NB = 1): eight rows a block, each row's 64 NB 16-byte pieces written
 // straight to their rearranged place — piece a of kperm block kb of residue r
 // holds elements i = 32 kb + (a >> 2) + 8 (a & 3) + 2 e, e = 0..3; a thread
 // 2 NB pieces, each four loads and one 16-byte store (a block writes its rows
@@ -644,7 +644,9 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       });
     });
   };
-  if (rowlen <= 1024) {
+  // (direct short rows only for K4 = 32: at K4 = 96, the 26^2 planes, the
+  // LDS row chunks measured faster, 25.6 vs 28.0 us, profiles/r04_dw_res_forms12)
+  if (rowlen <= 256) {
     const int nb = (int)(K4 / 32);
     auto by_nb = [&](auto&& f) {
       switch (nb) {
