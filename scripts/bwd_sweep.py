@@ -58,6 +58,9 @@ def main():
             torch.cuda.synchronize()
             return round(e0.elapsed_time(e1) / a.reps, 4)
 
+        for _ in range(50):  # a warm clock before the first timed form (~50 calls)
+            run()
+        torch.cuda.synchronize()
         row = {"shape": f"{s.c}x{s.h} k{s.size}s{s.stride}->{s.filters}", "default": timed()}
         if "dw" in a.what:
             forms = ([("sdot", f) for f in [0] + [1 + v for v in range(n_chain)] +
