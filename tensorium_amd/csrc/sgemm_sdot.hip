@@ -275,11 +275,13 @@ hipError_t launch_sgemm_nt_sdot(const GemmArgs& a, hipStream_t s) {
   // few outputs over a long k (conv dW of the 416/208/104-pixel YOLOv3
   // layers): the VALU chain kernel, tile by output count (scripts/
   // sdot_forms.py, profiles/r02_sdot_forms.json: YOLOv3 layer 0 dW at batch
-  // 8 1.44 -> 0.28 ms, layer 2 0.35 -> 0.10 ms, layer 5 0.089 -> 0.056 ms)
+  // 8 1.44 -> 0.28 ms, layer 2 0.35 -> 0.10 ms, layer 5 0.089 -> 0.056 ms;
+  // the 104^2 1x1 layers' 65536 outputs on four residues a lane, 0.130 ->
+  // 0.115 ms a call, profiles/r04_bwd_dw_sweep.json)
   const int64_t t32 = ((a.M + 31) / 32) * ((a.N + 31) / 32) * a.batch;
   if (g_sdot_form < 0 && a.K >= 4096 && t32 <= 64) {
     const int64_t outs = a.M * a.N * a.batch;
-    return launch_sdot_chains(a, outs <= 8192 ? 1 : (outs <= 32768 ? 2 : 4), s);
+    return launch_sdot_chains(a, outs <= 8192 ? 1 : (outs <= 32768 ? 2 : 6), s);
   }
   // many 64x64 tiles over a short k (conv dW of the 26^2 / 13^2 layers, k =
   // pixels per image): two waves per 32x32 tile, four residue chains each
