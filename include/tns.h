@@ -143,6 +143,9 @@ typedef struct tns_ctx tns_ctx;
 int  tns_hip_create(int32_t deviceIndex, tns_ctx** out);
 int  tns_hip_destroy(tns_ctx* ctx);
 int  tns_hip_set_stream(tns_ctx* ctx, void* hipStream);   /* hipStream_t */
+/* The context's stream, after it has been made to wait for any pipelined
+ * conv-backward dW products still pending on the side stream
+ * (TNS_OPT_BWD_OVERLAP = 2), so work enqueued on it sees their results. */
 void* tns_hip_get_stream(tns_ctx* ctx);
 int  tns_hip_finish(tns_ctx* ctx);                         /* nncuda.pas:1575 */
 
@@ -592,10 +595,14 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * context's stream wait for the side stream.  The dW of layer L then runs
  * under the following calls' derive / state.delta work; a later backward
  * call that writes into a pending dW's delta or input waits for that dW
- * first.  The caller must not modify a pending call's input, delta or
- * weight_updates by other means (work enqueued on the stream outside this
- * API, or host writes) before a join.  Same
- * results; state.delta always gets its own col buffer (the memory note above).
+ * first.  The caller must not read or modify a pending call's weight_updates,
+ * nor modify its input or delta, by other means (work enqueued on the stream
+ * outside this API, or host accesses) before a join: tns_hip_finish, any
+ * other entry point, or tns_hip_get_stream (which joins before it hands the
+ * stream out, so work the caller then enqueues on it is ordered after every
+ * pending dW).  Same results; state.delta always gets its own col buffer
+ * (the memory note above).  pascal/nnHip.pas initHIP selects this mode by
+ * default (pipelineBackward = true): there every access goes through the API.
  * TNS_OPT_DERIVE_SUMS (default 0): 1 = the conv backward's Derivative and
  * addSums (no batch norm) in one pass where the sums' chain kernel applies
  * (planes under 16384 pixels); 0 = two passes (measured level: 15.06 vs

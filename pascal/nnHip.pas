@@ -363,8 +363,19 @@ var
   once; device buffers of TTensor mirror as under USE_CUDART.  srssQuirk as
   useHipOpTable below: true (the default) selects the configured USE_AVX2
   lane drop of srss / sVarinceDelta_avx, so TNNHip.variances /
-  meansAndVarsDelta reproduce the CPU build's batch-norm statistics. }
-procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean = true);
+  meansAndVarsDelta reproduce the CPU build's batch-norm statistics.
+  pipelineBackward = true (the default) sets TNS_OPT_BWD_OVERLAP = 2: each
+  convBackward call (TConvolutionalLayer.backwardGPU, in TNet.backward's
+  loop nnet.pas:332-366) leaves its dW product running on the context's side
+  stream under the following layers' work; the next call of any other
+  TNNHip method (sgdUpdate in TNet.update, readBuffer, finish, a non-conv
+  layer's backward) joins it first, so every access made through TNNHip
+  sees finished weight_updates.  Contract (include/tns.h): nothing may read
+  or write a pending layer's weight_updates, or write its input or delta,
+  outside this API before such a join.  false keeps the library default
+  (1: dW and state.delta concurrently, joined before each call returns). }
+procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean = true;
+  const pipelineBackward: boolean = true);
 
 { Bind the host-pointer op-table drop-ins (boundary A) after
   TTensorOps.initSingle, as USE_OPENBLAS / USE_MKL do (ntensors.pas:
@@ -729,12 +740,17 @@ end;
 
 { ---- process-wide setup ---------------------------------------------------- }
 
-procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean);
+procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean;
+  const pipelineBackward: boolean);
 begin
   if srssQuirk then
     tns_set_option(TNS_OPT_SRSS_QUIRK, 1)
   else
     tns_set_option(TNS_OPT_SRSS_QUIRK, 0);
+  if pipelineBackward then
+    tns_set_option(TNS_OPT_BWD_OVERLAP, 2)
+  else
+    tns_set_option(TNS_OPT_BWD_OVERLAP, 1);
   if not assigned(hip) then
     hip := TNNHip<single>.Create(deviceIndex)
 end;

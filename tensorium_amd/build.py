@@ -61,6 +61,15 @@ def build_hip(verbose: bool = False, force: bool = False, out: Path | None = Non
     lib_path = (out / "libtensorium_hip.so") if out else LIB
     build.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.hpp")) + [ROOT / "include" / "tns.h"]
+    extra = os.environ.get("TNS_EXTRA_CFLAGS", "").split()  # A/B side builds
+    if os.environ.get("TNS_DIAG") == "1":   # + the measured, not picked forms
+        extra.append("-DTNS_DIAG_KERNELS")
+    # the flag set the objects were compiled with: a different set (e.g.
+    # TNS_DIAG toggled) rebuilds everything, never a mix of the two
+    stamp = build / "flags.stamp"
+    flags = " ".join([*CXXFLAGS, *extra])
+    if not stamp.exists() or stamp.read_text() != flags:
+        force = True
     objs: list[Path] = []
     jobs = []
     for src in _sources():
@@ -68,13 +77,12 @@ def build_hip(verbose: bool = False, force: bool = False, out: Path | None = Non
         objs.append(obj)
         if force or _newer(obj, [src, *headers]):
             lang = ["-x", "hip"] if src.suffix == ".hip" else []
-            extra = os.environ.get("TNS_EXTRA_CFLAGS", "").split()  # A/B side builds
-            if os.environ.get("TNS_DIAG") == "1":   # + the measured, not picked forms
-                extra.append("-DTNS_DIAG_KERNELS")
             jobs.append([HIPCC, *CXXFLAGS, *extra, *lang, "-c", str(src), "-o", str(obj)])
     if jobs:
+        stamp.unlink(missing_ok=True)  # (a failed build leaves no stamp)
         with ThreadPoolExecutor(max_workers=min(len(jobs), 8)) as ex:
             list(ex.map(lambda c: _run(c, verbose), jobs))
+        stamp.write_text(flags)
     if force or jobs or _newer(lib_path, objs):
         tmp = lib_path.with_suffix(".so.tmp")
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o",

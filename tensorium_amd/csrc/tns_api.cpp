@@ -127,6 +127,17 @@ int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
   return TNS_OK;
 }
 
+// give a scratch buffer back (every stream that may still use it drained)
+void release_scratch(tns_ctx* c, int slot) {
+  if (!c->scratch[slot]) return;
+  hipStreamSynchronize(c->stream);
+  if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+  if (c->home_stream) hipStreamSynchronize(c->home_stream);
+  hipFree(c->scratch[slot]);
+  c->scratch[slot] = nullptr;
+  c->scratch_elems[slot] = 0;
+}
+
 // the conv backward's side stream and its fork / join events, created
 // together on the context's device; false (nothing kept) if any of them
 // cannot be created, and the caller runs its sequential schedule
@@ -694,7 +705,12 @@ int tns_hip_set_stream(tns_ctx* c, void* s) {
   return TNS_OK;
 }
 
-void* tns_hip_get_stream(tns_ctx* c) { return c ? (void*)c->stream : nullptr; }
+void* tns_hip_get_stream(tns_ctx* c) {
+  // (pipelined backward: work the caller enqueues on the stream must see
+  // the pending dW products' weight_updates — join them first)
+  if (!c || join_side(c)) return nullptr;
+  return (void*)c->stream;
+}
 
 int tns_hip_finish(tns_ctx* c) {
   if (int r = check_ctx(c)) return r;
@@ -784,9 +800,22 @@ int tns_hip_gemm_batched(tns_ctx* c, uint8_t transA, uint8_t transB, int64_t M, 
     *st = (int64_t)(d / (intptr_t)sizeof(float));
     return true;
   };
+  // — only when the batch's GEMMs are independent: the C entries do not
+  // overlap one another and no C entry overlaps an A or B entry (the launch
+  // runs them concurrently; the loop below keeps the array order)
+  const int64_t extA = transA ? (K - 1) * lda + M : (M - 1) * lda + K;
+  const int64_t extB = transB ? (N - 1) * ldb + K : (K - 1) * ldb + N;
+  const int64_t extC = (M - 1) * ldc + N;
+  auto disjoint = [](const float* p, int64_t n, const float* q, int64_t m) {
+    return p + n <= q || q + m <= p;
+  };
   int64_t sA, sB, sC;
   if (stride_of(pa, &sA) && stride_of(pb, &sB) && stride_of(pc, &sC) &&
-      (sC > 0 || batchCount == 1))
+      (batchCount == 1 || sC >= extC) &&
+      disjoint(pc[0] + cOffset, sC * (batchCount - 1) + extC, pa[0] + aOffset,
+               sA * (batchCount - 1) + extA) &&
+      disjoint(pc[0] + cOffset, sC * (batchCount - 1) + extC, pb[0] + bOffset,
+               sB * (batchCount - 1) + extB))
     return do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, pa[0] + aOffset, lda, sA,
                    pb[0] + bOffset, ldb, sB, BETA, pc[0] + cOffset, ldc, sC, batchCount, EPI_NONE,
                    nullptr, 0);
@@ -1732,8 +1761,26 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
       dwr = (int)g_dw_res;
     else if (kSize == 3)  // (1x1 layers: behind the sdot kernels, 0.048 -> 0.058 ms at 52^2)
       dwr = dw_res_pick(i_m, i_n, i_k, batch);
-    if (dwr >= 0) dwv = -1;
   }
+  // its scratch (residue-major copies, group planes: in addition to the
+  // caller's workspace), sized before any fork; when the form was picked by
+  // shape and that memory cannot be had, the dW falls back to the paths
+  // that need only the workspace (dw_tile, or im2col + the sdot kernels)
+  DwResArgs dres{};
+  if (dwr >= 0) {
+    const int64_t rowlen = 8 * dw_res_k4(i_k);
+    int r = ensure_scratch(c, SLOT_RES_A, batch * i_m * rowlen + 32, &dres.dA);
+    if (!r) r = ensure_scratch(c, SLOT_RES_B, batch * dw_res_b_rows(dwr, i_n) * rowlen + 32, &dres.dB);
+    if (!r) r = ensure_scratch(c, SLOT_DW, batch * dw_res_groups(dwr) * i_m * i_n, &dres.part);
+    if (r) {
+      if (g_dw_res >= 0) return r;  // (forced: the error stands)
+      tns_clear_error();
+      release_scratch(c, SLOT_RES_A);
+      release_scratch(c, SLOT_RES_B);
+      dwr = -1;
+    }
+  }
+  if (dwr >= 0) dwv = -1;
   // a 1x1/s1/p0 layer's col2im adds each col element to its own pixel once:
   // the dX product adds into state.delta in its epilogue instead (EPI_ADD,
   // the same add), no col matrix
@@ -1790,18 +1837,12 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   auto run_dw = [&]() -> int {
     const float* col = input;
     if (dwr >= 0) {
-      DwResArgs d{};
+      DwResArgs d = dres;  // (scratch sized above)
       d.g = g;
       d.x = input; d.xStride = C * H * W;
       d.delta = delta; d.weight_updates = weight_updates;
       d.M = i_m; d.N = i_n; d.K = i_k; d.batch = batch;
       d.direct = !needs_col; d.alpha = 1.0f;
-      const int64_t rowlen = 8 * dw_res_k4(i_k);
-      if (int r = ensure_scratch(c, SLOT_RES_A, batch * i_m * rowlen + 32, &d.dA)) return r;
-      if (int r = ensure_scratch(c, SLOT_RES_B, batch * dw_res_b_rows(dwr, i_n) * rowlen + 32, &d.dB))
-        return r;
-      if (int r = ensure_scratch(c, SLOT_DW, batch * dw_res_groups(dwr) * i_m * i_n, &d.part))
-        return r;
       OpTimer t(c, TNS_OP_GEMM);
       const hipError_t e = launch_dw_res(dwr, d, c->stream);
       if (e == hipErrorInvalidValue)

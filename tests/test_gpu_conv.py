@@ -413,6 +413,118 @@ def test_conv_backward_pipelined_chain(hip, torch_cuda):
         assert np.array_equal(a, b)
 
 
+def _residual_block_case(seed):
+    """YOLOv3 layers 9, 10, 11 and the shortcut that adds layer 11's output
+    to layer 9's (a darknet residual block at 52^2, batch 8): inputs,
+    outputs, deltas, weights and the layers' update buffers."""
+    from tensorium_amd.yolo import yolov3_conv_table
+    specs = [yolov3_conv_table()[i] for i in (9, 10, 11)]
+    B = 8
+    rng = np.random.default_rng(seed)
+    x0 = rng.uniform(0, 1, (B, specs[0].c, specs[0].h, specs[0].h)).astype(np.float32)
+    outs = [rng.uniform(-1, 1, (B, s.filters, s.out_h, s.out_h)).astype(np.float32) for s in specs]
+    deltas = [rng.uniform(-1, 1, o.shape).astype(np.float32) for o in outs]
+    d_sc = rng.uniform(-1, 1, outs[2].shape).astype(np.float32)   # the shortcut layer's delta
+    ws = [rng.uniform(-0.1, 0.1, (s.filters, s.K)).astype(np.float32) for s in specs]
+    bs = [rng.uniform(-0.1, 0.1, s.filters).astype(np.float32) for s in specs]
+    wus = [rng.uniform(-1, 1, w.shape).astype(np.float32) for w in ws]
+    bus = [rng.uniform(-1, 1, s.filters).astype(np.float32) for s in specs]
+    return specs, B, x0, outs, deltas, d_sc, ws, bs, wus, bus
+
+
+def _residual_block_oracle(ora, specs, x0, outs, deltas, d_sc, ws, bs, wus, bus, lr, B, decay, mom):
+    D, W, Bi, WU, BU = ([a.copy() for a in arr] for arr in (deltas, ws, bs, wus, bus))
+    # TNet.backward (nnet.pas:332-366), i = 3 .. 0: the shortcut (TAddLayer,
+    # linear: its delta added to layer 11's and to layer 9's, naddlayer.pas)
+    D[2] += d_sc
+    D[0] += d_sc
+    inputs = [x0, outs[0], outs[1]]
+    for j in (2, 1, 0):
+        s = specs[j]
+        ora.conv_backward(inputs[j], W[j].ravel(), s.filters, s.size, s.stride, s.pad, s.activation,
+                          outs[j], D[j], BU[j], WU[j].ravel(), D[j - 1] if j else None)
+    # TNet.update: every layer's TConvolutionalLayer.update, fused
+    f32 = np.float32
+    lrb = f32(f32(lr) / f32(B))
+    ndb = f32(-f32(decay) * f32(B))
+    for j in range(3):
+        wflat, wuflat = W[j].reshape(-1), WU[j].reshape(-1)
+        ora.sgd_update(wflat, wuflat, Bi[j], BU[j], None, None, float(lrb), float(ndb), mom)
+    return D, W, Bi, WU, BU
+
+
+@pytest.mark.parametrize("pipelined", [True, False])
+def test_tnet_backward_order_through_tnnhip(hip, torch_cuda, ora, pipelined):
+    """TNet.backward's loop (nnet.pas:332-366) replayed through TNNHip over a
+    darknet residual block (YOLOv3 layers 9, 10, 11 + the shortcut) at batch
+    8: the shortcut's backward (two addvv calls — a non-conv TNNHip call
+    between the conv backward calls) first, then the conv layers from the top
+    down, each taking the layer below's delta as state.delta (layer 9, the
+    first, none), then TNet.update's sgdUpdate per layer — on the pipelined
+    schedule initHIP selects (each conv layer's dW left on the side stream)
+    and on the joined one; every delta, weight, bias and update bit-exact
+    against the oracle's restated sequence."""
+    specs, B, x0, outs, deltas, d_sc, ws, bs, wus, bus = _residual_block_case(911)
+    lr, decay, mom = 1e-3, 5e-4, 0.9
+    rD, rW, rB, rWU, rBU = _residual_block_oracle(ora, specs, x0, outs, deltas, d_sc, ws, bs, wus,
+                                                  bus, lr, B, decay, mom)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    X, O, D, W = t(x0), [t(o) for o in outs], [t(d) for d in deltas], [t(w) for w in ws]
+    Bi, WU, BU, DSC = [t(b) for b in bs], [t(w) for w in wus], [t(b) for b in bus], t(d_sc)
+    try:
+        hip.setBwdOverlap(2 if pipelined else 1)
+        n = DSC.numel()
+        hip.addvv(n, D[2], 0, 1, DSC, 0, 1, D[2], 0, 1)
+        hip.addvv(n, D[0], 0, 1, DSC, 0, 1, D[0], 0, 1)
+        inputs = [X, O[0], O[1]]
+        for j in (2, 1, 0):
+            s = specs[j]
+            hip.convBackward(B, s.c, s.h, s.h, inputs[j], W[j], s.filters, s.size, s.stride, s.pad, 1,
+                             s.activation, O[j], D[j], BU[j], WU[j], None, D[j - 1] if j else None)
+        for j in range(3):
+            hip.sgdUpdate(W[j], WU[j], Bi[j], BU[j], lr, B, decay, mom)
+        hip.finish()
+    finally:
+        hip.setBwdOverlap(True)
+    for got, ref in ((D, rD), (W, rW), (Bi, rB), (WU, rWU), (BU, rBU)):
+        for g, r in zip(got, ref):
+            assert np.array_equal(g.cpu().numpy(), r)
+
+
+def test_pipelined_backward_get_stream_joins(hip, torch_cuda, ora):
+    """A pipelined pass (TNS_OPT_BWD_OVERLAP = 2) leaves the dW products on
+    the side stream; tns_hip_get_stream joins them before handing out the
+    context's stream, so a torch read of weight_updates enqueued
+    on that stream right after the pass — no finish — sees the finished sums."""
+    specs, B, x0, outs, deltas, d_sc, ws, bs, wus, bus = _residual_block_case(912)
+    rD, rWU, rBU = [d.copy() for d in deltas], [w.copy() for w in wus], [b.copy() for b in bus]
+    inputs = [x0, outs[0], outs[1]]
+    for j in (2, 1, 0):
+        s = specs[j]
+        ora.conv_backward(inputs[j], ws[j].ravel(), s.filters, s.size, s.stride, s.pad,
+                          s.activation, outs[j], rD[j], rBU[j], rWU[j].ravel(),
+                          rD[j - 1] if j else None)
+    t = lambda a: torch_cuda.from_numpy(a.copy()).cuda()  # noqa: E731
+    X, O, D, W = t(x0), [t(o) for o in outs], [t(d) for d in deltas], [t(w) for w in ws]
+    WU, BU = [t(w) for w in wus], [t(b) for b in bus]
+    try:
+        hip.setBwdOverlap(2)
+        hip.finish()
+        ins = [X, O[0], O[1]]
+        for j in (2, 1, 0):
+            s = specs[j]
+            hip.convBackward(B, s.c, s.h, s.h, ins[j], W[j], s.filters, s.size, s.stride, s.pad, 1,
+                             s.activation, O[j], D[j], BU[j], WU[j], None, D[j - 1] if j else None)
+        stream = torch_cuda.cuda.ExternalStream(hip.stream)   # (joins the pending dW)
+        with torch_cuda.cuda.stream(stream):
+            snap = [w.clone() for w in WU]
+        stream.synchronize()
+    finally:
+        hip.setBwdOverlap(True)
+    for g, r in zip(snap, rWU):
+        assert np.array_equal(g.cpu().numpy(), r)
+
+
 @pytest.mark.parametrize("idx", [3, 4, 9, 10, 11, 27, 28, 44, 45, 58])
 def test_conv_backward_dx_yolov3_batch8(hip, torch_cuda, ora, idx):
     """state.delta at YOLOv3 layer shapes, batch 8, on the default path (the

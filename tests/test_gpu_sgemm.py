@@ -326,6 +326,48 @@ def test_gemm_batched_pointer_arrays(hip, torch_cuda, ora, ta, tb, layout):
         assert np.array_equal(got[i], ref), i
 
 
+@pytest.mark.parametrize("alias", ["overlap", "c_is_b"])
+def test_gemm_batched_dependent_entries_in_order(hip, torch_cuda, ora, alias):
+    """gemmBatched whose equally spaced entries are NOT independent: C entries
+    one row apart (each GEMM reads rows the previous one wrote, BETA = 1), or
+    C entry i the B entry i+1 — run GEMM by GEMM in array order (the header's
+    contract), not as one concurrent strided launch: bit-exact against the
+    oracle applied entry by entry to one buffer."""
+    T = torch_cuda
+    batch, M, N, K = 4, 24, 32, 32
+    rng = np.random.default_rng(11)
+    A = rng.uniform(-1, 1, (M * K,)).astype(np.float32)
+    if alias == "overlap":
+        buf = rng.uniform(-1, 1, (M * N + (batch - 1) * N,)).astype(np.float32)
+        Bs = rng.uniform(-1, 1, (batch * K * N,)).astype(np.float32)
+        dA, dB, dBuf = (T.from_numpy(x.copy()).cuda() for x in (A, Bs, buf))
+        pa = [dA.data_ptr()] * batch
+        pb = [dB.data_ptr() + 4 * i * K * N for i in range(batch)]
+        pc = [dBuf.data_ptr() + 4 * i * N for i in range(batch)]
+        ref = buf.copy()
+        for i in range(batch):
+            c = ref[i * N:i * N + M * N].copy()
+            ora.sgemm(False, False, M, N, K, 1.0, A, K, Bs[i * K * N:(i + 1) * K * N], N, 1.0, c, N)
+            ref[i * N:i * N + M * N] = c
+    else:  # K == M: C_i (M x N) is B_{i+1} (K x N)
+        buf = rng.uniform(-1, 1, ((batch + 1) * K * N,)).astype(np.float32)
+        dA, dBuf = (T.from_numpy(x.copy()).cuda() for x in (A, buf))
+        pa = [dA.data_ptr()] * batch
+        pb = [dBuf.data_ptr() + 4 * i * K * N for i in range(batch)]
+        pc = [dBuf.data_ptr() + 4 * (i + 1) * K * N for i in range(batch)]
+        ref = buf.copy()
+        for i in range(batch):
+            c = ref[(i + 1) * K * N:(i + 2) * K * N].copy()
+            ora.sgemm(False, False, M, N, K, 1.0, A, K, ref[i * K * N:(i + 1) * K * N].copy(), N,
+                      1.0, c, N)
+            ref[(i + 1) * K * N:(i + 2) * K * N] = c
+    arrs = [np.array(p, np.int64) for p in (pa, pb, pc)]
+    hip.gemmBatched(False, False, M, N, K, 1.0, arrs[0].ctypes.data, 0, K, arrs[1].ctypes.data, 0,
+                    N, 1.0, arrs[2].ctypes.data, 0, N, batch)
+    hip.finish()
+    assert np.array_equal(dBuf.cpu().numpy(), ref)
+
+
 def test_beta0_strict_propagates_nan(hip, torch_cuda, hiplib):
     A = np.ones((4, 4), np.float32)
     C = np.zeros((4, 4), np.float32)

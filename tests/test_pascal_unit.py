@@ -140,9 +140,13 @@ def test_tnnhip_has_tnncuda_method_list():
 
 def test_init_and_op_table_binding():
     src = PAS.read_text()
-    assert "procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean = true);" in src
-    body = src[src.index("procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean);"):]
-    assert "tns_set_option(TNS_OPT_SRSS_QUIRK, 1)" in body[:400]   # initHIP applies the drop
+    assert re.search(r"procedure initHIP\(const deviceIndex: SizeInt; const srssQuirk: boolean = true;"
+                     r"\s+const pipelineBackward: boolean = true\);", src)
+    i = src.index("procedure initHIP(const deviceIndex: SizeInt; const srssQuirk: boolean;")
+    body = src[i:src.index("end;", i)]
+    assert "tns_set_option(TNS_OPT_SRSS_QUIRK, 1)" in body   # initHIP applies the drop
+    # ... and, by default, the pipelined conv backward the bench headlines
+    assert re.search(r"if pipelineBackward then\s+tns_set_option\(TNS_OPT_BWD_OVERLAP, 2\)", body)
     assert "procedure useHipOpTable(const srssQuirk: boolean = true);" in src
     assert "tns_set_option(TNS_OPT_SRSS_QUIRK, 1)" in src
     for slot, fn in [("gemm", "tns_cblas_sgemm"), ("gemmStridedBatched",
