@@ -1,0 +1,39 @@
+#!/bin/bash
+# Round-5 GPU batch: STEPS selects the steps (space-separated names).
+#   tests   — pytest -m gpu (whole suite, or TESTS=<pytest args>)
+#   abfwd   — conv forward A/B: LIBS builds under ab/ (+ "main" = the tree)
+#   bwdab   — conv backward schedules (bwd_graph.py) for LIBS
+#   bench   — python bench.py (default flags) -> gpurun_out/bench.json
+#   trace   — rocprofv3 kernel trace of BENCH_ARGS -> gpurun_out/prof_trace
+set -u
+mkdir -p gpurun_out
+lib_of() { [ "$1" = main ] && echo tensorium_amd/libtensorium_hip.so || echo ab/$1/libtensorium_hip.so; }
+for S in ${STEPS}; do
+  case $S in
+    tests)
+      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:-} > gpurun_out/gpu_tests.log 2>&1
+      rc=$?; tail -5 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+    abfwd)
+      for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do
+        TNS_LIB=$(lib_of $L) timeout -k 10 300 python -u scripts/quick_perf.py --tag $L --yolo-only >> gpurun_out/abfwd.jsonl 2> gpurun_out/abfwd_$L.err
+        rc=$?; [ $rc -eq 0 ] || { echo "$L rc=$rc"; tail -5 gpurun_out/abfwd_$L.err; exit $rc; }
+      done; done
+      python3 -c "
+import json
+for l in open('gpurun_out/abfwd.jsonl'):
+    r=json.loads(l); print(r['tag'], r['yolo_ms'], r['yolo_tflops'])" ;;
+    bwdab)
+      for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do
+        echo "{\"tag\": \"$L\"}" >> gpurun_out/bwdab.jsonl
+        TNS_LIB=$(lib_of $L) timeout -k 10 400 python -u scripts/bwd_graph.py --rounds 1 >> gpurun_out/bwdab.jsonl 2> gpurun_out/bwdab_$L.err
+        rc=$?; [ $rc -eq 0 ] || { echo "$L rc=$rc"; tail -5 gpurun_out/bwdab_$L.err; exit $rc; }
+      done; done
+      cat gpurun_out/bwdab.jsonl | cut -c1-400 ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+      rc=$?; tail -c 3000 gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; } ;;
+    trace)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o trace -- python3 bench.py ${BENCH_ARGS:---no-cpu} > gpurun_out/trace_bench.json 2> gpurun_out/trace.err
+      rc=$?; [ $rc -eq 0 ] || { tail -5 gpurun_out/trace.err; exit $rc; } ;;
+  esac
+done

@@ -157,7 +157,12 @@ def load(path: str | os.PathLike | None = None) -> C.CDLL:
         raise TnsError(f"{p} not built — run `python -m tensorium_amd.build` "
                        "(the HIP backend has no CPU fallback)")
     lib = C.CDLL(str(p), mode=C.RTLD_GLOBAL)
+    # (an A/B build of an older revision may lack entry points added since;
+    # only the in-tree library must export every one)
+    older = bool(os.environ.get("TNS_LIB")) and path is None
     for name, (res, args) in PROTOTYPES.items():
+        if older and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -373,6 +373,9 @@ __global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restric
 // CH/8 consecutive i written as one run (LDS row stride 264: both phases
 // conflict-free).
 constexpr int RCH = 2048, RLD = 264;
+// im2col_res_lds_kernel's input stage (dynamic LDS), beside its 16.9 KB
+// transpose buffers: two blocks a CU
+constexpr int64_t kResStageBytes = 44 * 1024;
 
 // position of chain element i in its row: each 32-element block stored as
 // [h][q][j] for element 32 b + 8 q + h + 2 j (the kernel's step groups)
@@ -459,6 +462,100 @@ __global__ __launch_bounds__(256) void im2col_res_kernel(const float* __restrict
         return ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W) ? xc[iy * W + ix] : 0.0f;
       },
       dst + b * dstImg + (int64_t)n * 8 * K4, K4);
+}
+
+// The same rows from one block per (image, channel, chunk of output pixels):
+// the input rows the chunk's windows cover are staged in LDS ONCE (one
+// contiguous span of the plane, coalesced), and the block writes the chunk of
+// all kH * kW rows n = (c, kr, kc) from there, tap after tap — each input
+// element is fetched once instead of once per tap (the per-row kernel above
+// reads a plane kH * kW times, from different blocks on different XCDs).
+// Per tap: the values go through a residue-transpose buffer (double-buffered,
+// one barrier a tap) and leave as res_chunk's 16-byte pieces.
+template <int CH>
+__global__ __launch_bounds__(256) void im2col_res_lds_kernel(
+    const float* __restrict__ x, int64_t xImg, float* __restrict__ dst, int64_t dstImg, int C,
+    int H, int W, int kH, int kW, int sY, int sX, int pH, int pW, int dY, int dX, int oW, int HWo,
+    int rows, int K4, int plane0) {
+  extern __shared__ float stage[];
+  __shared__ float tb[2][8 * RLD];
+  const int pa = plane0 + (int)blockIdx.y;  // (image, channel)
+  const int b = pa / C, c = pa - b * C;
+  const int tid = threadIdx.x, base = (int)blockIdx.x * CH;
+  const float* xc = x + b * xImg + (int64_t)c * H * W;
+  // the input rows of the chunk's output rows (none past the plane's end)
+  const int oy_lo = base / oW, oy_hi = min((base + CH - 1) / oW, (HWo - 1) / oW);
+  const int r_lo = max(oy_lo * sY - pH, 0), r_hi = min(oy_hi * sY - pH + (kH - 1) * dY, H - 1);
+  const int span = base < HWo && r_hi >= r_lo ? (r_hi - r_lo + 1) * W : 0;
+  {
+    const float* src = xc + (int64_t)r_lo * W;
+    int e = tid;
+    for (; e + 768 < span; e += 1024) {  // (four loads in flight)
+      const float v0 = src[e], v1 = src[e + 256], v2 = src[e + 512], v3 = src[e + 768];
+      stage[e] = v0;
+      stage[e + 256] = v1;
+      stage[e + 512] = v2;
+      stage[e + 768] = v3;
+    }
+    for (; e < span; e += 256) stage[e] = src[e];
+  }
+  // a thread's pixels base + tid + 256 j: window origin in the plane, and the
+  // origin's offset in the stage (oy0 = -1 << 20 marks a pixel past HWo)
+  constexpr int NJ = CH / 256;
+  int iy0[NJ], ix0[NJ];
+  {
+    const int p0 = base + tid, dy = 256 / oW, dx = 256 - dy * oW;
+    int oy = p0 / oW, ox = p0 - oy * oW;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (j > 0) {
+        ox += dx;
+        oy += dy;
+        if (ox >= oW) {
+          ox -= oW;
+          ++oy;
+        }
+      }
+      const bool in = p0 + 256 * j < HWo;
+      iy0[j] = in ? oy * sY - pH : -(1 << 20);
+      ix0[j] = ox * sX - pW;
+    }
+  }
+  __syncthreads();
+  constexpr int PIECES = CH / 32;  // 16-byte pieces per residue and tap
+  const int i0 = (int)blockIdx.x * (CH / 8);
+  const int taps = kH * kW;
+  float* drow0 = dst + b * dstImg + (int64_t)c * taps * 8 * K4;
+  for (int t = 0, kr = 0, kc = 0; t < taps; ++t) {
+    float* tt = tb[t & 1];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int pl = tid + 256 * j;
+      const int iy = iy0[j] + kr * dY, ix = ix0[j] + kc * dX;
+      const bool ok = (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+      tt[(pl & 7) * RLD + (pl >> 3)] = ok ? stage[(iy - r_lo) * W + ix] : 0.0f;
+    }
+    __syncthreads();
+    float* drow = drow0 + (int64_t)t * 8 * K4;
+#pragma unroll
+    for (int u = 0; u < (8 * PIECES + 255) / 256; ++u) {
+      const int idx = tid + 256 * u;
+      if (8 * PIECES % 256 == 0 || idx < 8 * PIECES) {
+        const int r = idx / PIECES, pc = idx - r * PIECES, kb = pc >> 3, a = pc & 7;
+        if (i0 + 32 * kb < K4) {
+          const int e = 32 * kb + (a >> 2) + 8 * (a & 3);
+          const float* tr = tt + r * RLD + e;
+          *reinterpret_cast<float4*>(drow + (int64_t)r * K4 + i0 + 4 * pc) =
+              make_float4(tr[0], tr[2], tr[4], tr[6]);
+        }
+      }
+    }
+    if (++kc == kW) {
+      kc = 0;
+      ++kr;
+    }
+  }
+  (void)rows;
 }
 
 // Rows of up to 1024 elements (K4 = 32 NB, NB <= 4; launched for the 13^2
@@ -636,6 +733,40 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       default: f(std::integral_constant<int, 2048>{}); break;
     }
   };
+  // the im2col rearrangement from LDS-staged input rows (im2col_res_lds_kernel):
+  // the chunk's input rows must fit the stage budget
+  const ConvGeom& gg = d.g;
+  const int chl = rowlen <= 256 ? 256 : chs;
+  const int64_t lds_rows = ((chl - 1) / gg.ow + 1) * gg.sY + (gg.kH - 1) * gg.dY + 1;
+  const int64_t lds_bytes = std::min<int64_t>(lds_rows, gg.H) * gg.W * 4;
+#ifdef TNS_RES_LDS_OFF  // (A/B side builds: the per-row kernels)
+  const bool lds_im2col = false;
+#else
+  const bool lds_im2col = !d.direct && lds_bytes <= kResStageBytes;
+#endif
+  auto lds_launch = [&]() -> hipError_t {
+    const int64_t planes = d.batch * gg.C;
+    const unsigned gxl = (unsigned)((rowlen + chl - 1) / chl);
+    for (int64_t p0 = 0; p0 < planes; p0 += 65535) {
+      const dim3 gr(gxl, (unsigned)std::min<int64_t>(planes - p0, 65535));
+      auto go = [&](auto cc) {
+        constexpr int CHv = decltype(cc)::value;
+        hipLaunchKernelGGL((im2col_res_lds_kernel<CHv>), gr, dim3(256), (size_t)lds_bytes, s, d.x,
+                           d.xStride, d.dB, npad * rowlen, (int)gg.C, (int)gg.H, (int)gg.W,
+                           (int)gg.kH, (int)gg.kW, (int)gg.sY, (int)gg.sX, (int)gg.padH,
+                           (int)gg.padW, (int)gg.dY, (int)gg.dX, (int)gg.ow, (int)d.K, (int)d.N,
+                           (int)K4, (int)p0);
+      };
+      switch (chl) {
+        case 256: go(std::integral_constant<int, 256>{}); break;
+        case 512: go(std::integral_constant<int, 512>{}); break;
+        case 1024: go(std::integral_constant<int, 1024>{}); break;
+        default: go(std::integral_constant<int, 2048>{}); break;
+      }
+      if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  };
   auto delta_rows = [&]() {
     return rows_launch(d.batch * d.M, [&](dim3 gr, int r0) {
       by_chunk([&](auto c) {
@@ -673,7 +804,9 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
         });
         e != hipSuccess)
       return e;
-    if (hipError_t e = short_launch(d.batch * d.N, [&](dim3 gr, int r0, int tot) {
+    if (lds_im2col) {
+      if (hipError_t e = lds_launch(); e != hipSuccess) return e;
+    } else if (hipError_t e = short_launch(d.batch * d.N, [&](dim3 gr, int r0, int tot) {
           by_nb([&](auto c) {
             constexpr int NB = decltype(c)::value;
             if (d.direct) {
@@ -694,7 +827,9 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
       return e;
   } else {
     if (hipError_t e = delta_rows(); e != hipSuccess) return e;
-    if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
+    if (lds_im2col) {
+      if (hipError_t e = lds_launch(); e != hipSuccess) return e;
+    } else if (hipError_t e = rows_launch(d.batch * d.N, [&](dim3 gr, int r0) {
           by_chunk([&](auto c) {
             constexpr int C = decltype(c)::value;
             if (d.direct) {
