@@ -320,12 +320,22 @@ const TileInfo kTiles[] = {
 };
 #undef TNS_CT
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
-// the conv_tile4.hip forms picked by default
+// the conv_tile4.hip forms picked by default: since round 5 their A-in-
+// registers twins (AR: no weight staging through LDS; TNS_CT4_NO_AR builds
+// the LDS-staged forms for A/B runs)
+#ifndef TNS_CT4_NO_AR
+constexpr int kT4Big = 25;       // (3) 128 x 176 x 64, stores after group 1, reads interleaved
+constexpr int kT4Small = 26;     // (8) 64 x 96 x 32, reads interleaved
+constexpr int kT4OneByOne = 27;  // (13) 64 x 32 x 32, 4 waves (1x1 layers)
+constexpr int kT4Uneven = 28;    // (18) 64 x 176 x 32, wave columns 6 + 5 fragments
+constexpr int kT4Narrow = 29;    // (21) 128 x 48 x 64, stores and reads interleaved
+#else
 constexpr int kT4Big = 3;    // 128 x 176 x 64, stores after group 1 and reads interleaved
 constexpr int kT4Small = 8;  // 64 x 96 x 32, reads interleaved
 constexpr int kT4OneByOne = 13;  // 64 x 32 x 32, 4 waves (1x1 layers)
 constexpr int kT4Uneven = 18;    // 64 x 176 x 32, wave columns 6 + 5 fragments
 constexpr int kT4Narrow = 21;    // 128 x 48 x 64, stores and reads interleaved
+#endif
 
 }  // namespace
 

@@ -80,8 +80,16 @@ struct Frag4 {
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
           int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
           bool BD_ = false, bool BW_ = false, bool AP_ = false, bool AT_ = false,
-          bool DX_ = false>
+          bool DX_ = false, bool AR_ = false>
 struct Geo4 {
+  // AR: A (the weights, [M][K]) never goes through LDS: lane (r16, q) of a
+  // wave loads, per 4-step group g, the float4 A[row][16g + 4q .. 16g + 4q + 3]
+  // of its strip row, and the four lanes (r16, 0..3) of a row transpose their
+  // four float4s by two v_permlane32_swap + two v_permlane16_swap, after which
+  // lane (r16, q) holds A[row][16g + 4i + q], i = 0..3 — exactly the slot the
+  // LDS image gave it.  No A staging stores, no A fragment reads, and the LDS
+  // holds B only (every wave reads its own 16 rows: nothing to share)
+  static constexpr bool AR = AR_;
   // DX: the conv backward's state.delta of a stride-1 layer as one implicit
   // transposed convolution — A = the weights tap-major, wt[t][f][c] (k-major,
   // TA), B = the delta planes gathered through the flipped window, k = t*F + f:
@@ -140,8 +148,8 @@ struct Geo4 {
   static constexpr int JB = NA < WN ? (J - NA * JA) / (WN - NA) : 0;  // ... of the others
   static constexpr int NG = BK / 16;            // 4-step groups per k-tile
   static constexpr int ROWS = BK / 4;           // slot rows per image (4g + q)
-  static constexpr int A_TILE = ROWS * BM * 4;  // floats
-  static constexpr int STAGE = ROWS * (BM + BN) * 4;
+  static constexpr int A_TILE = AR ? 0 : ROWS * BM * 4;  // floats
+  static constexpr int STAGE = ROWS * ((AR ? 0 : BM) + BN) * 4;
   static constexpr int B_TILE = ROWS * BN * 4;  // floats
   static constexpr int AU = BM * BK / 4 / NT;   // float4 A units per thread
   static constexpr int KI = BK / 4 / NW;        // B k-slots per thread
@@ -166,6 +174,7 @@ struct Geo4 {
   static_assert(!AP || (!IL && !ST && !TA && BM % 64 == 0 && ROWS * BM % (64 * NW) == 0),
                 "A DMA: tile-top issue, whole 64-slot pieces");
   static_assert(!DX || (TA && !AT && !BD && !BW && !AP), "DX: k-major weights, b32 gather");
+  static_assert(!AR || (!TA && !AT && !AP && !DX && !IL && !ST), "AR: [M][K] weights, block staging");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
   static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
@@ -418,8 +427,41 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       a_dst[u] = (4 * (kq4 >> 2)) * BM * 4 + m * 4 + (kq4 & 3);
     }
   }
-  float4 ra[AU];  // (unused with AP)
+  float4 ra[G::AR ? 1 : AU];  // (unused with AP / AR)
+  // (AR) this tile's A fragments (acur) and the next tile's loads (rar,
+  // transposed in place before the tile's last group)
+  floatx4 acur[G::AR ? NG : 1], rar[G::AR ? NG : 1];
+  const float* ar_src =
+      G::AR ? p.A + (m0 + (w % G::WM) * 16 + (lane & 15)) * p.lda + 4 * (lane >> 4) : nullptr;
+  auto load_ar = [&](int k0) {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) rar[g] = *reinterpret_cast<const floatx4*>(ar_src + k0 + 16 * g);
+  };
+  auto xpose_ar = [&]() {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      // lane (r16, q) holds A[row][16g + 4q + c]; afterwards component i
+      // holds A[row][16g + 4i + q] (a 4 x 4 transpose over the lane quarters)
+      auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, rar[g][0]),
+                                                __builtin_bit_cast(unsigned, rar[g][2]), false, false);
+      rar[g][0] = __builtin_bit_cast(float, (unsigned)r[0]);
+      rar[g][2] = __builtin_bit_cast(float, (unsigned)r[1]);
+      r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, rar[g][1]),
+                                           __builtin_bit_cast(unsigned, rar[g][3]), false, false);
+      rar[g][1] = __builtin_bit_cast(float, (unsigned)r[0]);
+      rar[g][3] = __builtin_bit_cast(float, (unsigned)r[1]);
+      r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, rar[g][0]),
+                                           __builtin_bit_cast(unsigned, rar[g][1]), false, false);
+      rar[g][0] = __builtin_bit_cast(float, (unsigned)r[0]);
+      rar[g][1] = __builtin_bit_cast(float, (unsigned)r[1]);
+      r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, rar[g][2]),
+                                           __builtin_bit_cast(unsigned, rar[g][3]), false, false);
+      rar[g][2] = __builtin_bit_cast(float, (unsigned)r[0]);
+      rar[g][3] = __builtin_bit_cast(float, (unsigned)r[1]);
+    }
+  };
   auto load_a = [&](int k0, float* as) {
+    if constexpr (G::AR) return;  // (load_ar, after the tile's stores)
     if constexpr (G::AP) {
 #pragma unroll
       for (int u = 0; u < G::ADM; ++u) {
@@ -453,7 +495,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   };
   auto store_a = [&](float* as) {
-    if constexpr (G::AP) return;  // (landed by the DMA)
+    if constexpr (G::AP || G::AR) return;  // (landed by the DMA / in registers)
 #if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 8)
     return;  // diagnostic build: no A stores (timing only)
 #endif
@@ -522,9 +564,14 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   };
   using Frag = Frag4<JW>;
-  auto frag = [&](int stg, int g, Frag& f) {
-    const float* ap = a_st(stg) + ((4 * g + q) * BM + wm * 16 + r16) * 4;
-    f.a = *reinterpret_cast<const floatx4*>(ap);
+  // (AR: f.a from acur, or from rar for the next tile's first group)
+  auto frag = [&](int stg, int g, Frag& f, bool next = false) {
+    if constexpr (G::AR) {
+      f.a = next ? rar[g] : acur[g];
+    } else {
+      const float* ap = a_st(stg) + ((4 * g + q) * BM + wm * 16 + r16) * 4;
+      f.a = *reinterpret_cast<const floatx4*>(ap);
+    }
     const float* bp = b_st(stg) + ((4 * g + q) * BN + coff * 16 + r16) * 4;
 #pragma unroll
     for (int j = 0; j < JW; ++j) f.b[j] = *reinterpret_cast<const floatx4*>(bp + 64 * j);
@@ -559,6 +606,18 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   const int nt = K / BK;
   Frag f0, f1;
   if (nt > 0) {
+    if constexpr (G::AR) {
+      load_ar(0);
+      gather_b(b_st(0));
+      store_b(b_st(0));
+      xpose_ar();
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acur[g] = rar[g];
+      __syncthreads();
+      frag(0, 0, f0);
+    }
+  }
+  if (nt > 0 && !G::AR) {
     load_a(0, a_st(0));
     gather_b(b_st(0));
     store_a(a_st(0));
@@ -579,6 +638,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
         load_a((t + 1) * BK, a_st(tx));
       } else {
         load_a((t + 1) * BK, a_st(tx));
+        // (AR, two groups a tile: the next tile's A at the top, a whole tile
+        // ahead of its transpose; deeper tiles load it after their stores)
+        if constexpr (G::AR && NG <= 2) load_ar((t + 1) * BK);
         gather_b(b_st(tx));
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
@@ -609,10 +671,12 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       // one scheduling region per group: the next group's fragment reads,
       // interleaved staging (LI / SI) and this group's MFMAs
       const bool reads = g + 1 < NG || more;
+      if constexpr (more && G::AR)
+        if (g == NG - 1) xpose_ar();  // (the next tile's A, loaded after the stores)
       if (g + 1 < NG)
         frag(tc, g + 1, fn);
       else if (more)
-        frag(tx, 0, fn);
+        frag(tx, 0, fn, true);
       if constexpr (more && G::IL) {
         if (g == 0) {
           advance();
@@ -659,8 +723,17 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           __builtin_amdgcn_sched_barrier(0);
           TNS_PH(2);
         }
+      if constexpr (more && G::AR && NG > 2)
+        if (g == G::SG) {
+          load_ar((t + 1) * BK);  // (registers free since the last tile's end)
+          __builtin_amdgcn_sched_barrier(0);
+        }
     }
     if constexpr (G::DX) flush();
+    if constexpr (more && G::AR) {
+#pragma unroll
+      for (int g = 0; g < NG; ++g) acur[g] = rar[g];
+    }
   };
   static_assert(NG % 2 == 0, "f0 holds group 0 at every tile start");
   for (int t = 0; t + 1 < nt; ++t) tile(t, std::true_type{});
@@ -815,6 +888,12 @@ struct TileInfo4 {
                   false, false, true>>,                                                       \
    "conv_tile4_at<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",ri" #RIv ",j" #JAv   \
    "x" #NAv ">"}
+#define TNS_CT4R(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                           \
+  {BMv, BNv, BKv,                                                                             \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, false, false,  \
+                  false, false, false, false, true>>,                                        \
+   "conv_tile4_ar<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv \
+   ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -844,6 +923,13 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
     TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
     TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
+    // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
+    // LDS) of the picked forms 3, 8, 13, 18, 21
+    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 25 (3)
+    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 26 (8)
+    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 27 (13)
+    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 28 (18)
+    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 29 (21)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
@@ -918,6 +1004,7 @@ constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4UD
 #undef TNS_CT4X
 #undef TNS_CT4T
+#undef TNS_CT4R
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
