@@ -29,7 +29,7 @@ ap.add_argument("--warm-ms", type=float, default=0.0, help="load before the stam
 a = ap.parse_args()
 hip = TNNHip(0)
 lib = load()
-stamps = torch.zeros(8 * 65536, dtype=torch.int32, device="cuda")
+stamps = torch.zeros(16 * 65536, dtype=torch.int32, device="cuda")
 fn = lib.tns_debug_ct4_stamps
 fn.argtypes = [ctypes.c_void_p]
 for layer in map(int, a.layer.split(",")):
@@ -61,8 +61,20 @@ for layer in map(int, a.layer.split(",")):
     run()
     torch.cuda.synchronize()
     fn(None)
-    st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 8).astype(np.float64)
+    st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 16).astype(np.float64)
     st = st[st[:, 7] > 0]
+    # block timeline (100 MHz realtime): entry relative to the first block's,
+    # prologue (entry -> loop start), loop, epilogue (loop end -> wave 0's
+    # stores done), end relative to the first entry
+    ent = st[:, 8] + st[:, 9] * 2.0 ** 32
+    ent = (ent - ent.min()) / 100.0  # us
+    pro = st[:, 10] / 100.0
+    loop_us = (st[:, 12] - st[:, 10]) / 100.0
+    epi = (st[:, 11] - st[:, 12]) / 100.0
+    end = ent + st[:, 11] / 100.0
+    q = lambda v: [round(float(np.percentile(v, x)), 2) for x in (0, 50, 100)]  # noqa: E731
+    timeline = {"entry_us_min_med_max": q(ent), "prologue_us": q(pro), "loop_us": q(loop_us),
+                "epilogue_us": q(epi), "end_us": q(end)}
     nt = st[:, 7].astype(np.uint64) & 0xff
     rt = (st[:, 7].astype(np.uint64) >> 8).astype(np.float64)  # 100 MHz ticks
     nt = nt.astype(np.float64)
@@ -72,4 +84,4 @@ for layer in map(int, a.layer.split(",")):
     clock_ghz = round(float(np.median(st[:, 6] / np.maximum(rt, 1) * 0.1)), 3)
     print(json.dumps({"layer": layer, "variant": a.variant, "blocks": int(len(st)),
                       "k_tiles": int(nt[0]), "layer_ms": round(layer_ms, 4), "cycles_per_tile_wave0": per_tile,
-                      "clock_ghz_median": clock_ghz}))
+                      "clock_ghz_median": clock_ghz, "timeline": timeline}))

@@ -4,6 +4,7 @@
 #   abfwd   — conv forward A/B: LIBS builds under ab/ (+ "main" = the tree)
 #   bwdab   — conv backward schedules (bwd_graph.py) for LIBS
 #   bench   — python bench.py (default flags) -> gpurun_out/bench.json
+#   stamps  — conv_tile4 phase stamps (ab/stamps build) for LAYERS
 #   trace   — rocprofv3 kernel trace of BENCH_ARGS -> gpurun_out/prof_trace
 set -u
 mkdir -p gpurun_out
@@ -29,6 +30,9 @@ for l in open('gpurun_out/abfwd.jsonl'):
         rc=$?; [ $rc -eq 0 ] || { echo "$L rc=$rc"; tail -5 gpurun_out/bwdab_$L.err; exit $rc; }
       done; done
       cat gpurun_out/bwdab.jsonl | cut -c1-400 ;;
+    stamps)
+      TNS_LIB=ab/stamps/libtensorium_hip.so timeout -k 10 300 python -u scripts/ct4_stamps.py --layer ${LAYERS:-11,28,45,10} --warm-ms 200 ${STAMP_ARGS:-} > gpurun_out/stamps.jsonl 2> gpurun_out/stamps.err
+      rc=$?; cat gpurun_out/stamps.jsonl; [ $rc -eq 0 ] || { tail -5 gpurun_out/stamps.err; exit $rc; } ;;
     bench)
       timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
       rc=$?; tail -c 3000 gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; } ;;

@@ -187,6 +187,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, NG = G::NG;
   constexpr int A_TILE = G::A_TILE, STAGE = G::STAGE, AU = G::AU, KI = G::KI;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+#ifdef TNS_CT4_STAMPS
+  const unsigned long long rt_entry = __builtin_amdgcn_s_memrealtime();
+#endif
   // stage st: A image and B image (AT: [B0][B1][A0][A1], else [A0 B0][A1 B1])
   auto a_st = [&](int st) -> float* {
     return G::AT ? smem + 2 * G::B_TILE + st * A_TILE : smem + st * STAGE;
@@ -442,22 +445,22 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     for (int g = 0; g < NG; ++g) {
       // lane (r16, q) holds A[row][16g + 4q + c]; afterwards component i
       // holds A[row][16g + 4i + q] (a 4 x 4 transpose over the lane quarters)
-      auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, rar[g][0]),
-                                                __builtin_bit_cast(unsigned, rar[g][2]), false, false);
-      rar[g][0] = __builtin_bit_cast(float, (unsigned)r[0]);
-      rar[g][2] = __builtin_bit_cast(float, (unsigned)r[1]);
-      r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, rar[g][1]),
-                                           __builtin_bit_cast(unsigned, rar[g][3]), false, false);
-      rar[g][1] = __builtin_bit_cast(float, (unsigned)r[0]);
-      rar[g][3] = __builtin_bit_cast(float, (unsigned)r[1]);
-      r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, rar[g][0]),
-                                           __builtin_bit_cast(unsigned, rar[g][1]), false, false);
-      rar[g][0] = __builtin_bit_cast(float, (unsigned)r[0]);
-      rar[g][1] = __builtin_bit_cast(float, (unsigned)r[1]);
-      r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, rar[g][2]),
-                                           __builtin_bit_cast(unsigned, rar[g][3]), false, false);
-      rar[g][2] = __builtin_bit_cast(float, (unsigned)r[0]);
-      rar[g][3] = __builtin_bit_cast(float, (unsigned)r[1]);
+      // (components through scalars: hipcc's __builtin_bit_cast of a vector
+      // element reads element 0)
+      float x0 = rar[g][0], x1 = rar[g][1], x2 = rar[g][2], x3 = rar[g][3];
+      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x0), __float_as_uint(x2), false, false);
+      x0 = __uint_as_float(r[0]);
+      x2 = __uint_as_float(r[1]);
+      r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x1), __float_as_uint(x3), false, false);
+      x1 = __uint_as_float(r[0]);
+      x3 = __uint_as_float(r[1]);
+      r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
+      x0 = __uint_as_float(r[0]);
+      x1 = __uint_as_float(r[1]);
+      r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2), __float_as_uint(x3), false, false);
+      x2 = __uint_as_float(r[0]);
+      x3 = __uint_as_float(r[1]);
+      rar[g] = floatx4{x0, x1, x2, x3};
     }
   };
   auto load_a = [&](int k0, float* as) {
@@ -742,10 +745,17 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
 #ifdef TNS_CT4_STAMPS
   TNS_PH(5);
   if (tid == 0 && p.stamps != nullptr && blockIdx.x < (1u << 16)) {
-    unsigned* st = p.stamps + 8 * blockIdx.x;
+    unsigned* st = p.stamps + 16 * blockIdx.x;
     for (int i = 0; i < 6; ++i) st[i] = (unsigned)ph[i];
     st[6] = (unsigned)(tl - tk0);
-    st[7] = (unsigned)nt | (unsigned)(__builtin_amdgcn_s_memrealtime() - rt0) << 8;
+    const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
+    st[7] = (unsigned)nt | (unsigned)(rt_loop - rt0) << 8;
+    // (realtime, 100 MHz: block entry, loop start, loop end; the epilogue's
+    // end in word 11, written below)
+    st[8] = (unsigned)rt_entry;
+    st[9] = (unsigned)(rt_entry >> 32);
+    st[10] = (unsigned)(rt0 - rt_entry);
+    st[12] = (unsigned)(rt_loop - rt_entry);
   }
 #endif
 #undef TNS_PH
@@ -818,6 +828,12 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       cp[e * p.ldc] = v;
     }
   }
+#ifdef TNS_CT4_STAMPS
+  if (tid == 0 && p.stamps != nullptr && blockIdx.x < (1u << 16)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's stores done)
+    p.stamps[16 * blockIdx.x + 11] = (unsigned)(__builtin_amdgcn_s_memrealtime() - rt_entry);
+  }
+#endif
   };
   if constexpr (G::NA == G::WN) {
     run(std::integral_constant<int, G::JA>{}, wn * G::JA);
@@ -1035,7 +1051,7 @@ int conv_tile4_bk(int v) { return v >= 0 && v < kNumTiles4 ? kTiles4[v].bk : 0; 
 
 #ifdef TNS_CT4_STAMPS
 // diagnostic build only (not in include/tns.h): per-block phase cycle sums
-// of wave 0 into dev_buf (8 words per block), or nothing when NULL
+// of wave 0 into dev_buf (16 words per block), or nothing when NULL
 extern "C" int tns_debug_ct4_stamps(unsigned* dev_buf) {
   g_ct4_stamps = dev_buf;
   return 0;

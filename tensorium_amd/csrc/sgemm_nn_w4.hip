@@ -88,6 +88,63 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   float* __restrict__ C = p.C + bz * p.strideC;
   const int64_t lda = p.lda, ldb = p.ldb, ldc = p.ldc;
 
+  // ---- LDS-DMA staging: wave w moves A row groups 8q..8q+7 (q = 8w + u,
+  // u < 8: 1 KB each) and B k-rows r = 8w + u of a tile ----------------------
+  // A: lane i -> row 8q + (i >> 3), LDS chunk slot i & 7 <- k-chunk
+  //    (i & 7) ^ ((row >> 1) & 7)
+  // B: lane i -> LDS chunk i of row r <- n-chunk (i + 8 (r & 1)) & 63
+  const int arow = lane >> 3;  // row within the group (group rows are 8-aligned)
+  const unsigned a_voff = (unsigned)(arow * lda * 4) + 16u * (unsigned)((lane & 7) ^ ((arow >> 1) & 7));
+  // ((8q + arow) >> 1) & 7 = (4q + (arow >> 1)) & 7: q even -> (arow >> 1),
+  // q odd -> (arow >> 1) ^ 4; odd groups use the second offset
+  const unsigned a_voff1 = (unsigned)(arow * lda * 4) +
+                           16u * (unsigned)((lane & 7) ^ (((arow >> 1) & 7) ^ 4));
+  const unsigned b_voff0 = 16u * (unsigned)lane;
+  const unsigned b_voff1 = 16u * (unsigned)((lane + 8) & 63);
+  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem;
+  const float* a_row0 = A + m0 * lda;  // + (8q) * lda + k0
+  const float* b_row0 = B + n0;        // + (k0 + r) * ldb
+  // DMA instruction u (0..15) of this wave for tile k0 into stage st
+  auto issue1 = [&](int u, int64_t k0, int st) {
+    const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
+    if (u < 8) {
+      const int q = 8 * wid + u;
+      dma16(a_row0 + (int64_t)(8 * q) * lda + k0, (u & 1) ? a_voff1 : a_voff,
+            sb + (unsigned)(q * 1024));
+    } else {
+      const int r = 8 * wid + (u - 8);
+      dma16(b_row0 + (k0 + r) * ldb, (u & 1) ? b_voff1 : b_voff0,
+            sb + (unsigned)(A_TILE * 4 + r * 1024));
+    }
+  };
+  auto issue = [&](int64_t k0, int st) {
+    const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = 8 * wid + u;
+      dma16(a_row0 + (int64_t)(8 * q) * lda + k0, (u & 1) ? a_voff1 : a_voff,
+            sb + (unsigned)(q * 1024));
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int r = 8 * wid + u;
+      dma16(b_row0 + (k0 + r) * ldb, (u & 1) ? b_voff1 : b_voff0,
+            sb + (unsigned)(A_TILE * 4 + r * 1024));
+    }
+  };
+
+  // the first two tiles' DMA goes out before the beta*C loads, so the two
+  // latencies overlap (the C loads are younger: waiting for them waits for
+  // the DMA too)
+  const int nt = (int)(p.K / BK);
+#ifdef TNS_W4_DMA_LATE  // (A/B side builds: round 4's order, DMA after the C loads)
+  constexpr bool kDmaFirst = false;
+#else
+  constexpr bool kDmaFirst = true;
+#endif
+  if (kDmaFirst && nt > 0) issue(0, 0);
+  if (kDmaFirst && nt > 1) issue(BK, 1);
+
   // ---- accumulators: 0, C or beta*C ---------------------------------------
   // C through a buffer resource over this block's rows: the lane's column in
   // a 32-bit VGPR offset, the row (wave-uniform: i, e) in the SGPR offset,
@@ -140,51 +197,8 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(acc[i][j]));
-
-  // ---- LDS-DMA staging: wave w moves A row groups 8q..8q+7 (q = 8w + u,
-  // u < 8: 1 KB each) and B k-rows r = 8w + u of a tile ----------------------
-  // A: lane i -> row 8q + (i >> 3), LDS chunk slot i & 7 <- k-chunk
-  //    (i & 7) ^ ((row >> 1) & 7)
-  // B: lane i -> LDS chunk i of row r <- n-chunk (i + 8 (r & 1)) & 63
-  const int arow = lane >> 3;  // row within the group (group rows are 8-aligned)
-  const unsigned a_voff = (unsigned)(arow * lda * 4) + 16u * (unsigned)((lane & 7) ^ ((arow >> 1) & 7));
-  // ((8q + arow) >> 1) & 7 = (4q + (arow >> 1)) & 7: q even -> (arow >> 1),
-  // q odd -> (arow >> 1) ^ 4; odd groups use the second offset
-  const unsigned a_voff1 = (unsigned)(arow * lda * 4) +
-                           16u * (unsigned)((lane & 7) ^ (((arow >> 1) & 7) ^ 4));
-  const unsigned b_voff0 = 16u * (unsigned)lane;
-  const unsigned b_voff1 = 16u * (unsigned)((lane + 8) & 63);
-  const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem;
-  const float* a_row0 = A + m0 * lda;  // + (8q) * lda + k0
-  const float* b_row0 = B + n0;        // + (k0 + r) * ldb
-  // DMA instruction u (0..15) of this wave for tile k0 into stage st
-  auto issue1 = [&](int u, int64_t k0, int st) {
-    const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
-    if (u < 8) {
-      const int q = 8 * wid + u;
-      dma16(a_row0 + (int64_t)(8 * q) * lda + k0, (u & 1) ? a_voff1 : a_voff,
-            sb + (unsigned)(q * 1024));
-    } else {
-      const int r = 8 * wid + (u - 8);
-      dma16(b_row0 + (k0 + r) * ldb, (u & 1) ? b_voff1 : b_voff0,
-            sb + (unsigned)(A_TILE * 4 + r * 1024));
-    }
-  };
-  auto issue = [&](int64_t k0, int st) {
-    const unsigned sb = lds0 + (unsigned)(st * STAGE * 4);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int q = 8 * wid + u;
-      dma16(a_row0 + (int64_t)(8 * q) * lda + k0, (u & 1) ? a_voff1 : a_voff,
-            sb + (unsigned)(q * 1024));
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = 8 * wid + u;
-      dma16(b_row0 + (k0 + r) * ldb, (u & 1) ? b_voff1 : b_voff0,
-            sb + (unsigned)(A_TILE * 4 + r * 1024));
-    }
-  };
+  if (!kDmaFirst && nt > 0) issue(0, 0);
+  if (!kDmaFirst && nt > 1) issue(BK, 1);
 
   // ---- fragments: step s (k = 2s + h) --------------------------------------
   // A tile i: row wm*128 + 32 i + lc, chunk (k >> 2) ^ swz, swz = (lc >> 1) & 7
@@ -229,7 +243,6 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
     }
   };
 
-  const int nt = (int)(p.K / BK);
   float a0[4], b0[4], a1[4], b1[4];
   {
     // the barrier that publishes tile t+1 sits before step 15 of tile
@@ -237,10 +250,9 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
     // DMA of tile t+2 (into tile t's stage, whose reads all completed before
     // the barrier) goes out a whole tile ahead of its use
     if (nt > 0) {
-      issue(0, 0);
       if (nt > 1) {
-        issue(BK, 1);
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // tile 0's 16 DMAs of this wave
+        // tile 0's 16 DMAs of this wave (with beta*C loaded: all of them)
+        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
