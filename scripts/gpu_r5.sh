@@ -23,6 +23,20 @@ for S in ${STEPS}; do
 import json
 for l in open('gpurun_out/abfwd.jsonl'):
     r=json.loads(l); print(r['tag'], r['yolo_ms'], r['yolo_tflops'])" ;;
+    abgemm)
+      for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do
+        TNS_LIB=$(lib_of $L) timeout -k 10 300 python -u scripts/quick_perf.py --tag $L >> gpurun_out/abgemm.jsonl 2> gpurun_out/abgemm_$L.err
+        rc=$?; [ $rc -eq 0 ] || { echo "$L rc=$rc"; tail -5 gpurun_out/abgemm_$L.err; exit $rc; }
+      done; done
+      python3 -c "
+import json
+for l in open('gpurun_out/abgemm.jsonl'):
+    r=json.loads(l); print(r['tag'], r['sgemm4096_ms'], r['batched_tflops'], r['yolo_ms'])" ;;
+    batched)
+      for L in ${LIBS:-main}; do
+        TNS_LIB=$(lib_of $L) timeout -k 10 300 python -u scripts/batched_probe.py > gpurun_out/batched_$L.json 2> gpurun_out/batched_$L.err
+        rc=$?; echo "$L $(cat gpurun_out/batched_$L.json)"; [ $rc -eq 0 ] || { tail -5 gpurun_out/batched_$L.err; exit $rc; }
+      done ;;
     bwdab)
       for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do
         echo "{\"tag\": \"$L\"}" >> gpurun_out/bwdab.jsonl

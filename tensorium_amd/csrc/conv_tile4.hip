@@ -80,8 +80,14 @@ struct Frag4 {
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
           int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
           bool BD_ = false, bool BW_ = false, bool AP_ = false, bool AT_ = false,
-          bool DX_ = false, bool AR_ = false>
+          bool DX_ = false, bool AR_ = false, bool PF_ = false>
 struct Geo4 {
+  // PF: the register-staged operands of tile t+2 are loaded at the top of
+  // tile t (two register sets, the tile pairs unrolled), so a gather has a
+  // whole tile to land before its stores (the 2-group 26^2 / 13^2 forms
+  // otherwise wait at the barrier for their loads: block stamps,
+  // profiles/r05_conv_fwd_stamps.json)
+  static constexpr bool PF = PF_;
   // AR: A (the weights, [M][K]) never goes through LDS: lane (r16, q) of a
   // wave loads, per 4-step group g, the float4 A[row][16g + 4q .. 16g + 4q + 3]
   // of its strip row, and the four lanes (r16, 0..3) of a row transpose their
@@ -175,6 +181,7 @@ struct Geo4 {
                 "A DMA: tile-top issue, whole 64-slot pieces");
   static_assert(!DX || (TA && !AT && !BD && !BW && !AP), "DX: k-major weights, b32 gather");
   static_assert(!AR || (!TA && !AT && !AP && !DX && !IL && !ST), "AR: [M][K] weights, block staging");
+  static_assert(!PF || (!AR && !AT && !AP && !BD && !BW && !IL && !ST), "PF: register staging");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
   static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
@@ -302,10 +309,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       }
     }
   };
-  float rb[KI][J];  // (unused with BD / BW)
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  float rbs[G::PF ? 2 : 1][KI][J];  // (unused with BD / BW; PF: one set a tile parity)
   floatx4 rw[G::BW ? KI : 1][G::BW ? G::CH : 1];  // (BW)
   const unsigned lds0 = (unsigned)(uintptr_t)(__attribute__((address_space(3))) float*)smem;
-  auto gather_b = [&](const float* bs) {
+  auto gather_b = [&](const float* bs, auto SET) {
+    auto& rb = rbs[decltype(SET)::value];
     if constexpr (G::BW) {
 #pragma unroll
       for (int ii = 0; ii < KI; ++ii)
@@ -368,7 +378,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   int b_dst[KI];
 #pragma unroll
   for (int ii = 0; ii < KI; ++ii) b_dst[ii] = (w * KI + ii) * BN * 4 + r16 * 4 + q;
-  auto store_b = [&](float* bs) {
+  auto store_b = [&](float* bs, auto SET) {
+    auto& rb = rbs[decltype(SET)::value];
 #if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 2)
     return;  // diagnostic build: no B stores (timing only)
 #endif
@@ -430,7 +441,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       a_dst[u] = (4 * (kq4 >> 2)) * BM * 4 + m * 4 + (kq4 & 3);
     }
   }
-  float4 ra[G::AR ? 1 : AU];  // (unused with AP / AR)
+  float4 ras[G::PF ? 2 : 1][G::AR ? 1 : AU];  // (unused with AP / AR)
   // (AR) this tile's A fragments (acur) and the next tile's loads (rar,
   // transposed in place before the tile's last group)
   floatx4 acur[G::AR ? NG : 1], rar[G::AR ? NG : 1];
@@ -463,7 +474,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       rar[g] = floatx4{x0, x1, x2, x3};
     }
   };
-  auto load_a = [&](int k0, float* as) {
+  auto load_a = [&](int k0, float* as, auto SET) {
+    auto& ra = ras[decltype(SET)::value];
     if constexpr (G::AR) return;  // (load_ar, after the tile's stores)
     if constexpr (G::AP) {
 #pragma unroll
@@ -497,7 +509,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       }
     }
   };
-  auto store_a = [&](float* as) {
+  auto store_a = [&](float* as, auto SET) {
+    auto& ra = ras[decltype(SET)::value];
     if constexpr (G::AP || G::AR) return;  // (landed by the DMA / in registers)
 #if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 8)
     return;  // diagnostic build: no A stores (timing only)
@@ -611,8 +624,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   if (nt > 0) {
     if constexpr (G::AR) {
       load_ar(0);
-      gather_b(b_st(0));
-      store_b(b_st(0));
+      gather_b(b_st(0), S0{});
+      store_b(b_st(0), S0{});
       xpose_ar();
 #pragma unroll
       for (int g = 0; g < NG; ++g) acur[g] = rar[g];
@@ -621,30 +634,49 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   }
   if (nt > 0 && !G::AR) {
-    load_a(0, a_st(0));
-    gather_b(b_st(0));
-    store_a(a_st(0));
-    store_b(b_st(0));
+    load_a(0, a_st(0), S0{});
+    gather_b(b_st(0), S0{});
+    if constexpr (G::PF) {  // (tile 1 into set 1, in flight past the barrier)
+      if (nt > 1) {
+        advance();
+        load_a(BK, nullptr, S1{});
+        gather_b(nullptr, S1{});
+      }
+    }
+    store_a(a_st(0), S0{});
+    store_b(b_st(0), S0{});
     if constexpr (G::BD || G::AP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (G::AT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (asm stores)
     __syncthreads();
     frag(0, 0, f0);
   }
-  auto tile = [&](int t, auto MORE) {
+  auto tile = [&](int t, auto MORE, auto PAR) {
     constexpr bool more = decltype(MORE)::value;
+    // (PF) tile t's set parity: the loads of tile t+2 go into set PAR at
+    // the top, the stores of tile t+1 come from set PAR ^ 1
+    constexpr int par = decltype(PAR)::value;
+    using SL = std::integral_constant<int, G::PF ? par : 0>;
+    using SS = std::integral_constant<int, G::PF ? par ^ 1 : 0>;
     const int tc = t & 1, tx = (t + 1) & 1;
     TNS_PH(5);
-    if constexpr (more && !G::IL && !G::ST) {
+    if constexpr (more && G::PF) {
+      if (t + 2 < nt) {
+        advance();
+        load_a((t + 2) * BK, nullptr, SL{});
+        gather_b(nullptr, SL{});
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
+    } else if constexpr (more && !G::IL && !G::ST) {
       advance();
       if constexpr (G::BD) {
-        gather_b(b_st(tx));
-        load_a((t + 1) * BK, a_st(tx));
+        gather_b(b_st(tx), S0{});
+        load_a((t + 1) * BK, a_st(tx), S0{});
       } else {
-        load_a((t + 1) * BK, a_st(tx));
+        load_a((t + 1) * BK, a_st(tx), S0{});
         // (AR, two groups a tile: the next tile's A at the top, a whole tile
         // ahead of its transpose; deeper tiles load it after their stores)
         if constexpr (G::AR && NG <= 2) load_ar((t + 1) * BK);
-        gather_b(b_st(tx));
+        gather_b(b_st(tx), S0{});
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
     }
@@ -667,8 +699,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (more && G::ST)
         if (g < 2 && half == g) {
           advance();
-          load_a((t + 1) * BK, a_st(tx));
-          gather_b(b_st(tx));
+          load_a((t + 1) * BK, a_st(tx), S0{});
+          gather_b(b_st(tx), S0{});
           __builtin_amdgcn_sched_barrier(0);
         }
       // one scheduling region per group: the next group's fragment reads,
@@ -683,14 +715,14 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (more && G::IL) {
         if (g == 0) {
           advance();
-          load_a((t + 1) * BK, a_st(tx));
-          gather_b(b_st(tx));
+          load_a((t + 1) * BK, a_st(tx), S0{});
+          gather_b(b_st(tx), S0{});
         }
       }
       if constexpr (more && G::SI) {
         if (g == G::SG) {
-          store_a(a_st(tx));
-          store_b(b_st(tx));
+          store_a(a_st(tx), SS{});
+          store_b(b_st(tx), SS{});
         }
       }
       mma(fc);
@@ -714,15 +746,15 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (more && G::ST)
         if (g >= G::SG && g <= G::SG + 1 && g == G::SG + half) {
-          store_a(a_st(tx));
-          store_b(b_st(tx));
+          store_a(a_st(tx), S0{});
+          store_b(b_st(tx), S0{});
           __builtin_amdgcn_sched_barrier(0);
         }
       if constexpr (more && !G::SI && !G::ST)
         if (g == G::SG) {
           TNS_PH(1);
-          store_a(a_st(tx));
-          store_b(b_st(tx));
+          store_a(a_st(tx), SS{});
+          store_b(b_st(tx), SS{});
           __builtin_amdgcn_sched_barrier(0);
           TNS_PH(2);
         }
@@ -739,8 +771,22 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   };
   static_assert(NG % 2 == 0, "f0 holds group 0 at every tile start");
-  for (int t = 0; t + 1 < nt; ++t) tile(t, std::true_type{});
-  if (nt > 0) tile(nt - 1, std::false_type{});
+  if constexpr (G::PF) {  // (tile pairs: the set parity a compile-time constant)
+    int t = 0;
+    for (; t + 2 < nt; t += 2) {
+      tile(t, std::true_type{}, S0{});
+      tile(t + 1, std::true_type{}, S1{});
+    }
+    if (t + 1 < nt) {
+      tile(t, std::true_type{}, S0{});
+      tile(t + 1, std::false_type{}, S1{});
+    } else if (t < nt) {
+      tile(t, std::false_type{}, S0{});
+    }
+  } else {
+    for (int t = 0; t + 1 < nt; ++t) tile(t, std::true_type{}, S0{});
+    if (nt > 0) tile(nt - 1, std::false_type{}, S0{});
+  }
 
 #ifdef TNS_CT4_STAMPS
   TNS_PH(5);
@@ -910,6 +956,12 @@ struct TileInfo4 {
                   false, false, false, false, true>>,                                        \
    "conv_tile4_ar<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv \
    ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4P(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                           \
+  {BMv, BNv, BKv,                                                                             \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, false, false,  \
+                  false, false, false, false, false, true>>,                                 \
+   "conv_tile4_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv \
+   ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -939,36 +991,47 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
     TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
     TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
-    // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
-    // LDS) of the picked forms 3, 8, 13, 18, 21
-    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 25 (3)
-    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 26 (8)
-    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 27 (13)
-    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 28 (18)
-    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 29 (21)
+    // loads two tiles ahead (PF: two register sets) of the picked forms
+    TNS_CT4P(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 25 (18)
+    TNS_CT4P(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 26 (21)
+    TNS_CT4P(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 27 (13)
+    TNS_CT4P(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 28 (8)
+    TNS_CT4P(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 29 (3)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
+    // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
+    // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
+    // class but the stride-2 104^2 / 208^2 ones (YOLOv3 batch 8, same box,
+    // interleaved: 6.18-6.24 ms a batch against 5.94-6.03; 26^2 +4.9 %,
+    // 13^2 +8 %, 1x1 +4..11 %): every wave loads its own 16 rows, and the
+    // loads of a 64-deep tile go out after the stores, too late for the
+    // tile's last group (block stamps: profiles/r05_conv_fwd_stamps.json)
+    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 30 (3)
+    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 31 (8)
+    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 32 (13)
+    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 33 (18)
+    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 34 (21)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 25 (3, BD)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 26 (3, BW)
-    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 27 (18, BW)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 35 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 36 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 37 (18, BW)
     // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
-    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 28 (3)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 38 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
     // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
     // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 29 (1)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 30
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 31 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 32 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 33 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 34 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 35 (11)
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 39 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 40
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 41 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 42 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 43 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 44 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 45 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
@@ -1021,6 +1084,7 @@ constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4X
 #undef TNS_CT4T
 #undef TNS_CT4R
+#undef TNS_CT4P
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
