@@ -47,6 +47,24 @@ for l in open('gpurun_out/abgemm.jsonl'):
     stamps)
       TNS_LIB=ab/stamps/libtensorium_hip.so timeout -k 10 300 python -u scripts/ct4_stamps.py --layer ${LAYERS:-11,28,45,10} --warm-ms 200 ${STAMP_ARGS:-} > gpurun_out/stamps.jsonl 2> gpurun_out/stamps.err
       rc=$?; cat gpurun_out/stamps.jsonl; [ $rc -eq 0 ] || { tail -5 gpurun_out/stamps.err; exit $rc; } ;;
+    fwdsweep)
+      # VARIANTS: "<layers>:<v1>,<v2>,..." groups separated by spaces (v as
+      # TNS_OPT_CONV_VARIANT, -1 the pick); two passes, interleaved
+      for r in 1 2; do for grp in ${VARIANTS}; do
+        L=${grp%%:*}; VS=${grp#*:}
+        for v in ${VS//,/ }; do
+          echo -n "{\"round\": $r, \"variant\": $v, \"res\": " >> gpurun_out/fwdsweep.jsonl
+          timeout -k 10 120 python -u scripts/conv_fwd_layers.py --layers $L --variant $v --warm-ms 100 --reps 20 >> gpurun_out/fwdsweep.jsonl 2> gpurun_out/fwdsweep.err
+          rc=$?; echo "}" >> gpurun_out/fwdsweep.jsonl; [ $rc -eq 0 ] || { tail -5 gpurun_out/fwdsweep.err; exit $rc; }
+        done
+      done; done
+      python3 -c "
+import json,collections
+d=collections.defaultdict(list)
+for l in open('gpurun_out/fwdsweep.jsonl'):
+    r=json.loads(l.replace('\n',''))
+    for x in r['res']['layers']: d[(x['layer'], r['variant'])].append(x['ms'])
+for k in sorted(d): print(k, d[k])" ;;
     bench)
       timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
       rc=$?; tail -c 3000 gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; } ;;

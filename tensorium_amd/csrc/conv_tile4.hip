@@ -168,7 +168,7 @@ struct Geo4 {
   static_assert(BM == 16 * WM, "one 16-row strip per wave");
   static_assert(BM % 16 == 0 && BN % 16 == 0, "b128 slot rows: 64-dword multiples");
   static_assert(BK % 16 == 0 && SG <= NG - 2, "stores precede the barrier");
-  static_assert(!(IL && SI) || SG >= 1, "interleaved stores need a group after the loads");
+  static_assert(!(IL && SI) || SG >= 1 || PF_, "interleaved stores need a group after the loads");
   static_assert(!ST || (!IL && !SI && SG + 1 <= NG - 2 && NW % 2 == 0), "staggered staging");
   static_assert(AU >= 1 && BM * BK / 4 % NT == 0 && KI >= 1 && BK / 4 % NW == 0, "geometry");
   static_assert(NA * JA + (WN - NA) * JB == J && NA >= 1 && NA <= WN, "wave column split");
@@ -181,7 +181,7 @@ struct Geo4 {
                 "A DMA: tile-top issue, whole 64-slot pieces");
   static_assert(!DX || (TA && !AT && !BD && !BW && !AP), "DX: k-major weights, b32 gather");
   static_assert(!AR || (!TA && !AT && !AP && !DX && !IL && !ST), "AR: [M][K] weights, block staging");
-  static_assert(!PF || (!AR && !AT && !AP && !BD && !BW && !IL && !ST), "PF: register staging");
+  static_assert(!PF || (!AR && !AT && !AP && !BD && !BW && !ST), "PF: register staging");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
   static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
@@ -659,14 +659,14 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     using SS = std::integral_constant<int, G::PF ? par ^ 1 : 0>;
     const int tc = t & 1, tx = (t + 1) & 1;
     TNS_PH(5);
-    if constexpr (more && G::PF) {
-      if (t + 2 < nt) {
-        advance();
-        load_a((t + 2) * BK, nullptr, SL{});
-        gather_b(nullptr, SL{});
-      }
+    if constexpr (more && G::PF && !G::IL) {
+      // (unconditional: past the last tile the weight rows' k is clamped
+      // and the gather's offsets run past the images' range — read, unused)
+      advance();
+      load_a(min((t + 2) * BK, K - BK), nullptr, SL{});
+      gather_b(nullptr, SL{});
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
-    } else if constexpr (more && !G::IL && !G::ST) {
+    } else if constexpr (more && !G::IL && !G::ST && !G::PF) {
       advance();
       if constexpr (G::BD) {
         gather_b(b_st(tx), S0{});
@@ -715,8 +715,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (more && G::IL) {
         if (g == 0) {
           advance();
-          load_a((t + 1) * BK, a_st(tx), S0{});
-          gather_b(b_st(tx), S0{});
+          if constexpr (G::PF) {  // (tile t+2 into this tile's set, as above)
+            load_a(min((t + 2) * BK, K - BK), nullptr, SL{});
+            gather_b(nullptr, SL{});
+          } else {
+            load_a((t + 1) * BK, a_st(tx), S0{});
+            gather_b(b_st(tx), S0{});
+          }
         }
       }
       if constexpr (more && G::SI) {
@@ -962,6 +967,12 @@ struct TileInfo4 {
                   false, false, false, false, false, true>>,                                 \
    "conv_tile4_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv \
    ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4PI(BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, JAv, NAv)                     \
+  {BMv, BNv, BKv,                                                                             \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, false, JAv, NAv, false, false, \
+                  false, false, false, false, false, true>>,                                 \
+   "conv_tile4_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si" #SIv  \
+   ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -997,6 +1008,14 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4P(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 27 (13)
     TNS_CT4P(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 28 (8)
     TNS_CT4P(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 29 (3)
+    // ... with the loads of tile t+2 (IL: 2 VALU per MFMA) and / or the
+    // stores of tile t+1 interleaved with group 0's MFMAs
+    TNS_CT4PI(64, 176, 4, 2, 32, 0, 2, false, 3, 6, 1),  // 30 (18, IL)
+    TNS_CT4PI(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 31 (18, SI)
+    TNS_CT4PI(64, 176, 4, 2, 32, 0, 2, true, 3, 6, 1),   // 32 (18, IL + SI)
+    TNS_CT4PI(64, 176, 4, 2, 64, 1, 2, true, 2, 6, 1),   // 33 (17, IL + SI)
+    TNS_CT4PI(128, 48, 8, 1, 64, 1, 2, true, 2, 0, 0),   // 34 (21, IL + SI)
+    TNS_CT4PI(128, 48, 8, 1, 64, 0, 2, true, 2, 0, 0),   // 35 (21, IL + SI in group 0)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
     // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
@@ -1005,33 +1024,33 @@ const TileInfo4 kTiles4[] = {
     // 13^2 +8 %, 1x1 +4..11 %): every wave loads its own 16 rows, and the
     // loads of a 64-deep tile go out after the stores, too late for the
     // tile's last group (block stamps: profiles/r05_conv_fwd_stamps.json)
-    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 30 (3)
-    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 31 (8)
-    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 32 (13)
-    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 33 (18)
-    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 34 (21)
+    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 36 (3)
+    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 37 (8)
+    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 38 (13)
+    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 39 (18)
+    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 40 (21)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 35 (3, BD)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 36 (3, BW)
-    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 37 (18, BW)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 41 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 42 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 43 (18, BW)
     // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
-    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 38 (3)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 44 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
     // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
     // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 39 (1)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 40
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 41 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 42 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 43 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 44 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 45 (11)
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 45 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 46
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 47 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 48 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 49 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 50 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 51 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
@@ -1085,6 +1104,7 @@ constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4T
 #undef TNS_CT4R
 #undef TNS_CT4P
+#undef TNS_CT4PI
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
