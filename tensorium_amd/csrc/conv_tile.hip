@@ -323,6 +323,7 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 // the conv_tile4.hip forms picked by default (TNS_CT4_AR: their A-in-
 // registers twins, diagnostics builds only — measured slower, conv_tile4.hip)
 #ifdef TNS_CT4_AR
+constexpr int kT4UnevenS2 = 39;
 constexpr int kT4Big = 36;       // (3) 128 x 176 x 64, stores after group 1, reads interleaved
 constexpr int kT4Small = 37;     // (8) 64 x 96 x 32, reads interleaved
 constexpr int kT4OneByOne = 38;  // (13) 64 x 32 x 32, 4 waves (1x1 layers)
@@ -335,9 +336,16 @@ constexpr int kT4Narrow = 40;    // (21) 128 x 48 x 64, stores and reads interle
 constexpr int kT4Big = 3;
 constexpr int kT4Small = 8;
 constexpr int kT4OneByOne = 13;
-constexpr int kT4Uneven = 25;    // (18) 64 x 176 x 32, wave columns 6 + 5 fragments, PF
-constexpr int kT4Narrow = 21;    // 128 x 48 x 64 (PF: level, 13^2 +1.2 %)
+// 64 x 176 x 32, wave columns 6 + 5 fragments, PF: stride 1 with the stores
+// interleaved into group 0 (SI), stride 2 with the loads (IL) — warm clock,
+// batch 8 (scripts/conv_fwd_layers.py, profiles/r05_conv_fwd_sweep.json):
+// 26^2 0.1348 -> 0.1268 ms (PF alone 0.1296), 52^2 -> 26^2 stride 2 0.1431
+// -> 0.1320 (PF alone 0.1426)
+constexpr int kT4Uneven = 31;
+constexpr int kT4UnevenS2 = 30;
+constexpr int kT4Narrow = 21;    // 128 x 48 x 64 (every PF form level or slower on 13^2)
 #else
+constexpr int kT4UnevenS2 = 18;
 constexpr int kT4Big = 3;    // 128 x 176 x 64, stores after group 1 and reads interleaved
 constexpr int kT4Small = 8;  // 64 x 96 x 32, reads interleaved
 constexpr int kT4OneByOne = 13;  // 64 x 32 x 32, 4 waves (1x1 layers)
@@ -383,7 +391,7 @@ int conv_tile_pick(const GemmArgs& a, int ks) {
   // 512 filters (the 26^2 layers and the 52^2 -> 26^2 stride-2 one): 64 x 176
   // with wave columns of 6 + 5 fragments, 8 x 31 blocks (warm clock 0.137 ->
   // 0.128 ms, stride 2 0.151 -> 0.134)
-  if (a.M == 512) return kNumTiles + kT4Uneven;
+  if (a.M == 512) return kNumTiles + (a.conv_sY == 1 ? kT4Uneven : kT4UnevenS2);
   // 1024 filters (13^2 planes, N = 1352): 8 x 29 blocks of 128 x 48 (warm clock
   // 0.149 -> 0.139 ms, the 26^2 -> 13^2 stride-2 layer 0.157 -> 0.140)
   if (a.M == 1024 && a.K % conv_tile4_bk(kT4Narrow) == 0) return kNumTiles + kT4Narrow;

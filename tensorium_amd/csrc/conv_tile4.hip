@@ -1080,6 +1080,12 @@ constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
                   false, false, false, true>>,                                             \
    "conv_tile4_dx<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv         \
    ",ri" #RIv ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4DXP(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                         \
+  {BMv, BNv, BKv,                                                                          \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, true, false,  \
+                  false, false, false, true, false, true>>,                                \
+   "conv_tile4_dx_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv      \
+   ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4DX[] = {
     TNS_CT4DX(64, 176, 4, 2, 32, 0, false, 3, 6, 1),   // 0: >= 52^2 planes
     TNS_CT4DX(64, 96, 4, 1, 32, 0, false, 3, 0, 0),    // 1: 26^2
@@ -1088,6 +1094,11 @@ const TileInfo4 kTiles4DX[] = {
     TNS_CT4DX(64, 64, 4, 2, 32, 0, false, 3, 0, 0),    // 4
     TNS_CT4DX(128, 48, 8, 1, 64, 1, true, 2, 0, 0),    // 5
     TNS_CT4DX(32, 176, 2, 4, 64, 1, true, 2, 3, 3),    // 6: 32-channel planes (208^2)
+    // the same with the operands of tile t+2 loaded at the top of tile t (PF)
+    TNS_CT4DXP(64, 176, 4, 2, 32, 0, false, 3, 6, 1),  // 7 (0)
+    TNS_CT4DXP(64, 64, 4, 2, 32, 0, false, 3, 0, 0),   // 8 (4)
+    TNS_CT4DXP(32, 176, 2, 4, 64, 1, true, 2, 3, 3),   // 9 (6)
+    TNS_CT4DXP(64, 48, 4, 1, 32, 0, false, 3, 0, 0),   // 10 (2)
     // (128 x 176: the running sums take it past 256 VGPRs — spills; not built.
     // Eight-wave 64 x 96 / 32 x 96 forms for the 26^2 / 13^2 row counts
     // measured no better than these: 26^2 0.369 / 0.378 ms a call against
@@ -1095,6 +1106,7 @@ const TileInfo4 kTiles4DX[] = {
 };
 constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4DX
+#undef TNS_CT4DXP
 #undef TNS_CT4
 #undef TNS_CT4U
 #undef TNS_CT4D
