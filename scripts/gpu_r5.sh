@@ -65,6 +65,9 @@ for l in open('gpurun_out/fwdsweep.jsonl'):
     r=json.loads(l.replace('\n',''))
     for x in r['res']['layers']: d[(x['layer'], r['variant'])].append(x['ms'])
 for k in sorted(d): print(k, d[k])" ;;
+    bwdsweep)
+      timeout -k 10 900 python -u scripts/bwd_sweep.py --layers ${BLAYERS:-1,3,4,6,11} --what ${BWHAT:-dx} > gpurun_out/bwdsweep.json 2> gpurun_out/bwdsweep.err
+      rc=$?; tail -c 4000 gpurun_out/bwdsweep.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bwdsweep.err; exit $rc; } ;;
     bench)
       timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
       rc=$?; tail -c 3000 gpurun_out/bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench.err; exit $rc; } ;;

@@ -1016,6 +1016,11 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4PI(64, 176, 4, 2, 64, 1, 2, true, 2, 6, 1),   // 33 (17, IL + SI)
     TNS_CT4PI(128, 48, 8, 1, 64, 1, 2, true, 2, 0, 0),   // 34 (21, IL + SI)
     TNS_CT4PI(128, 48, 8, 1, 64, 0, 2, true, 2, 0, 0),   // 35 (21, IL + SI in group 0)
+    // 128 x 176 x 32 (the 52^2 / 104^2 tile in 2-group k-tiles: one
+    // register set fits where the 64-deep PF form spills)
+    TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, false, 3, 0, 0), // 36 (0, PF)
+    TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, true, 3, 0, 0),  // 37 (0, PF + SI)
+    TNS_CT4PI(128, 176, 8, 1, 32, 0, 2, false, 3, 0, 0), // 38 (0, PF + IL)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
     // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
@@ -1024,33 +1029,33 @@ const TileInfo4 kTiles4[] = {
     // 13^2 +8 %, 1x1 +4..11 %): every wave loads its own 16 rows, and the
     // loads of a 64-deep tile go out after the stores, too late for the
     // tile's last group (block stamps: profiles/r05_conv_fwd_stamps.json)
-    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 36 (3)
-    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 37 (8)
-    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 38 (13)
-    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 39 (18)
-    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 40 (21)
+    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 39 (3)
+    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 40 (8)
+    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 41 (13)
+    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 42 (18)
+    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 43 (21)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 41 (3, BD)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 42 (3, BW)
-    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 43 (18, BW)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 44 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 45 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 46 (18, BW)
     // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
-    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 44 (3)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 47 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
     // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
     // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 45 (1)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 46
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 47 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 48 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 49 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 50 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 51 (11)
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 48 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 49
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 50 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 51 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 52 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 53 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 54 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
