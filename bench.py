@@ -530,7 +530,9 @@ def bench_conv_backward(torch, hip, ctx, rank, steps=2):
     torch.cuda.empty_cache()
     return {"layers": len(specs), "batch_per_gpu": batch, "ms_per_batch": round(wall * 1e3, 3),
             "schedule": "pipelined (TNS_OPT_BWD_OVERLAP = 2: each layer's dW on the side "
-                        "stream under the following layers' work)",
+                        "stream under the following layers' work) — the schedule the Pascal "
+                        "drop-in selects (pascal/nnHip.pas initHIP, pipelineBackward = true); "
+                        "ms_per_batch_joined: the C library's default (1)",
             "ms_per_batch_joined": round(wall_joined * 1e3, 3),
             "gflop_per_batch": round(gflop, 2), "tflops": round(gflop / wall / 1e3, 2),
             "images_per_s_total": round(ctx.world * batch / wall, 1),

@@ -58,13 +58,7 @@ for l in open('gpurun_out/abgemm.jsonl'):
           rc=$?; echo "}" >> gpurun_out/fwdsweep.jsonl; [ $rc -eq 0 ] || { tail -5 gpurun_out/fwdsweep.err; exit $rc; }
         done
       done; done
-      python3 -c "
-import json,collections
-d=collections.defaultdict(list)
-for l in open('gpurun_out/fwdsweep.jsonl'):
-    r=json.loads(l.replace('\n',''))
-    for x in r['res']['layers']: d[(x['layer'], r['variant'])].append(x['ms'])
-for k in sorted(d): print(k, d[k])" ;;
+      python3 scripts/parse_fwdsweep.py ;;
     bwdsweep)
       timeout -k 10 900 python -u scripts/bwd_sweep.py --layers ${BLAYERS:-1,3,4,6,11} --what ${BWHAT:-dx} > gpurun_out/bwdsweep.json 2> gpurun_out/bwdsweep.err
       rc=$?; tail -c 4000 gpurun_out/bwdsweep.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bwdsweep.err; exit $rc; } ;;

@@ -181,7 +181,7 @@ struct Geo4 {
                 "A DMA: tile-top issue, whole 64-slot pieces");
   static_assert(!DX || (TA && !AT && !BD && !BW && !AP), "DX: k-major weights, b32 gather");
   static_assert(!AR || (!TA && !AT && !AP && !DX && !IL && !ST), "AR: [M][K] weights, block staging");
-  static_assert(!PF || (!AR && !AT && !AP && !BD && !BW && !ST), "PF: register staging");
+  static_assert(!PF || (!AT && !AP && !BD && !BW && !ST), "PF: register staging");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
   static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
@@ -445,11 +445,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   // (AR) this tile's A fragments (acur) and the next tile's loads (rar,
   // transposed in place before the tile's last group)
   floatx4 acur[G::AR ? NG : 1], rar[G::AR ? NG : 1];
+  // (AR + PF) the raw loads of the next two tiles, one set a tile parity
+  floatx4 rpf[G::AR && G::PF ? 2 : 1][G::AR && G::PF ? NG : 1];
   const float* ar_src =
       G::AR ? p.A + (m0 + (w % G::WM) * 16 + (lane & 15)) * p.lda + 4 * (lane >> 4) : nullptr;
-  auto load_ar = [&](int k0) {
+  auto load_ar = [&](int k0, floatx4* dst) {
 #pragma unroll
-    for (int g = 0; g < NG; ++g) rar[g] = *reinterpret_cast<const floatx4*>(ar_src + k0 + 16 * g);
+    for (int g = 0; g < NG; ++g) dst[g] = *reinterpret_cast<const floatx4*>(ar_src + k0 + 16 * g);
   };
   auto xpose_ar = [&]() {
 #pragma unroll
@@ -623,8 +625,20 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   Frag f0, f1;
   if (nt > 0) {
     if constexpr (G::AR) {
-      load_ar(0);
-      gather_b(b_st(0), S0{});
+      if constexpr (G::PF) {
+        load_ar(0, rpf[0]);
+        gather_b(b_st(0), S0{});
+        if (nt > 1) {  // (tile 1 into set 1, in flight past the barrier)
+          advance();
+          load_ar(BK, rpf[G::PF ? 1 : 0]);
+          gather_b(nullptr, S1{});
+        }
+#pragma unroll
+        for (int g = 0; g < NG; ++g) rar[g] = rpf[0][g];
+      } else {
+        load_ar(0, rar);
+        gather_b(b_st(0), S0{});
+      }
       store_b(b_st(0), S0{});
       xpose_ar();
 #pragma unroll
@@ -664,6 +678,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       // and the gather's offsets run past the images' range — read, unused)
       advance();
       load_a(min((t + 2) * BK, K - BK), nullptr, SL{});
+      if constexpr (G::AR) load_ar(min((t + 2) * BK, K - BK), rpf[SL::value]);
       gather_b(nullptr, SL{});
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
     } else if constexpr (more && !G::IL && !G::ST && !G::PF) {
@@ -675,7 +690,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
         load_a((t + 1) * BK, a_st(tx), S0{});
         // (AR, two groups a tile: the next tile's A at the top, a whole tile
         // ahead of its transpose; deeper tiles load it after their stores)
-        if constexpr (G::AR && NG <= 2) load_ar((t + 1) * BK);
+        if constexpr (G::AR && NG <= 2) load_ar((t + 1) * BK, rar);
         gather_b(b_st(tx), S0{});
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
@@ -707,7 +722,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       // interleaved staging (LI / SI) and this group's MFMAs
       const bool reads = g + 1 < NG || more;
       if constexpr (more && G::AR)
-        if (g == NG - 1) xpose_ar();  // (the next tile's A, loaded after the stores)
+        if (g == NG - 1) {  // (the next tile's A, loaded after the stores / PF: a tile before)
+          if constexpr (G::PF) {
+#pragma unroll
+            for (int u = 0; u < NG; ++u) rar[u] = rpf[SS::value][u];
+          }
+          xpose_ar();
+        }
       if (g + 1 < NG)
         frag(tc, g + 1, fn);
       else if (more)
@@ -717,6 +738,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           advance();
           if constexpr (G::PF) {  // (tile t+2 into this tile's set, as above)
             load_a(min((t + 2) * BK, K - BK), nullptr, SL{});
+            if constexpr (G::AR) load_ar(min((t + 2) * BK, K - BK), rpf[SL::value]);
             gather_b(nullptr, SL{});
           } else {
             load_a((t + 1) * BK, a_st(tx), S0{});
@@ -763,9 +785,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           __builtin_amdgcn_sched_barrier(0);
           TNS_PH(2);
         }
-      if constexpr (more && G::AR && NG > 2)
+      if constexpr (more && G::AR && NG > 2 && !G::PF)
         if (g == G::SG) {
-          load_ar((t + 1) * BK);  // (registers free since the last tile's end)
+          load_ar((t + 1) * BK, rar);  // (registers free since the last tile's end)
           __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -973,6 +995,12 @@ struct TileInfo4 {
                   false, false, false, false, false, true>>,                                 \
    "conv_tile4_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si" #SIv  \
    ",ri" #RIv ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4RP(BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, JAv, NAv)                     \
+  {BMv, BNv, BKv,                                                                             \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, false, JAv, NAv, false, false, \
+                  false, false, false, false, true, true>>,                                  \
+   "conv_tile4_arpf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si"   \
+   #SIv ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -1021,6 +1049,10 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, false, 3, 0, 0), // 36 (0, PF)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, true, 3, 0, 0),  // 37 (0, PF + SI)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 2, false, 3, 0, 0), // 38 (0, PF + IL)
+    // A in registers AND loaded two tiles ahead (AR + PF)
+    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, true, 2, 0, 0),   // 39 (21)
+    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, false, 2, 0, 0),  // 40 (21, stores after group 1)
+    TNS_CT4RP(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 41 (31)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
     // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
@@ -1029,33 +1061,33 @@ const TileInfo4 kTiles4[] = {
     // 13^2 +8 %, 1x1 +4..11 %): every wave loads its own 16 rows, and the
     // loads of a 64-deep tile go out after the stores, too late for the
     // tile's last group (block stamps: profiles/r05_conv_fwd_stamps.json)
-    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 39 (3)
-    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 40 (8)
-    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 41 (13)
-    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 42 (18)
-    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 43 (21)
+    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 42 (3)
+    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 43 (8)
+    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 44 (13)
+    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 45 (18)
+    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 46 (21)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 44 (3, BD)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 45 (3, BW)
-    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 46 (18, BW)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 47 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 48 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 49 (18, BW)
     // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
-    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 47 (3)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 50 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
     // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
     // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 48 (1)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 49
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 50 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 51 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 52 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 53 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 54 (11)
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 51 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 52
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 53 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 54 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 55 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 56 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 57 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
@@ -1122,6 +1154,7 @@ constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4R
 #undef TNS_CT4P
 #undef TNS_CT4PI
+#undef TNS_CT4RP
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
