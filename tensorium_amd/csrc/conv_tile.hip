@@ -323,6 +323,7 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 // the conv_tile4.hip forms picked by default (TNS_CT4_AR: their A-in-
 // registers twins, diagnostics builds only — measured slower, conv_tile4.hip)
 #ifdef TNS_CT4_AR
+constexpr int kT4OneByOnePF = 44;
 constexpr int kT4UnevenS2 = 45;
 constexpr int kT4Big = 42;       // (3) 128 x 176 x 64, stores after group 1, reads interleaved
 constexpr int kT4Small = 43;     // (8) 64 x 96 x 32, reads interleaved
@@ -343,8 +344,10 @@ constexpr int kT4OneByOne = 13;
 // -> 0.1320 (PF alone 0.1426)
 constexpr int kT4Uneven = 31;
 constexpr int kT4UnevenS2 = 30;
+constexpr int kT4OneByOnePF = 27;
 constexpr int kT4Narrow = 21;    // 128 x 48 x 64 (every PF form level or slower on 13^2)
 #else
+constexpr int kT4OneByOnePF = 13;
 constexpr int kT4UnevenS2 = 18;
 constexpr int kT4Big = 3;    // 128 x 176 x 64, stores after group 1 and reads interleaved
 constexpr int kT4Small = 8;  // 64 x 96 x 32, reads interleaved
@@ -382,8 +385,12 @@ int conv_tile_pick(const GemmArgs& a, int ks) {
   // 1x1 layers with 64..256 filters over >= 5408 pixels: the 64 x 32 form
   // (104^2 0.029 -> 0.022 ms, 52^2 0.023 -> 0.021, 26^2 0.023 -> 0.020); the
   // 512-filter 13^2 ones keep the sgemm_kernel.hpp tiles
-  if (ks == 1)
-    return a.M % 64 == 0 && a.M <= 256 && a.N >= 5408 ? kNumTiles + kT4OneByOne : -1;
+  if (ks == 1) {
+    if (a.M % 64 || a.M > 256 || a.N < 5408) return -1;
+    // (round 5: the 26^2 planes on the PF twin, 0.0205 -> 0.0194 ms;
+    // level on 52^2 / 104^2)
+    return kNumTiles + (a.N < 16384 ? kT4OneByOnePF : kT4OneByOne);
+  }
   if (ks != 3) return -1;
   if ((a.M == 128 || a.M == 256) && a.K % conv_tile4_bk(kT4Big) == 0) return kNumTiles + kT4Big;
   if ((a.M == 128 || a.M == 256) && a.conv_sY == 1) return 0;  // (stride 2: a tie)

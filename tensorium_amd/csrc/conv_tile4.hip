@@ -1049,11 +1049,13 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, false, 3, 0, 0), // 36 (0, PF)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, true, 3, 0, 0),  // 37 (0, PF + SI)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 2, false, 3, 0, 0), // 38 (0, PF + IL)
-    // A in registers AND loaded two tiles ahead (AR + PF)
+#ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
+    // A in registers AND loaded two tiles ahead (AR + PF): slower still than
+    // the LDS-staged picks (13^2 0.1336 -> 0.1447 / 0.1472 ms, 26^2 0.1269 ->
+    // 0.1402; profiles/r05_conv_fwd_sweep.json)
     TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, true, 2, 0, 0),   // 39 (21)
     TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, false, 2, 0, 0),  // 40 (21, stores after group 1)
     TNS_CT4RP(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 41 (31)
-#ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
     // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
     // class but the stride-2 104^2 / 208^2 ones (YOLOv3 batch 8, same box,
@@ -1269,13 +1271,23 @@ bool dx3_fits(int v, int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, 
 int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
                         int64_t pad) {
   const int64_t N = batch * H * W, oh = H + 2 * pad - ks + 1, ow = W + 2 * pad - ks + 1;
+  // Round 5 (scripts/bwd_sweep.py --what dx, profiles/r05_bwd_dx_sweep.json):
+  // the PF twin of the 64 x 64 form on the 104^2 (0.357 -> 0.343 ms a call)
+  // and 52^2 planes (0.318 -> 0.315); the 208^2 32-channel layer level
   int v = -1;
+#ifdef TNS_CT4_NO_PF  // (A/B side builds: round 4's picks)
   if (C % 64 && N >= 50000)
     v = 6;
   else if (N >= 50000)
     v = 4;
   else if (N >= 16384)
     v = 0;
+#else
+  if (C % 64 && N >= 50000)
+    v = 6;
+  else if (N >= 16384)
+    v = 8;
+#endif
   return v >= 0 && dx3_fits(v, batch, C, H, W, F, ks, pad, oh, ow) ? v : -1;
 }
 
@@ -1353,11 +1365,16 @@ int conv_tile4_dx3s2_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_
   if (ks != 3) return -1;
   const int64_t N = batch * (H / 2) * (W / 2), oh = (H + 2 * pad - 3) / 2 + 1,
                 ow = (W + 2 * pad - 3) / 2 + 1;
+  // (round 5: 208^2 -> 104^2 on the PF twin of 64 x 48, 0.427 -> 0.416 ms)
   int v = -1;
   if (C % 64 && N >= 50000)
     v = 6;
   else if (N >= 50000)
+#ifdef TNS_CT4_NO_PF
     v = 2;
+#else
+    v = 10;
+#endif
   return v >= 0 && dx3s2_fits(v, batch, C, H, W, F, pad, oh, ow) ? v : -1;
 }
 
