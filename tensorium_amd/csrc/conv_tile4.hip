@@ -1271,23 +1271,19 @@ bool dx3_fits(int v, int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, 
 int conv_tile4_dx3_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_t F, int64_t ks,
                         int64_t pad) {
   const int64_t N = batch * H * W, oh = H + 2 * pad - ks + 1, ow = W + 2 * pad - ks + 1;
-  // Round 5 (scripts/bwd_sweep.py --what dx, profiles/r05_bwd_dx_sweep.json):
-  // the PF twin of the 64 x 64 form on the 104^2 (0.357 -> 0.343 ms a call)
-  // and 52^2 planes (0.318 -> 0.315); the 208^2 32-channel layer level
+  // Round 5: the PF twins (forms 7..10) measured 1-4 % faster a call on
+  // the 104^2 / 52^2 / stride-2 208^2 planes (scripts/bwd_sweep.py --what dx,
+  // profiles/r05_bwd_dx_sweep.json) but level-to-slower over the pipelined
+  // 75-layer pass, where they run beside the pending dW products (14.70 /
+  // 14.72 -> 14.82 / 14.80 ms, joined 17.03 / 17.01 -> 16.94 / 16.97;
+  // profiles/r05_bwd_schedules.json): not picked
   int v = -1;
-#ifdef TNS_CT4_NO_PF  // (A/B side builds: round 4's picks)
   if (C % 64 && N >= 50000)
     v = 6;
   else if (N >= 50000)
     v = 4;
   else if (N >= 16384)
     v = 0;
-#else
-  if (C % 64 && N >= 50000)
-    v = 6;
-  else if (N >= 16384)
-    v = 8;
-#endif
   return v >= 0 && dx3_fits(v, batch, C, H, W, F, ks, pad, oh, ow) ? v : -1;
 }
 
@@ -1365,16 +1361,11 @@ int conv_tile4_dx3s2_pick(int64_t batch, int64_t C, int64_t H, int64_t W, int64_
   if (ks != 3) return -1;
   const int64_t N = batch * (H / 2) * (W / 2), oh = (H + 2 * pad - 3) / 2 + 1,
                 ow = (W + 2 * pad - 3) / 2 + 1;
-  // (round 5: 208^2 -> 104^2 on the PF twin of 64 x 48, 0.427 -> 0.416 ms)
   int v = -1;
   if (C % 64 && N >= 50000)
     v = 6;
   else if (N >= 50000)
-#ifdef TNS_CT4_NO_PF
-    v = 2;
-#else
-    v = 10;
-#endif
+    v = 2;  // (its PF twin 10: see conv_tile4_dx3_pick)
   return v >= 0 && dx3s2_fits(v, batch, C, H, W, F, pad, oh, ow) ? v : -1;
 }
 
