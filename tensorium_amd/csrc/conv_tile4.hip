@@ -216,8 +216,20 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     const int nb = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, qq = nb >> 3, rr = nb & 7;
     const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+#if defined(TNS_CT4_MAP) && TNS_CT4_MAP == 1  // (A/B side builds: row tiles outer)
+    const int tiles_n = (int)((p.N + BN - 1) / BN);
+    tn = wg % tiles_n;
+    tm = wg / tiles_n;
+#elif defined(TNS_CT4_MAP) && TNS_CT4_MAP == 2  // (groups of 4 row tiles, column-major within)
+    const int tiles_n = (int)((p.N + BN - 1) / BN);
+    const int gm = min(4, tiles_m), per = gm * tiles_n, grp = wg / per;
+    const int gs = min(gm, tiles_m - grp * gm), in = wg - grp * per;
+    tm = grp * gm + in % gs;
+    tn = in / gs;
+#else
     tm = wg % tiles_m;
     tn = wg / tiles_m;
+#endif
   }
   const int64_t m0 = (int64_t)tm * BM;
   const int n0 = tn * BN;
