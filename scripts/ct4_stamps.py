@@ -29,7 +29,7 @@ ap.add_argument("--warm-ms", type=float, default=0.0, help="load before the stam
 a = ap.parse_args()
 hip = TNNHip(0)
 lib = load()
-stamps = torch.zeros(16 * 65536, dtype=torch.int32, device="cuda")
+stamps = torch.zeros(32 * 65536, dtype=torch.int32, device="cuda")
 fn = lib.tns_debug_ct4_stamps
 fn.argtypes = [ctypes.c_void_p]
 for layer in map(int, a.layer.split(",")):
@@ -61,7 +61,7 @@ for layer in map(int, a.layer.split(",")):
     run()
     torch.cuda.synchronize()
     fn(None)
-    st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 16).astype(np.float64)
+    st = stamps.cpu().numpy().view(np.uint32).reshape(-1, 32).astype(np.float64)
     st = st[st[:, 7] > 0]
     # block timeline (100 MHz realtime): entry relative to the first block's,
     # prologue (entry -> loop start), loop, epilogue (loop end -> wave 0's
@@ -75,6 +75,17 @@ for layer in map(int, a.layer.split(",")):
     q = lambda v: [round(float(np.percentile(v, x)), 2) for x in (0, 50, 100)]  # noqa: E731
     timeline = {"entry_us_min_med_max": q(ent), "prologue_us": q(pro), "loop_us": q(loop_us),
                 "epilogue_us": q(epi), "end_us": q(end)}
+    # tile 8's barrier: each wave's arrival (s_memtime cycles) after the
+    # block's first arrival; mean lateness per wave index, and how often each
+    # wave is the last to arrive
+    arr = st[:, 16:32]
+    nw = int((arr[0] > 0).sum()) if len(arr) else 0
+    if nw > 1 and int(nt[0]) > 8:
+        a_ = arr[:, :nw]
+        late = a_ - a_.min(axis=1, keepdims=True)
+        timeline["barrier8_late_cycles_by_wave"] = [round(float(v), 1) for v in late.mean(axis=0)]
+        last = np.bincount(a_.argmax(axis=1), minlength=nw)
+        timeline["barrier8_last_counts_by_wave"] = [int(v) for v in last]
     nt = st[:, 7].astype(np.uint64) & 0xff
     rt = (st[:, 7].astype(np.uint64) >> 8).astype(np.float64)  # 100 MHz ticks
     nt = nt.astype(np.float64)

@@ -719,6 +719,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           TNS_PH(3);
           if constexpr (G::BD || G::AP) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           if constexpr (G::AT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (asm stores)
+#ifdef TNS_CT4_STAMPS
+          // every wave's arrival at tile 8's barrier (words 16 + w, realtime
+          // ticks after block entry) — who the barrier waits for
+          if (t == 8 && lane == 0 && p.stamps != nullptr && blockIdx.x < (1u << 16) && w < 16)
+            p.stamps[32 * blockIdx.x + 16 + w] =
+                (unsigned)(__builtin_amdgcn_s_memtime() & 0xffffffffu);
+#endif
           __syncthreads();
           TNS_PH(4);
         }
@@ -830,7 +837,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
 #ifdef TNS_CT4_STAMPS
   TNS_PH(5);
   if (tid == 0 && p.stamps != nullptr && blockIdx.x < (1u << 16)) {
-    unsigned* st = p.stamps + 16 * blockIdx.x;
+    unsigned* st = p.stamps + 32 * blockIdx.x;
     for (int i = 0; i < 6; ++i) st[i] = (unsigned)ph[i];
     st[6] = (unsigned)(tl - tk0);
     const unsigned long long rt_loop = __builtin_amdgcn_s_memrealtime();
@@ -916,7 +923,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
 #ifdef TNS_CT4_STAMPS
   if (tid == 0 && p.stamps != nullptr && blockIdx.x < (1u << 16)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's stores done)
-    p.stamps[16 * blockIdx.x + 11] = (unsigned)(__builtin_amdgcn_s_memrealtime() - rt_entry);
+    p.stamps[32 * blockIdx.x + 11] = (unsigned)(__builtin_amdgcn_s_memrealtime() - rt_entry);
   }
 #endif
   };
@@ -1199,7 +1206,7 @@ int conv_tile4_bk(int v) { return v >= 0 && v < kNumTiles4 ? kTiles4[v].bk : 0; 
 
 #ifdef TNS_CT4_STAMPS
 // diagnostic build only (not in include/tns.h): per-block phase cycle sums
-// of wave 0 into dev_buf (16 words per block), or nothing when NULL
+// of wave 0 into dev_buf (32 words per block), or nothing when NULL
 extern "C" int tns_debug_ct4_stamps(unsigned* dev_buf) {
   g_ct4_stamps = dev_buf;
   return 0;
