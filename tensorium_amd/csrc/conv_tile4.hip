@@ -1117,6 +1117,12 @@ const TileInfo4 kTiles4[] = {
    launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, true>>,  \
    "conv_tile4_ta<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv     \
    ",ri" #RIv ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4TP(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                      \
+  {BMv, BNv, BKv,                                                                      \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, true, false, \
+                  false, false, false, false, false, true>>,                            \
+   "conv_tile4_ta_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv   \
+   ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4T[] = {
     TNS_CT4T(128, 176, 8, 1, 64, 1, true, 2, 0, 0),   // 0
     TNS_CT4T(128, 96, 8, 1, 64, 1, true, 2, 0, 0),    // 1
@@ -1129,6 +1135,10 @@ const TileInfo4 kTiles4T[] = {
     TNS_CT4T(64, 64, 4, 1, 32, 0, false, 3, 0, 0),    // 8
     TNS_CT4T(128, 64, 8, 1, 32, 0, false, 3, 0, 0),   // 9
     TNS_CT4T(64, 128, 4, 2, 32, 0, false, 3, 0, 0),   // 10
+    // PF twins (operands of tile t+2 loaded at the top of tile t) of 4, 7, 2
+    TNS_CT4TP(64, 96, 4, 1, 32, 0, false, 3, 0, 0),   // 11 (4)
+    TNS_CT4TP(64, 64, 4, 2, 32, 0, false, 3, 0, 0),   // 12 (7)
+    TNS_CT4TP(128, 48, 8, 1, 64, 1, true, 2, 0, 0),   // 13 (2)
 };
 constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
 // k-major A, tap-major k (DX): state.delta of stride-1 3x3 layers
@@ -1172,6 +1182,7 @@ constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4UD
 #undef TNS_CT4X
 #undef TNS_CT4T
+#undef TNS_CT4TP
 #undef TNS_CT4R
 #undef TNS_CT4P
 #undef TNS_CT4PI
