@@ -177,8 +177,10 @@ int tns_hip_gemm_strided_batched(tns_ctx* ctx, uint8_t transA, uint8_t transB,
  * device-resident as the reference builds them with writeBuffer
  * (nConvolutionLayer.pas:1083-1085) or host-resident; the element offsets
  * apply to every entry.  The arrays are read in stream order (the call
- * waits for them); equally spaced entries run as one strided-batched
- * launch, others GEMM by GEMM in array order.  Results as tns_hip_gemm. */
+ * waits for them); equally spaced entries whose GEMMs are independent (no
+ * C entry overlaps another C entry or any A / B entry) run as one
+ * strided-batched launch, all others GEMM by GEMM in array order, so an
+ * entry may read what an earlier one wrote.  Results as tns_hip_gemm. */
 int tns_hip_gemm_batched(tns_ctx* ctx, uint8_t transA, uint8_t transB,
                          int64_t M, int64_t N, int64_t K, float ALPHA,
                          const float* const* A, int64_t aOffset, int64_t lda,

@@ -80,7 +80,7 @@ for layer in map(int, a.layer.split(",")):
     # wave is the last to arrive
     arr = st[:, 16:32]
     nw = int((arr[0] > 0).sum()) if len(arr) else 0
-    if nw > 1 and int(nt[0]) > 8:
+    if nw > 1 and int(st[0, 7]) & 0xff > 8:
         a_ = arr[:, :nw]
         late = a_ - a_.min(axis=1, keepdims=True)
         timeline["barrier8_late_cycles_by_wave"] = [round(float(v), 1) for v in late.mean(axis=0)]

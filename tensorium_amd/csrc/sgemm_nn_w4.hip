@@ -70,22 +70,9 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   // XCD-contiguous grouped raster (as sgemm_nn_big.hip)
   const int tiles_m = (int)(p.M / BM), tiles_n = (int)(p.N / BN);
   int tm, tn;
-  int64_t bz = blockIdx.y;
-  int bidx = blockIdx.x;
-#ifndef TNS_W4_XCD_SPREAD
-  // a batch of small GEMMs (every GEMM's tiles fit one XCD, the batch a
-  // multiple of 8): all tiles of GEMM g on XCD g % 8 (the dispatcher deals
-  // workgroups to the XCDs round-robin by linear id), so a GEMM's A and B
-  // k-slices are fetched into ONE L2 and shared by its tiles there, instead
-  // of every XCD holding two of each GEMM's tiles
-  if (gridDim.y % 8 == 0 && gridDim.x <= 32) {
-    const int L = (int)(blockIdx.x + blockIdx.y * gridDim.x), xcd = L & 7, loc = L >> 3;
-    bz = (int64_t)(loc / (int)gridDim.x) * 8 + xcd;
-    bidx = loc % (int)gridDim.x;
-  }
-#endif
+  const int64_t bz = blockIdx.y;
   {
-    const int nb = tiles_m * tiles_n, bid = bidx;
+    const int nb = tiles_m * tiles_n, bid = blockIdx.x;
     const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
     constexpr int GROUP_M = 8;
