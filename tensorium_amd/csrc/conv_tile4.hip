@@ -80,8 +80,21 @@ struct Frag4 {
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
           int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
           bool BD_ = false, bool BW_ = false, bool AP_ = false, bool AT_ = false,
-          bool DX_ = false, bool AR_ = false, bool PF_ = false>
+          bool DX_ = false, bool AR_ = false, bool PF_ = false, bool AB_ = false>
 struct Geo4 {
+  // AB: no workgroup barrier in the k-loop.  Three LDS stages and per-stage
+  // counters in LDS: a wave adds 1 to stored[s] once its stores of a tile
+  // into stage s are issued and to consumed[s] once its last read of the
+  // tile in s is done; a reader of tile j waits for stored[j % 3] to reach
+  // NW * (j / 3 + 1), a writer of tile j for consumed[j % 3] to reach
+  // NW * (j / 3) (LDS operations of one wave complete in order, so a count
+  // seen implies the data it covers).  The older wave of a SIMD, which the
+  // issue arbiter favours, then runs up to a tile ahead instead of waiting
+  // at a barrier for its partner (block stamps: waves w + NW/2 always arrive
+  // last, profiles/r05_conv_fwd_stamps.json).  With PF; the tile's stores
+  // at its top
+  static constexpr bool AB = AB_;
+  static constexpr int NSTG = AB_ ? 3 : 2;
   // PF: the register-staged operands of tile t+2 are loaded at the top of
   // tile t (two register sets, the tile pairs unrolled), so a gather has a
   // whole tile to land before its stores (the 2-group 26^2 / 13^2 forms
@@ -172,7 +185,7 @@ struct Geo4 {
   static_assert(!ST || (!IL && !SI && SG + 1 <= NG - 2 && NW % 2 == 0), "staggered staging");
   static_assert(AU >= 1 && BM * BK / 4 % NT == 0 && KI >= 1 && BK / 4 % NW == 0, "geometry");
   static_assert(NA * JA + (WN - NA) * JB == J && NA >= 1 && NA <= WN, "wave column split");
-  static_assert(2 * STAGE * 4 <= 163840, "LDS");
+  static_assert(NSTG * STAGE * 4 + 64 <= 163840, "LDS");
   static_assert(!BD || (!IL && !ST && !TA), "DMA gather: tile-top issue only");
   static_assert(!(BD && BW), "one gather form");
   static_assert(!AT || (!BD && !BW && !TA && !AP && !SI && 2 * B_TILE * 4 <= 98304),
@@ -182,6 +195,7 @@ struct Geo4 {
   static_assert(!DX || (TA && !AT && !BD && !BW && !AP), "DX: k-major weights, b32 gather");
   static_assert(!AR || (!TA && !AT && !AP && !DX && !IL && !ST), "AR: [M][K] weights, block staging");
   static_assert(!PF || (!AT && !AP && !BD && !BW && !ST), "PF: register staging");
+  static_assert(!AB || (PF && !AR && !IL && !SI && !ST), "AB: PF, stores at the tile top");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
   static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
@@ -193,7 +207,11 @@ template <class G, int KS>
 __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) {
   constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, NG = G::NG;
   constexpr int A_TILE = G::A_TILE, STAGE = G::STAGE, AU = G::AU, KI = G::KI;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) float smem[G::NSTG * STAGE];
+  // (AB) stored[3], consumed[3]: stage s is read by a wave only once
+  // stored[s] counts every wave's stores of its tile, rewritten only once
+  // consumed[s] counts every wave's reads of the previous one
+  __shared__ unsigned abc[G::AB ? 6 : 1];
 #ifdef TNS_CT4_STAMPS
   const unsigned long long rt_entry = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -659,6 +677,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       frag(0, 0, f0);
     }
   }
+  if constexpr (G::AB)  // (tile 0: stored by every wave before the prologue's barrier)
+    if (tid < 6) abc[tid] = tid == 0 ? (unsigned)G::NW : 0u;
   if (nt > 0 && !G::AR) {
     load_a(0, a_st(0), S0{});
     gather_b(b_st(0), S0{});
@@ -683,7 +703,20 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     constexpr int par = decltype(PAR)::value;
     using SL = std::integral_constant<int, G::PF ? par : 0>;
     using SS = std::integral_constant<int, G::PF ? par ^ 1 : 0>;
-    const int tc = t & 1, tx = (t + 1) & 1;
+    const int tc = G::AB ? t % 3 : t & 1, tx = G::AB ? (t + 1) % 3 : (t + 1) & 1;
+    // (AB) counter waits and signals: relaxed LDS atomics between compiler
+    // fences (the hardware keeps a wave's LDS operations in order)
+    auto ab_wait = [&](int c, unsigned target) {
+      asm volatile("" ::: "memory");
+      while (__hip_atomic_load(&abc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+        __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");
+    };
+    auto ab_signal = [&](int c) {
+      asm volatile("" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(&abc[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      asm volatile("" ::: "memory");
+    };
     TNS_PH(5);
     if constexpr (more && G::PF && !G::IL) {
       // (unconditional: past the last tile the weight rows' k is clamped
@@ -693,6 +726,13 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (G::AR) load_ar(min((t + 2) * BK, K - BK), rpf[SL::value]);
       gather_b(nullptr, SL{});
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
+      if constexpr (G::AB) {  // tile t+1 into stage tx, once tile t-2's readers are done
+        ab_wait(3 + tx, (unsigned)(G::NW * ((t + 1) / 3)));
+        store_a(a_st(tx), SS{});
+        store_b(b_st(tx), SS{});
+        ab_signal(tx);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     } else if constexpr (more && !G::IL && !G::ST && !G::PF) {
       advance();
       if constexpr (G::BD) {
@@ -726,7 +766,12 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
             p.stamps[32 * blockIdx.x + 16 + w] =
                 (unsigned)(__builtin_amdgcn_s_memtime() & 0xffffffffu);
 #endif
-          __syncthreads();
+          if constexpr (G::AB) {
+            ab_signal(3 + tc);  // (this wave's reads of tile t are issued and waited for below)
+            ab_wait(tx, (unsigned)(G::NW * ((t + 1) / 3 + 1)));
+          } else {
+            __syncthreads();
+          }
           TNS_PH(4);
         }
       __builtin_amdgcn_sched_barrier(0);
@@ -796,7 +841,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           store_b(b_st(tx), S0{});
           __builtin_amdgcn_sched_barrier(0);
         }
-      if constexpr (more && !G::SI && !G::ST)
+      if constexpr (more && !G::SI && !G::ST && !G::AB)
         if (g == G::SG) {
           TNS_PH(1);
           store_a(a_st(tx), SS{});
@@ -1020,6 +1065,11 @@ struct TileInfo4 {
                   false, false, false, false, true, true>>,                                  \
    "conv_tile4_arpf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si"   \
    #SIv ",ri" #RIv ",j" #JAv "x" #NAv ">"}
+#define TNS_CT4AB(BMv, BNv, WMv, WNv, BKv, RIv, JAv, NAv)                                      \
+  {BMv, BNv, BKv,                                                                             \
+   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, 0, 0, false, RIv, false, JAv, NAv, false, false,   \
+                  false, false, false, false, false, true, true>>,                           \
+   "conv_tile4_ab<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -1068,13 +1118,19 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, false, 3, 0, 0), // 36 (0, PF)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, true, 3, 0, 0),  // 37 (0, PF + SI)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 2, false, 3, 0, 0), // 38 (0, PF + IL)
+    // no workgroup barrier in the k-loop (AB: three stages, LDS counters)
+    TNS_CT4AB(64, 176, 4, 2, 32, 3, 6, 1),               // 39 (25)
+    TNS_CT4AB(128, 48, 8, 1, 64, 2, 0, 0),               // 40 (26)
+    TNS_CT4AB(128, 176, 8, 1, 32, 3, 0, 0),              // 41 (36)
+    TNS_CT4AB(64, 32, 4, 1, 32, 0, 0, 0),                // 42 (27)
+    TNS_CT4AB(64, 96, 4, 1, 32, 3, 0, 0),                // 43 (28)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
     // A in registers AND loaded two tiles ahead (AR + PF): slower still than
     // the LDS-staged picks (13^2 0.1336 -> 0.1447 / 0.1472 ms, 26^2 0.1269 ->
     // 0.1402; profiles/r05_conv_fwd_sweep.json)
-    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, true, 2, 0, 0),   // 39 (21)
-    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, false, 2, 0, 0),  // 40 (21, stores after group 1)
-    TNS_CT4RP(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 41 (31)
+    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, true, 2, 0, 0),   // 44 (21)
+    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, false, 2, 0, 0),  // 45 (21, stores after group 1)
+    TNS_CT4RP(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 46 (31)
     // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
     // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
     // class but the stride-2 104^2 / 208^2 ones (YOLOv3 batch 8, same box,
@@ -1082,33 +1138,33 @@ const TileInfo4 kTiles4[] = {
     // 13^2 +8 %, 1x1 +4..11 %): every wave loads its own 16 rows, and the
     // loads of a 64-deep tile go out after the stores, too late for the
     // tile's last group (block stamps: profiles/r05_conv_fwd_stamps.json)
-    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 42 (3)
-    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 43 (8)
-    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 44 (13)
-    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 45 (18)
-    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 46 (21)
+    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 47 (3)
+    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 48 (8)
+    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 49 (13)
+    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 50 (18)
+    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 51 (21)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 47 (3, BD)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 48 (3, BW)
-    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 49 (18, BW)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 52 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 53 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 54 (18, BW)
     // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
-    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 50 (3)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 55 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
     // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
     // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 51 (1)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 52
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 53 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 54 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 55 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 56 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 57 (11)
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 56 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 57
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 58 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 59 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 60 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 61 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 62 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
@@ -1187,6 +1243,7 @@ constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4P
 #undef TNS_CT4PI
 #undef TNS_CT4RP
+#undef TNS_CT4AB
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
