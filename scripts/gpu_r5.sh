@@ -12,7 +12,8 @@ lib_of() { [ "$1" = main ] && echo tensorium_amd/libtensorium_hip.so || echo ab/
 for S in ${STEPS}; do
   case $S in
     tests)
-      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:-} > gpurun_out/gpu_tests.log 2>&1
+      if [ -n "${TESTK:-}" ]; then KARG=(-k "$TESTK"); else KARG=(); fi
+      timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${KARG[@]}" > gpurun_out/gpu_tests.log 2>&1
       rc=$?; tail -5 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
     abfwd)
       for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do

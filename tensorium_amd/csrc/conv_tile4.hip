@@ -84,11 +84,11 @@ template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, boo
 struct Geo4 {
   // AB: no workgroup barrier in the k-loop.  Three LDS stages and per-stage
   // counters in LDS: a wave adds 1 to stored[s] once its stores of a tile
-  // into stage s are issued and to consumed[s] once its last read of the
-  // tile in s is done; a reader of tile j waits for stored[j % 3] to reach
-  // NW * (j / 3 + 1), a writer of tile j for consumed[j % 3] to reach
-  // NW * (j / 3) (LDS operations of one wave complete in order, so a count
-  // seen implies the data it covers).  The older wave of a SIMD, which the
+  // into stage s are issued, and a reader of tile j waits for stored[j % 3]
+  // to reach NW * (j / 3 + 1) (LDS operations of one wave complete in order,
+  // so a count seen implies the data it covers); a stage is rewritten only
+  // by a wave that has seen the previous tile's count, i.e. once every wave
+  // has issued its stores of that tile — after its last read two tiles back.  The older wave of a SIMD, which the
   // issue arbiter favours, then runs up to a tile ahead instead of waiting
   // at a barrier for its partner (block stamps: waves w + NW/2 always arrive
   // last, profiles/r05_conv_fwd_stamps.json).  With PF; the tile's stores
@@ -208,10 +208,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, NG = G::NG;
   constexpr int A_TILE = G::A_TILE, STAGE = G::STAGE, AU = G::AU, KI = G::KI;
   __shared__ __attribute__((aligned(16))) float smem[G::NSTG * STAGE];
-  // (AB) stored[3], consumed[3]: stage s is read by a wave only once
-  // stored[s] counts every wave's stores of its tile, rewritten only once
-  // consumed[s] counts every wave's reads of the previous one
-  __shared__ unsigned abc[G::AB ? 6 : 1];
+  // (AB) stored[3]: stage s is read by a wave only once stored[s] counts
+  // every wave's stores of its tile
+  __shared__ unsigned abc[G::AB ? 3 : 1];
 #ifdef TNS_CT4_STAMPS
   const unsigned long long rt_entry = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -678,7 +677,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   }
   if constexpr (G::AB)  // (tile 0: stored by every wave before the prologue's barrier)
-    if (tid < 6) abc[tid] = tid == 0 ? (unsigned)G::NW : 0u;
+    if (tid < 3) abc[tid] = tid == 0 ? (unsigned)G::NW : 0u;
   if (nt > 0 && !G::AR) {
     load_a(0, a_st(0), S0{});
     gather_b(b_st(0), S0{});
@@ -726,8 +725,10 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       if constexpr (G::AR) load_ar(min((t + 2) * BK, K - BK), rpf[SL::value]);
       gather_b(nullptr, SL{});
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
-      if constexpr (G::AB) {  // tile t+1 into stage tx, once tile t-2's readers are done
-        ab_wait(3 + tx, (unsigned)(G::NW * ((t + 1) / 3)));
+      if constexpr (G::AB) {
+        // tile t+1 into stage tx, whose previous tile (t-2) every wave has
+        // read: this wave passed the wait for tile t's stores, which every
+        // wave issues at the top of its tile t-1, after its last read of t-2
         store_a(a_st(tx), SS{});
         store_b(b_st(tx), SS{});
         ab_signal(tx);
@@ -767,7 +768,6 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
                 (unsigned)(__builtin_amdgcn_s_memtime() & 0xffffffffu);
 #endif
           if constexpr (G::AB) {
-            ab_signal(3 + tc);  // (this wave's reads of tile t are issued and waited for below)
             ab_wait(tx, (unsigned)(G::NW * ((t + 1) / 3 + 1)));
           } else {
             __syncthreads();
