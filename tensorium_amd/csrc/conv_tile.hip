@@ -323,13 +323,13 @@ constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 // the conv_tile4.hip forms picked by default (TNS_CT4_AR: their A-in-
 // registers twins, diagnostics builds only — measured slower, conv_tile4.hip)
 #ifdef TNS_CT4_AR
-constexpr int kT4OneByOnePF = 49;
-constexpr int kT4UnevenS2 = 50;
-constexpr int kT4Big = 47;       // (3) 128 x 176 x 64, stores after group 1, reads interleaved
-constexpr int kT4Small = 48;     // (8) 64 x 96 x 32, reads interleaved
-constexpr int kT4OneByOne = 49;  // (13) 64 x 32 x 32, 4 waves (1x1 layers)
-constexpr int kT4Uneven = 50;    // (18) 64 x 176 x 32, wave columns 6 + 5 fragments
-constexpr int kT4Narrow = 51;    // (21) 128 x 48 x 64, stores and reads interleaved
+constexpr int kT4OneByOnePF = 48;
+constexpr int kT4UnevenS2 = 49;
+constexpr int kT4Big = 46;       // (3) 128 x 176 x 64, stores after group 1, reads interleaved
+constexpr int kT4Small = 47;     // (8) 64 x 96 x 32, reads interleaved
+constexpr int kT4OneByOne = 48;  // (13) 64 x 32 x 32, 4 waves (1x1 layers)
+constexpr int kT4Uneven = 49;    // (18) 64 x 176 x 32, wave columns 6 + 5 fragments
+constexpr int kT4Narrow = 50;    // (21) 128 x 48 x 64, stores and reads interleaved
 #elif !defined(TNS_CT4_NO_PF)
 // the 2-group 26^2 and the 13^2 forms as their loads-two-tiles-ahead twins
 // (PF); the others keep one register set (PF: 128 x 176 spills, 64 x 96 and
@@ -342,9 +342,9 @@ constexpr int kT4OneByOne = 13;
 // batch 8 (scripts/conv_fwd_layers.py, profiles/r05_conv_fwd_sweep.json):
 // 26^2 0.1348 -> 0.1268 ms (PF alone 0.1296), 52^2 -> 26^2 stride 2 0.1431
 // -> 0.1320 (PF alone 0.1426)
-constexpr int kT4Uneven = 31;
-constexpr int kT4UnevenS2 = 30;
-constexpr int kT4OneByOnePF = 27;
+constexpr int kT4Uneven = 27;
+constexpr int kT4UnevenS2 = 26;
+constexpr int kT4OneByOnePF = 25;
 constexpr int kT4Narrow = 21;    // 128 x 48 x 64 (every PF form level or slower on 13^2)
 #else
 constexpr int kT4OneByOnePF = 13;

@@ -385,11 +385,14 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           const unsigned off = ok ? vbase[j] + x : 0x80000000u;
           const unsigned row = lds0 + 4u * (unsigned)((bs - smem) + ((wu * KI + ii) * BN + 16 * j) * 4);
           unsigned keep;
+          // (a copy: an asm operand alone does not make the generic lambda
+          // capture rsrc)
+          const __amdgpu_buffer_rsrc_t rs = rsrc;
           asm volatile(
               "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
               "buffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
               : "=&s"(keep)
-              : "v"(off), "s"(rsrc), "s"(row)
+              : "v"(off), "s"(rs), "s"(row)
               : "memory");
         } else {
 #if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 1)
@@ -707,8 +710,11 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     // fences (the hardware keeps a wave's LDS operations in order)
     auto ab_wait = [&](int c, unsigned target) {
       asm volatile("" ::: "memory");
-      while (__hip_atomic_load(&abc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+      while (__hip_atomic_load(&abc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
+#ifndef TNS_CT4_AB_SPIN  // (A/B: a bare spin)
         __builtin_amdgcn_s_sleep(1);
+#endif
+      }
       asm volatile("" ::: "memory");
     };
     auto ab_signal = [&](int c) {
@@ -1099,38 +1105,43 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4(64, 48, 4, 1, 32, 0, 0, false, 3, false),    // 22
     TNS_CT4(64, 48, 4, 1, 64, 1, 0, true, 2, false),     // 23
     TNS_CT4(128, 96, 8, 1, 64, 1, 0, true, 2, false),    // 24
-    // loads two tiles ahead (PF: two register sets) of the picked forms
-    TNS_CT4P(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 25 (18)
-    TNS_CT4P(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 26 (21)
-    TNS_CT4P(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 27 (13)
-    TNS_CT4P(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 28 (8)
-    TNS_CT4P(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 29 (3)
-    // ... with the loads of tile t+2 (IL: 2 VALU per MFMA) and / or the
-    // stores of tile t+1 interleaved with group 0's MFMAs
-    TNS_CT4PI(64, 176, 4, 2, 32, 0, 2, false, 3, 6, 1),  // 30 (18, IL)
-    TNS_CT4PI(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 31 (18, SI)
-    TNS_CT4PI(64, 176, 4, 2, 32, 0, 2, true, 3, 6, 1),   // 32 (18, IL + SI)
-    TNS_CT4PI(64, 176, 4, 2, 64, 1, 2, true, 2, 6, 1),   // 33 (17, IL + SI)
-    TNS_CT4PI(128, 48, 8, 1, 64, 1, 2, true, 2, 0, 0),   // 34 (21, IL + SI)
-    TNS_CT4PI(128, 48, 8, 1, 64, 0, 2, true, 2, 0, 0),   // 35 (21, IL + SI in group 0)
-    // 128 x 176 x 32 (the 52^2 / 104^2 tile in 2-group k-tiles: one
-    // register set fits where the 64-deep PF form spills)
-    TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, false, 3, 0, 0), // 36 (0, PF)
-    TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, true, 3, 0, 0),  // 37 (0, PF + SI)
-    TNS_CT4PI(128, 176, 8, 1, 32, 0, 2, false, 3, 0, 0), // 38 (0, PF + IL)
-    // no workgroup barrier in the k-loop (AB: three stages, LDS counters)
-    TNS_CT4AB(64, 176, 4, 2, 32, 3, 6, 1),               // 39 (25)
-    TNS_CT4AB(128, 48, 8, 1, 64, 2, 0, 0),               // 40 (26)
-    TNS_CT4AB(128, 176, 8, 1, 32, 3, 0, 0),              // 41 (36)
-    TNS_CT4AB(64, 32, 4, 1, 32, 0, 0, 0),                // 42 (27)
-    TNS_CT4AB(64, 96, 4, 1, 32, 3, 0, 0),                // 43 (28)
+    // round 5, loads two tiles ahead (PF: two register sets, tile pairs
+    // unrolled) — the picked ones (profiles/r05_conv_fwd_sweep.json)
+    TNS_CT4P(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 25 (13: 26^2 1x1 layers)
+    TNS_CT4PI(64, 176, 4, 2, 32, 0, 2, false, 3, 6, 1),  // 26 (18 + loads interleaved: stride 2)
+    TNS_CT4PI(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 27 (18 + stores interleaved: stride 1)
 #ifdef TNS_DIAG_KERNELS  // (diagnostics build only: measured, not picked)
+    // PF forms measured and not picked (sweeps: profiles/r05_conv_fwd_sweep.json):
+    // 26^2 0.1296 (PF alone) / 0.1311 (IL + SI) / 0.1273 (64-deep) against
+    // 0.1268 for 27; 13^2 0.141 / 0.143 / 0.136 against 0.134 for 21; the
+    // 64-deep 128 x 176 PF form spills, the 32-deep ones 2-3 % behind 3
+    TNS_CT4P(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 28 (18)
+    TNS_CT4P(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 29 (21)
+    TNS_CT4P(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 30 (8)
+    TNS_CT4PI(64, 176, 4, 2, 32, 0, 2, true, 3, 6, 1),   // 31 (18, IL + SI)
+    TNS_CT4PI(64, 176, 4, 2, 64, 1, 2, true, 2, 6, 1),   // 32 (17, IL + SI)
+    TNS_CT4PI(128, 48, 8, 1, 64, 1, 2, true, 2, 0, 0),   // 33 (21, IL + SI)
+    TNS_CT4PI(128, 48, 8, 1, 64, 0, 2, true, 2, 0, 0),   // 34 (21, IL + SI in group 0)
+    TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, false, 3, 0, 0), // 35 (0, PF)
+    TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, true, 3, 0, 0),  // 36 (0, PF + SI)
+    TNS_CT4PI(128, 176, 8, 1, 32, 0, 2, false, 3, 0, 0), // 37 (0, PF + IL)
+    // no workgroup barrier in the k-loop (AB: three LDS stages, per-stage
+    // counters): bit-exact and slower on every class — 26^2 0.1267 -> 0.131,
+    // 13^2 0.134 -> 0.139, 52^2 0.1145 -> 0.119 (with s_sleep in the poll;
+    // a bare spin 0.139 / 0.144; with a second, consumed-side counter
+    // 0.137 / 0.142): the barrier the wave pairs meet at costs less than the
+    // polls that replace it
+    TNS_CT4AB(64, 176, 4, 2, 32, 3, 6, 1),               // 38 (18's shape)
+    TNS_CT4AB(128, 48, 8, 1, 64, 2, 0, 0),               // 39 (21's shape)
+    TNS_CT4AB(128, 176, 8, 1, 32, 3, 0, 0),              // 40 (0's shape, 32 deep)
+    TNS_CT4AB(64, 32, 4, 1, 32, 0, 0, 0),                // 41 (13's shape)
+    TNS_CT4AB(64, 96, 4, 1, 32, 3, 0, 0),                // 42 (8's shape)
     // A in registers AND loaded two tiles ahead (AR + PF): slower still than
     // the LDS-staged picks (13^2 0.1336 -> 0.1447 / 0.1472 ms, 26^2 0.1269 ->
     // 0.1402; profiles/r05_conv_fwd_sweep.json)
-    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, true, 2, 0, 0),   // 44 (21)
-    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, false, 2, 0, 0),  // 45 (21, stores after group 1)
-    TNS_CT4RP(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 46 (31)
+    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, true, 2, 0, 0),   // 43 (21)
+    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, false, 2, 0, 0),  // 44 (21, stores after group 1)
+    TNS_CT4RP(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 45 (31)
     // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
     // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
     // class but the stride-2 104^2 / 208^2 ones (YOLOv3 batch 8, same box,
@@ -1138,33 +1149,33 @@ const TileInfo4 kTiles4[] = {
     // 13^2 +8 %, 1x1 +4..11 %): every wave loads its own 16 rows, and the
     // loads of a 64-deep tile go out after the stores, too late for the
     // tile's last group (block stamps: profiles/r05_conv_fwd_stamps.json)
-    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 47 (3)
-    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 48 (8)
-    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 49 (13)
-    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 50 (18)
-    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 51 (21)
+    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 46 (3)
+    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 47 (8)
+    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 48 (13)
+    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 49 (18)
+    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 50 (21)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 52 (3, BD)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 53 (3, BW)
-    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 54 (18, BW)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 51 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 52 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 53 (18, BW)
     // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
-    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 55 (3)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 54 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
     // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
     // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 56 (1)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 57
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 58 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 59 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 60 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 61 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 62 (11)
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 55 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 56
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 57 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 58 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 59 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 60 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 61 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
