@@ -1,6 +1,9 @@
 #!/bin/bash
 # Round-5 GPU batch: STEPS selects the steps (space-separated names).
-#   tests   — pytest -m gpu (whole suite, or TESTS=<pytest args>)
+#   tests   — pytest -m gpu (whole suite, or TESTK=<pytest -k expression>)
+#   diagtests — the variant sweeps against the ab/diag build (TNS_DIAG=1:
+#             the measured, not picked forms included)
+#   mlpst   — MNIST fused-step stage stamps (ab/mlpst: -DTNS_MLP_STAMPS)
 #   abfwd   — conv forward A/B: LIBS builds under ab/ (+ "main" = the tree)
 #   bwdab   — conv backward schedules (bwd_graph.py) for LIBS
 #   bench   — python bench.py (default flags) -> gpurun_out/bench.json
@@ -15,6 +18,12 @@ for S in ${STEPS}; do
       if [ -n "${TESTK:-}" ]; then KARG=(-k "$TESTK"); else KARG=(); fi
       timeout -k 10 1200 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "${KARG[@]}" > gpurun_out/gpu_tests.log 2>&1
       rc=$?; tail -5 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+    diagtests)
+      TNS_LIB=ab/diag/libtensorium_hip.so timeout -k 10 900 python -u -m pytest tests/test_gpu_conv.py -m gpu -x -q --timeout 600 --timeout-method thread -k "variants" > gpurun_out/gpu_diag_tests.log 2>&1
+      rc=$?; tail -5 gpurun_out/gpu_diag_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+    mlpst)
+      TNS_LIB=ab/mlpst/libtensorium_hip.so timeout -k 10 120 python -u scripts/mlp_stamps.py > gpurun_out/mlp_stamps.log 2>&1
+      rc=$?; grep -v amdgpu.ids gpurun_out/mlp_stamps.log; [ $rc -eq 0 ] || exit $rc ;;
     abfwd)
       for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do
         TNS_LIB=$(lib_of $L) timeout -k 10 300 python -u scripts/quick_perf.py --tag $L --yolo-only >> gpurun_out/abfwd.jsonl 2> gpurun_out/abfwd_$L.err

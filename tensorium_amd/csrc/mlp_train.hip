@@ -402,6 +402,28 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   const float wdec = -a.decay * (float)B;
   const float mom = a.momentum;
 
+  // ---- L2 warm-up: one load per 128-byte line of layers 1.. (weights, their
+  // updates, the stored outputs read as 0*C, the per-channel vectors; the
+  // first 256 KB), issued before anything else so the lines the previous
+  // step's launch wrote (another XCD's L2, or memory) are in this XCD's L2
+  // when the stages read them.  Consumed after layer 0's partials are in LDS:
+  // those loads were issued later, so waiting for them already waited for
+  // these (loads complete in order)
+  constexpr int NWARM = 2;
+  float warmv[NWARM];
+#pragma unroll
+  for (int j = 0; j < NWARM; ++j) warmv[j] = 0.0f;
+#ifndef TNS_MLP_NO_WARM
+  if (L > 1) {
+    const int64_t lo = a.off[1][F_W], hi = a.softmax_off;
+#pragma unroll
+    for (int j = 0; j < NWARM; ++j) {
+      const int64_t i = lo + 32 * ((int64_t)threadIdx.x + (int64_t)j * NT);
+      warmv[j] = a.buf[i < hi ? i : lo];
+    }
+  }
+#endif
+
   // ---- forward ------------------------------------------------------------
   MLP_STAMP(0);
   const float* in = a.X;
@@ -447,6 +469,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       } else {
         for (int i = tid; i < (int)(8 * BO); i += NT) lds[i] = a.l0part[i];
       }
+      asm volatile("" ::"v"(warmv[0]), "v"(warmv[1]));  // (NWARM = 2)
     } else if (tm * tn * 8 <= NWAVES && a.lds_chunks) {
       if (I > 64)
         gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn, tid);
