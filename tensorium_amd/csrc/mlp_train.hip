@@ -102,7 +102,7 @@ enum { F_W, F_B, F_DW, F_DB, F_SCALES, F_RMEAN, F_RVAR, F_DSCALES, F_OUT, F_DELT
 struct Layer {
   const MlpArgs* a;
   int l;
-  int64_t I, O;
+  int I, O;
   int act;
   __device__ Layer(const MlpArgs& args, int layer)
       : a(&args), l(layer), I(args.widths[layer]), O(args.widths[layer + 1]),
@@ -132,15 +132,15 @@ struct Layer {
 // (va / vb false) are 0.  Operands of U steps are loaded together (one memory
 // latency per U steps), then consumed by U dependent MFMAs in step order.
 template <int U = 8>
-__device__ __forceinline__ void mfma_chain(floatx16& acc, int steps, const float* pa, int64_t sa,
-                                           bool va, const float* pb, int64_t sb, bool vb,
-                                           int64_t k0, int64_t kstep, int64_t K) {
+__device__ __forceinline__ void mfma_chain(floatx16& acc, int steps, const float* pa, int sa,
+                                           bool va, const float* pb, int sb, bool vb,
+                                           int k0, int kstep, int K) {
   for (int s = 0; s < steps; s += U) {
     float av[U], bv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // the last batch may be partial: loads stay together
-      const bool ok = (s + u < steps) && k0 + (int64_t)(s + u) * kstep < K;
-      const int64_t ia = ok ? (int64_t)(s + u) * sa : 0, ib = ok ? (int64_t)(s + u) * sb : 0;
+      const bool ok = (s + u < steps) && k0 + (int)(s + u) * kstep < K;
+      const int ia = ok ? (int)(s + u) * sa : 0, ib = ok ? (int)(s + u) * sb : 0;
       const float x = pa[ia], y = pb[ib];
       av[u] = (ok && va) ? x : 0.0f;
       bv[u] = (ok && vb) ? y : 0.0f;
@@ -178,8 +178,8 @@ __device__ __forceinline__ int stage_tid() {
 // two.  The chunks alias the partial-sum region: every wave has passed the
 // barrier after the last chunk before any partial is written.
 template <int KCH>
-__device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const float* W, int64_t B,
-                                             int64_t O, int64_t I, int tm, int tn, int tid) {
+__device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const float* W, int B,
+                                             int O, int I, int tm, int tn, int tid) {
   constexpr int KP = KCH + 1;  // LDS row: an odd stride for the lanes' row reads
   constexpr int QR = KCH / 4;  // float4 units per staged row
   constexpr int UV = (3 * 32 * QR + NT - 1) / NT;  // units per thread (tm + tn <= 3)
@@ -204,17 +204,17 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
     }
   };
   const bool vec = (I & 3) == 0 && ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(W)) & 15) == 0;
-  const int64_t nch = (I + KCH - 1) / KCH;
+  const int nch = (I + KCH - 1) / KCH;
   if (vec) {
     const int units = rows * QR;
-    auto load = [&](int64_t kc0, float4 (&v)[UV]) {
+    auto load = [&](int kc0, float4 (&v)[UV]) {
 #pragma unroll
       for (int u = 0; u < UV; ++u) {
         const int idx = tid + u * NT;
         const int row = idx / QR, kq = idx % QR;
-        const int64_t k = kc0 + 4 * kq;
+        const int k = kc0 + 4 * kq;
         const bool isx = row < rowsX;
-        const int64_t rr = isx ? row : row - rowsX;
+        const int rr = isx ? row : row - rowsX;
         const bool ok = idx < units && k < I && rr < (isx ? B : O);
         const float* src = isx ? in : W;
         const float4 x = *reinterpret_cast<const float4*>(src + (ok ? rr * I + k : 0));
@@ -234,7 +234,7 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
     float4 r0[UV], r1[UV];
     load(0, r0);
     if (nch > 1) load(KCH, r1);
-    for (int64_t c = 0; c < nch; c += 2) {
+    for (int c = 0; c < nch; c += 2) {
       store(r0);
       lds_barrier();
       if (c + 2 < nch) load((c + 2) * KCH, r0);
@@ -249,13 +249,13 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
       }
     }
   } else {
-    for (int64_t kc0 = 0; kc0 < I; kc0 += KCH) {
+    for (int kc0 = 0; kc0 < I; kc0 += KCH) {
 #pragma unroll 4
       for (int i = tid; i < rows * KCH; i += NT) {
         const int row = i / KCH, kk = i % KCH;
-        const int64_t k = kc0 + kk;
+        const int k = kc0 + kk;
         const bool isx = row < rowsX;
-        const int64_t rr = isx ? row : row - rowsX;
+        const int rr = isx ? row : row - rowsX;
         const bool ok = k < I && rr < (isx ? B : O);
         const float* src = isx ? in : W;
         const float v = src[ok ? rr * I + k : 0];
@@ -268,7 +268,7 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
   }
   if (active)
     for (int e = 0; e < 16; ++e) {
-      const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
+      const int m = m0 + acc_row(e, lane), n = n0 + l31;
       if (m < B && n < O) lds[(r * B + m) * O + n] = acc[e];
     }
 }
@@ -283,31 +283,31 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
 //  * dX tile (NN: prev_delta += delta . W, k over the outputs): prev_delta
 //    is the forward pass's zeroed delta, so the chain starts from +0; the
 //    result goes to memory and to the LDS block `nxt` the next stage reads.
-__device__ __forceinline__ void dw_task(const float* sdel, int64_t m0, int64_t n0, int64_t B,
-                                        int64_t O, int64_t I, const float* lin, const float* dW,
+__device__ __forceinline__ void dw_task(const float* sdel, int m0, int n0, int B,
+                                        int O, int I, const float* lin, const float* dW,
                                         const float* W, bool upd, floatx16& acc, float (&wv)[16],
                                         int lane) {
   const int l31 = lane & 31, h = lane >> 5;
   for (int e = 0; e < 16; ++e) {
-    const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
+    const int m = m0 + acc_row(e, lane), n = n0 + l31;
     const bool ok = m < O && n < I;
-    const int64_t ix = ok ? m * I + n : 0;
+    const int ix = ok ? m * I + n : 0;
     const float c = dW[ix];
     acc[e] = ok ? c : 0.0f;
     wv[e] = upd ? W[ix] : 0.0f;
   }
-  const int64_t m = m0 + l31, n = n0 + l31;
+  const int m = m0 + l31, n = n0 + l31;
   const bool vm = m < O, vn = n < I;
-  const int64_t mc = vm ? m : 0, nc = vn ? n : 0;
+  const int mc = vm ? m : 0, nc = vn ? n : 0;
   const int steps = (int)((B + 1) / 2);
   constexpr int U = 8;
   for (int s = 0; s < steps; s += U) {
     float av[U], bv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t k = 2 * (int64_t)(s + u) + h;
+      const int k = 2 * (int)(s + u) + h;
       const bool ok = s + u < steps && k < B;
-      const int64_t kc = ok ? k : 0;
+      const int kc = ok ? k : 0;
       const float x = sdel[kc * O + mc], y = lin[kc * I + nc];
       av[u] = (ok && vm) ? x : 0.0f;
       bv[u] = (ok && vn) ? y : 0.0f;
@@ -319,13 +319,13 @@ __device__ __forceinline__ void dw_task(const float* sdel, int64_t m0, int64_t n
 }
 
 // weight update of one dW tile (ora_sgd_update's weight part) or its plain store
-__device__ __forceinline__ void dw_store(int64_t m0, int64_t n0, int64_t O, int64_t I, float* dW,
+__device__ __forceinline__ void dw_store(int m0, int n0, int O, int I, float* dW,
                                          float* W, bool upd, const floatx16& acc,
                                          const float (&wv)[16], float lrb, float wdec,
                                          float momentum, int lane) {
   const int l31 = lane & 31;
   for (int e = 0; e < 16; ++e) {
-    const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
+    const int m = m0 + acc_row(e, lane), n = n0 + l31;
     if (m < O && n < I) {
       if (upd) {
         const float dw = fmaf(wdec, wv[e], acc[e]);  // weight_updates.axpy(-decay*batch, W)
@@ -338,24 +338,24 @@ __device__ __forceinline__ void dw_store(int64_t m0, int64_t n0, int64_t O, int6
   }
 }
 
-__device__ __forceinline__ void dx_task(const float* sdel, int64_t m0, int64_t n0, int64_t B,
-                                        int64_t O, int64_t I, const float* W, float* prev,
+__device__ __forceinline__ void dx_task(const float* sdel, int m0, int n0, int B,
+                                        int O, int I, const float* W, float* prev,
                                         float* nxt, int lane) {
   const int l31 = lane & 31, h = lane >> 5;
   floatx16 acc;
   for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
-  const int64_t m = m0 + l31, n = n0 + l31;
+  const int m = m0 + l31, n = n0 + l31;
   const bool vm = m < B, vn = n < I;
-  const int64_t mc = vm ? m : 0, nc = vn ? n : 0;
+  const int mc = vm ? m : 0, nc = vn ? n : 0;
   const int steps = (int)((O + 1) / 2);
   constexpr int U = 8;
   for (int s = 0; s < steps; s += U) {
     float av[U], bv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int64_t k = 2 * (int64_t)(s + u) + h;
+      const int k = 2 * (int)(s + u) + h;
       const bool ok = s + u < steps && k < O;
-      const int64_t kc = ok ? k : 0;
+      const int kc = ok ? k : 0;
       const float x = sdel[mc * O + kc], y = W[kc * I + nc];
       av[u] = (ok && vm) ? x : 0.0f;
       bv[u] = (ok && vn) ? y : 0.0f;
@@ -365,7 +365,7 @@ __device__ __forceinline__ void dx_task(const float* sdel, int64_t m0, int64_t n
       if (s + u < steps) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[u], bv[u], acc, 0, 0, 0);
   }
   for (int e = 0; e < 16; ++e) {
-    const int64_t mm = m0 + acc_row(e, lane), nn = n0 + l31;
+    const int mm = m0 + acc_row(e, lane), nn = n0 + l31;
     if (mm < B && nn < I) {
       prev[mm * I + nn] = acc[e];
       nxt[mm * I + nn] = acc[e];
@@ -375,8 +375,8 @@ __device__ __forceinline__ void dx_task(const float* sdel, int64_t m0, int64_t n
 
 // every layer's dW/dX tasks fit one per wave: the weight update of layer l
 // is applied by its dW waves right after the stage's dX tasks are done
-__device__ __forceinline__ bool defer_update(int64_t B, int64_t O, int64_t I) {
-  const int64_t tmo = (O + 31) / 32, tni = (I + 31) / 32, tmb = (B + 31) / 32;
+__device__ __forceinline__ bool defer_update(int B, int O, int I) {
+  const int tmo = (O + 31) / 32, tni = (I + 31) / 32, tmb = (B + 31) / 32;
   return tmo * tni + tmb * tni <= NWAVES;
 }
 
@@ -390,9 +390,9 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   // back from memory.
   extern __shared__ float lds[];
   float* act = lds + a.act_off;
-  const int64_t B = a.batch;
+  const int B = a.batch;
   const int L = a.nlayers;
-  const int64_t C = a.widths[L];
+  const int C = a.widths[L];
   const int Bi = (int)B, Ci = (int)C;  // LDS-resident sizes: 9*B*max(O) <= 40960
   float* smx = a.buf + a.softmax_off;
   float* sm_out = smx;
@@ -402,35 +402,13 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   const float wdec = -a.decay * (float)B;
   const float mom = a.momentum;
 
-  // ---- L2 warm-up: one load per 128-byte line of layers 1.. (weights, their
-  // updates, the stored outputs read as 0*C, the per-channel vectors; the
-  // first 256 KB), issued before anything else so the lines the previous
-  // step's launch wrote (another XCD's L2, or memory) are in this XCD's L2
-  // when the stages read them.  Consumed after layer 0's partials are in LDS:
-  // those loads were issued later, so waiting for them already waited for
-  // these (loads complete in order)
-  constexpr int NWARM = 2;
-  float warmv[NWARM];
-#pragma unroll
-  for (int j = 0; j < NWARM; ++j) warmv[j] = 0.0f;
-#ifndef TNS_MLP_NO_WARM
-  if (L > 1) {
-    const int64_t lo = a.off[1][F_W], hi = a.softmax_off;
-#pragma unroll
-    for (int j = 0; j < NWARM; ++j) {
-      const int64_t i = lo + 32 * ((int64_t)threadIdx.x + (int64_t)j * NT);
-      warmv[j] = a.buf[i < hi ? i : lo];
-    }
-  }
-#endif
-
   // ---- forward ------------------------------------------------------------
   MLP_STAMP(0);
   const float* in = a.X;
   for (int l = 0; l < L; ++l) {
     const int tid = stage_tid(), wid = tid >> 6, lane = tid & 63;
     const Layer lay(a, l);
-    const int64_t I = lay.I, O = lay.O, BO = B * O;
+    const int I = lay.I, O = lay.O, BO = B * O;
     const int Oi = (int)O;
     float* out = lay.out();
     // ahead of the gemm: per element slot the stored C (beta = 0 still reads
@@ -459,7 +437,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     // gemm(RowMajor, NoTrans, Trans, B, O, I, 1, in, I, W, I, 0, out, O):
     // sdot_avx2 residue classes r = k mod 8, each an ascending MFMA chain
     const int tm = (int)((B + 31) / 32), tn = (int)((O + 31) / 32);
-    const int64_t kr = (I + 7) / 8;            // k values per residue class
+    const int kr = (I + 7) / 8;            // k values per residue class
     const int steps = (int)((kr + 1) / 2);
     if (l == 0) {
       // layer 0's partials come from mlp_l0_forward_kernel, in this layout
@@ -469,7 +447,6 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
       } else {
         for (int i = tid; i < (int)(8 * BO); i += NT) lds[i] = a.l0part[i];
       }
-      asm volatile("" ::"v"(warmv[0]), "v"(warmv[1]));  // (NWARM = 2)
     } else if (tm * tn * 8 <= NWAVES && a.lds_chunks) {
       if (I > 64)
         gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn, tid);
@@ -478,18 +455,18 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     } else
     for (int w = wid; w < tm * tn * 8; w += NWAVES) {
       const int r = w & 7, tile = w >> 3;
-      const int64_t m0 = (int64_t)(tile / tn) * 32, n0 = (int64_t)(tile % tn) * 32;
+      const int m0 = (int)(tile / tn) * 32, n0 = (int)(tile % tn) * 32;
       floatx16 acc;
       for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
       {
         const int l31 = lane & 31, h = lane >> 5;
-        const int64_t m = m0 + l31, n = n0 + l31, k0 = r + 8 * h;
+        const int m = m0 + l31, n = n0 + l31, k0 = r + 8 * h;
         // step s consumes k = r + 8*(2s + h) of residue class r
         mfma_chain(acc, steps, in + (m < B ? m : 0) * I + k0, 16, m < B,
                    lay.W() + (n < O ? n : 0) * I + k0, 16, n < O, k0, 16, I);
       }
       for (int e = 0; e < 16; ++e) {
-        const int64_t m = m0 + acc_row(e, lane), n = n0 + (lane & 31);
+        const int m = m0 + acc_row(e, lane), n = n0 + (lane & 31);
         if (m < B && n < O) lds[(r * B + m) * O + n] = acc[e];
       }
     }
@@ -641,7 +618,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   for (int l = L - 1; l >= 0; --l) {
     const int tid = stage_tid(), wid = tid >> 6, lane = tid & 63;
     const Layer lay(a, l);
-    const int64_t I = lay.I, O = lay.O, BO = B * O;
+    const int I = lay.I, O = lay.O, BO = B * O;
     const int Oi = (int)O;
     const float* lin = a.X;
     float* prev_delta = nullptr;
@@ -718,7 +695,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     // the double pow of meansAndVarsDelta depends on the forward variance
     // only: the last wave evaluates it for every channel while wave 0 runs
     // the chains (it was the longest single latency of the chain thread)
-    double* st_pw = reinterpret_cast<double*>(st + ((4 * O + 1) & ~(int64_t)1));
+    double* st_pw = reinterpret_cast<double*>(st + ((4 * O + 1) & ~(int)1));
     if (a.bn && wid == NWAVES - 1)
       for (int o = lane; o < Oi; o += 64) {
         const float var = lay.var()[o];
@@ -810,12 +787,12 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     // chains; layer 0 (no dX) updates its weights in the dW epilogue, other
     // layers after the stage's dX tasks (or in the pass after the backward)
     bool have = false;
-    int64_t hm0 = 0, hn0 = 0;
+    int hm0 = 0, hn0 = 0;
     floatx16 hacc;
     float hw[16];
     for (int w = wid; w < nw_dw + nw_dx; w += NWAVES) {
       if (w < nw_dw) {
-        const int64_t m0 = (int64_t)(w / tni) * 32, n0 = (int64_t)(w % tni) * 32;
+        const int m0 = (int)(w / tni) * 32, n0 = (int)(w % tni) * 32;
         dw_task(sdel, m0, n0, B, O, I, lin, lay.dW(), lay.W(), l == 0 || defer, hacc, hw, lane);
         if (l == 2) MLP_MARK(17);
         if (defer) {
@@ -827,7 +804,7 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         }
       } else {
         const int t = w - nw_dw;
-        const int64_t m0 = (int64_t)(t / tni) * 32, n0 = (int64_t)(t % tni) * 32;
+        const int m0 = (int)(t / tni) * 32, n0 = (int)(t % tni) * 32;
         dx_task(sdel, m0, n0, B, O, I, lay.W(), prev_delta, act, lane);
       }
     }
@@ -848,21 +825,21 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
     for (int l = 1; l < L; ++l) {
       const Layer lay(a, l);
       if (defer_update(B, lay.O, lay.I)) continue;
-      const int64_t IO = lay.I * lay.O;
+      const int IO = lay.I * lay.O;
       float* W = lay.W();
       float* dW = lay.dW();
       constexpr int UB = 8;
-      for (int64_t e0 = tid; e0 < IO; e0 += (int64_t)NT * UB) {
+      for (int e0 = tid; e0 < IO; e0 += (int)NT * UB) {
         float w[UB], g[UB];
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
-          const int64_t e = e0 + (int64_t)u * NT;
+          const int e = e0 + (int)u * NT;
           w[u] = W[e < IO ? e : e0];
           g[u] = dW[e < IO ? e : e0];
         }
 #pragma unroll
         for (int u = 0; u < UB; ++u) {
-          const int64_t e = e0 + (int64_t)u * NT;
+          const int e = e0 + (int)u * NT;
           if (e < IO) {
             const float dw = fmaf(wdec, w[u], g[u]);  // weight_updates.axpy(-decay*batch, W)
             W[e] = fmaf(lrb, dw, w[u]);               // weights.axpy(lr/batch, dW)
@@ -879,17 +856,17 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
   // tail (sm_loss was written before the full barrier after the softmax) ----
   const int wid = stage_tid() >> 6, lane = threadIdx.x & 63;
   if (wid == 0) {
-    const int64_t n = B * C, blocks = n >> 3;
+    const int n = B * C, blocks = n >> 3;
     float acc = 0.0f;
     if (lane < 8)
-      for (int64_t t = 0; t < blocks; ++t) acc = acc + sm_loss[8 * t + lane];
+      for (int t = 0; t < blocks; ++t) acc = acc + sm_loss[8 * t + lane];
     const float a0 = __shfl(acc, 0), a1 = __shfl(acc, 1), a2 = __shfl(acc, 2),
                 a3 = __shfl(acc, 3), a4 = __shfl(acc, 4), a5 = __shfl(acc, 5),
                 a6 = __shfl(acc, 6), a7 = __shfl(acc, 7);
     if (lane == 0) {
       const float s0 = a0 + a4, s1 = a1 + a5, s2 = a2 + a6, s3 = a3 + a7;
       float r = (s0 + s1) + (s2 + s3);
-      for (int64_t i = blocks * 8; i < n; ++i) r = r + sm_loss[i];
+      for (int i = blocks * 8; i < n; ++i) r = r + sm_loss[i];
       *a.cost = r;
     }
   }
