@@ -4,6 +4,7 @@
 #   diagtests — the variant sweeps against the ab/diag build (TNS_DIAG=1:
 #             the measured, not picked forms included)
 #   mlpst   — MNIST fused-step stage stamps (ab/mlpst: -DTNS_MLP_STAMPS)
+#   bnab    — BN reduction rates (bn_perf.py) for LIBS
 #   abfwd   — conv forward A/B: LIBS builds under ab/ (+ "main" = the tree)
 #   bwdab   — conv backward schedules (bwd_graph.py) for LIBS
 #   bench   — python bench.py (default flags) -> gpurun_out/bench.json
@@ -24,6 +25,16 @@ for S in ${STEPS}; do
     mlpst)
       TNS_LIB=ab/mlpst/libtensorium_hip.so timeout -k 10 120 python -u scripts/mlp_stamps.py > gpurun_out/mlp_stamps.log 2>&1
       rc=$?; grep -v amdgpu.ids gpurun_out/mlp_stamps.log; [ $rc -eq 0 ] || exit $rc ;;
+    bnab)
+      for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do
+        echo -n "{\"tag\": \"$L\", \"res\": " >> gpurun_out/bnab.jsonl
+        TNS_LIB=$(lib_of $L) timeout -k 10 300 python -u scripts/bn_perf.py >> gpurun_out/bnab.jsonl 2> gpurun_out/bnab_$L.err
+        rc=$?; echo "}" >> gpurun_out/bnab.jsonl; [ $rc -eq 0 ] || { echo "$L rc=$rc"; tail -5 gpurun_out/bnab_$L.err; exit $rc; }
+      done; done
+      python3 -c "
+import json
+for l in open('gpurun_out/bnab.jsonl'):
+    r=json.loads(l); d=r['res']['8x32x173056']; print(r['tag'], d['means_vars_ms'], d['add_sums_ms'], d['add_dots_ms'], d['means_vars_delta_ms'])" ;;
     abfwd)
       for r in $(seq 1 ${ROUNDS:-2}); do for L in ${LIBS}; do
         TNS_LIB=$(lib_of $L) timeout -k 10 300 python -u scripts/quick_perf.py --tag $L --yolo-only >> gpurun_out/abfwd.jsonl 2> gpurun_out/abfwd_$L.err

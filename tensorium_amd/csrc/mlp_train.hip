@@ -283,6 +283,7 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
 //  * dX tile (NN: prev_delta += delta . W, k over the outputs): prev_delta
 //    is the forward pass's zeroed delta, so the chain starts from +0; the
 //    result goes to memory and to the LDS block `nxt` the next stage reads.
+template <int U = 8>  // steps whose loads are issued together
 __device__ __forceinline__ void dw_task(const float* sdel, int m0, int n0, int B,
                                         int O, int I, const float* lin, const float* dW,
                                         const float* W, bool upd, floatx16& acc, float (&wv)[16],
@@ -300,7 +301,6 @@ __device__ __forceinline__ void dw_task(const float* sdel, int m0, int n0, int B
   const bool vm = m < O, vn = n < I;
   const int mc = vm ? m : 0, nc = vn ? n : 0;
   const int steps = (int)((B + 1) / 2);
-  constexpr int U = 8;
   for (int s = 0; s < steps; s += U) {
     float av[U], bv[U];
 #pragma unroll
@@ -707,6 +707,9 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
 #endif
       }
     auto chain = [&](int o, float db0, float b0, float ds0, float sc, float mu) {
+      // rows past the batch add +0.0f, selected off the chains (every chain
+      // starts at +0, so none is ever -0, and x + (+0) == x otherwise): the
+      // chains hold only their adds
       float r = 0.0f, dd = 0.0f, m = 0.0f, v = 0.0f;
       for (int b0r = 0; b0r < Bi; b0r += 8) {
         float cs[8], cn[8], cx[8];
@@ -720,15 +723,15 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         hold8(cs);
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          if (b0r + u < Bi) {
-            const float sv = cs[u];
-            r = r + sv;
-            if (a.bn) {
-              dd = dd + cn[u] * sv;
-              const float d = sv * sc;  // forwardScale
-              m = m + d;
-              v = v + (cx[u] - mu) * d;
-            }
+          const bool in = b0r + u < Bi;
+          const float sv = cs[u];
+          r = r + (in ? sv : 0.0f);
+          if (a.bn) {
+            const float d = sv * sc;  // forwardScale
+            const float pd = cn[u] * sv, pv = (cx[u] - mu) * d;
+            dd = dd + (in ? pd : 0.0f);
+            m = m + (in ? d : 0.0f);
+            v = v + (in ? pv : 0.0f);
           }
         }
       }
@@ -882,20 +885,48 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
 // block = one 32x32 output tile x 4 residue classes (one per wave); both
 // operands' tile rows staged through LDS in k-chunks of KCH, float4 loads two
 // chunks ahead; partial r of (m, n) to part[(r*B + m)*O + n].
-template <int KCH, int VEC>
+// NCMAX > 0 (I <= NCMAX*KCH): every chunk's loads issued at the start into
+// registers (the block moves ~200 KB through one CU; two chunks in flight
+// left it waiting on memory latency once per chunk), two LDS buffers, one
+// barrier per chunk.
+template <int KCH, int VEC, int NCMAX>
 __global__ __launch_bounds__(256) void mlp_l0_forward_kernel(const float* X, const float* W,
                                                              int64_t B, int64_t O, int64_t I,
                                                              float* part) {
   // VEC = 4: float4 units (16-byte rows); 1: single floats
   constexpr int KP = KCH + 1, QR = KCH / VEC, UV = (64 * QR + 255) / 256;
-  __shared__ float lds[64 * KP];
+  __shared__ float lds[(NCMAX > 0 ? 2 : 1) * 64 * KP];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, l31 = lane & 31, h = lane >> 5;
   const int tn = (int)((O + 31) / 32), tile = blockIdx.x >> 1;
   const int64_t m0 = (int64_t)(tile / tn) * 32, n0 = (int64_t)(tile % tn) * 32;
   const int r = 4 * (blockIdx.x & 1) + wid;
   floatx16 acc;
   for (int e = 0; e < 16; ++e) acc[e] = 0.0f;
+  // NCMAX forms: buffer loads, rows 8u..8u+7 of unit u are all X rows (u <
+  // 4) or all W rows, out-of-range units read 0 through an offset past the
+  // buffer (no select, so no branch around the load that would make the
+  // compiler wait between the loads)
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(X), 0, (int)(B * I * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(W), 0, (int)(O * I * 4), 0x00020000);
   auto load = [&](int64_t kc0, float4 (&v)[UV]) {
+    if constexpr (NCMAX > 0) {
+      static_assert(VEC == 4 && QR == 32 && UV == 8, "unit u = rows 8u .. 8u+7");
+#pragma unroll
+      for (int u = 0; u < UV; ++u) {
+        const int row = (tid >> 5) + 8 * u, kq = tid & 31;
+        const int64_t k = kc0 + 4 * kq;
+        const int64_t g = u < 4 ? m0 + row : n0 + row - 32;
+        const bool ok = k < I && g < (u < 4 ? B : O);
+        const unsigned off = ok ? (unsigned)((g * I + k) * 4) : 0x80000000u;
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const u4 x = __builtin_amdgcn_raw_buffer_load_b128(u < 4 ? rx : rw, off, 0, 0);
+        v[u] = make_float4(__uint_as_float(x.x), __uint_as_float(x.y), __uint_as_float(x.z),
+                           __uint_as_float(x.w));
+      }
+      return;
+    }
 #pragma unroll
     for (int u = 0; u < UV; ++u) {
       const int idx = tid + u * 256;
@@ -914,12 +945,12 @@ __global__ __launch_bounds__(256) void mlp_l0_forward_kernel(const float* X, con
       }
     }
   };
-  auto store = [&](const float4 (&v)[UV]) {
+  auto store = [&](const float4 (&v)[UV], int buf = 0) {
 #pragma unroll
     for (int u = 0; u < UV; ++u) {
       const int idx = tid + u * 256;
       if (idx < 64 * QR) {
-        float* d = lds + (idx / QR) * KP + VEC * (idx % QR);
+        float* d = lds + buf * 64 * KP + (idx / QR) * KP + VEC * (idx % QR);
         d[0] = v[u].x;
         if constexpr (VEC == 4) {
           d[1] = v[u].y; d[2] = v[u].z; d[3] = v[u].w;
@@ -927,15 +958,32 @@ __global__ __launch_bounds__(256) void mlp_l0_forward_kernel(const float* X, con
       }
     }
   };
-  auto compute = [&]() {
+  auto compute = [&](int buf = 0) {
+    const float* L = lds + buf * 64 * KP;
 #pragma unroll
     for (int st = 0; st < KCH / 16; ++st) {  // k = kc0 + r + 8*(2*st + h)
       const int kk = r + 8 * (2 * st + h);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(lds[l31 * KP + kk], lds[(32 + l31) * KP + kk],
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(L[l31 * KP + kk], L[(32 + l31) * KP + kk],
                                                  acc, 0, 0, 0);
     }
   };
   const int64_t nch = (I + KCH - 1) / KCH;
+  if constexpr (NCMAX > 0) {
+    // (chunks past the last load zeros from clamped addresses: no branch
+    // between the loads, so the waits before each store count exactly)
+    float4 rr[NCMAX][UV];
+#pragma unroll
+    for (int c = 0; c < NCMAX; ++c) load((int64_t)c * KCH, rr[c]);
+    asm volatile("" ::: "memory");  // (keeps every load above the first store)
+#pragma unroll
+    for (int c = 0; c < NCMAX; ++c) {
+      if (c < nch) {
+        store(rr[c], c & 1);
+        __syncthreads();  // (also: every wave is past compute(c - 2) of this buffer)
+        compute(c & 1);
+      }
+    }
+  } else {
   float4 r0[UV], r1[UV];
   load(0, r0);
   if (nch > 1) load(KCH, r1);
@@ -952,6 +1000,7 @@ __global__ __launch_bounds__(256) void mlp_l0_forward_kernel(const float* X, con
       compute();
       __syncthreads();
     }
+  }
   }
   for (int e = 0; e < 16; ++e) {
     const int64_t m = m0 + acc_row(e, lane), n = n0 + l31;
@@ -971,7 +1020,7 @@ __global__ __launch_bounds__(64) void mlp_l0_dw_kernel(const float* delta, const
   const int64_t m0 = (int64_t)(blockIdx.x / tni) * 32, n0 = (int64_t)(blockIdx.x % tni) * 32;
   floatx16 acc;
   float wv[16];
-  dw_task(delta, m0, n0, B, O, I, X, dW, W, true, acc, wv, lane);
+  dw_task<16>(delta, m0, n0, B, O, I, X, dW, W, true, acc, wv, lane);  // (B <= 32: one batch)
   dw_store(m0, n0, O, I, dW, W, true, acc, wv, lrb, wdec, momentum, lane);
 }
 
@@ -1053,11 +1102,17 @@ hipError_t launch_mlp_train_step(const MlpArgs& args, hipStream_t s) {
   const bool vec0 = I0 % 4 == 0 && ((reinterpret_cast<uintptr_t>(a.X) |
                                      reinterpret_cast<uintptr_t>(W0)) & 15) == 0;
   const unsigned fblocks = (unsigned)(2 * ((B0 + 31) / 32) * ((O0 + 31) / 32));
+#ifndef TNS_MLP_L0_TWO
+  if (vec0 && I0 <= 8 * 128)
+    hipLaunchKernelGGL((mlp_l0_forward_kernel<128, 4, 8>), dim3(fblocks), dim3(256), 0, s, a.X,
+                       W0, B0, O0, I0, a.l0part);
+  else
+#endif
   if (vec0)
-    hipLaunchKernelGGL((mlp_l0_forward_kernel<128, 4>), dim3(fblocks), dim3(256), 0, s, a.X, W0,
+    hipLaunchKernelGGL((mlp_l0_forward_kernel<128, 4, 0>), dim3(fblocks), dim3(256), 0, s, a.X, W0,
                        B0, O0, I0, a.l0part);
   else
-    hipLaunchKernelGGL((mlp_l0_forward_kernel<64, 1>), dim3(fblocks), dim3(256), 0, s, a.X, W0,
+    hipLaunchKernelGGL((mlp_l0_forward_kernel<64, 1, 0>), dim3(fblocks), dim3(256), 0, s, a.X, W0,
                        B0, O0, I0, a.l0part);
   if (hipError_t e = hipGetLastError(); e != hipSuccess) return e;
   if (blk <= EPT_S * NT)
