@@ -894,8 +894,15 @@ __global__ __launch_bounds__(256) void mlp_l0_forward_kernel(const float* X, con
                                                              int64_t B, int64_t O, int64_t I,
                                                              float* part) {
   // VEC = 4: float4 units (16-byte rows); 1: single floats
-  constexpr int KP = KCH + 1, QR = KCH / VEC, UV = (64 * QR + 255) / 256;
-  __shared__ float lds[(NCMAX > 0 ? 2 : 1) * 64 * KP];
+  // NCMAX forms: rows padded to KCH + 4 (16-byte aligned: one ds_write_b128 a
+  // unit; the fragment reads then meet two lanes a bank); else KCH + 1
+#ifdef TNS_MLP_L0_KP1
+  constexpr int KP = KCH + 1;
+#else
+  constexpr int KP = NCMAX > 0 ? KCH + 4 : KCH + 1;
+#endif
+  constexpr int QR = KCH / VEC, UV = (64 * QR + 255) / 256;
+  __shared__ __attribute__((aligned(16))) float lds[(NCMAX > 0 ? 2 : 1) * 64 * KP];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, l31 = lane & 31, h = lane >> 5;
   const int tn = (int)((O + 31) / 32), tile = blockIdx.x >> 1;
   const int64_t m0 = (int64_t)(tile / tn) * 32, n0 = (int64_t)(tile % tn) * 32;
@@ -951,6 +958,10 @@ __global__ __launch_bounds__(256) void mlp_l0_forward_kernel(const float* X, con
       const int idx = tid + u * 256;
       if (idx < 64 * QR) {
         float* d = lds + buf * 64 * KP + (idx / QR) * KP + VEC * (idx % QR);
+        if constexpr (VEC == 4 && KP % 4 == 0) {
+          *reinterpret_cast<float4*>(d) = v[u];
+          continue;
+        }
         d[0] = v[u].x;
         if constexpr (VEC == 4) {
           d[1] = v[u].y; d[2] = v[u].z; d[3] = v[u].w;
