@@ -62,3 +62,8 @@ bw = {11: "B1 done", 12: "after barrier", 13: "chains done", 14: "after barrier"
 print("backward stage 2:")
 for i in range(11, 20):
     print(f"  {bw[i]:20s} {mk(i) - mk(i - 1):8d}")
+gm = {20: "gemm: start", 21: "operand loads issued", 22: "stored to LDS", 23: "after barrier",
+      24: "MFMAs issued", 25: "after barrier", 26: "partials stored"}
+print("forward layer 1 gemm (wave 0, cycles since the layer's mark 0):")
+for i in range(20, 27):
+    print(f"  {gm[i]:22s} {mk(i) - mk(0):8d}")

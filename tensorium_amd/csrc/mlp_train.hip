@@ -177,9 +177,19 @@ __device__ __forceinline__ int stage_tid() {
 // registers, so a chunk's global latency overlaps the MFMAs of the previous
 // two.  The chunks alias the partial-sum region: every wave has passed the
 // barrier after the last chunk before any partial is written.
+// gmark: diagnostic stamps (wave 0's clock at its sub-steps; nullptr in the
+// product, folded away)
+__device__ __forceinline__ void gmark(unsigned* st, int i) {
+  if (st && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    st[2 * i] = (unsigned)t;
+    st[2 * i + 1] = (unsigned)(t >> 32);
+  }
+}
 template <int KCH>
 __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const float* W, int B,
-                                             int O, int I, int tm, int tn, int tid) {
+                                             int O, int I, int tm, int tn, int tid,
+                                             unsigned* st = nullptr) {
   constexpr int KP = KCH + 1;  // LDS row: an odd stride for the lanes' row reads
   constexpr int QR = KCH / 4;  // float4 units per staged row
   constexpr int UV = (3 * 32 * QR + NT - 1) / NT;  // units per thread (tm + tn <= 3)
@@ -232,14 +242,20 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
       }
     };
     float4 r0[UV], r1[UV];
+    gmark(st, 20);
     load(0, r0);
     if (nch > 1) load(KCH, r1);
+    gmark(st, 21);
     for (int c = 0; c < nch; c += 2) {
       store(r0);
+      gmark(st, 22);
       lds_barrier();
+      gmark(st, 23);
       if (c + 2 < nch) load((c + 2) * KCH, r0);
       compute();
+      gmark(st, 24);
       lds_barrier();
+      gmark(st, 25);
       if (c + 1 < nch) {
         store(r1);
         lds_barrier();
@@ -270,7 +286,7 @@ __device__ __forceinline__ void gemm_chunked(float* lds, const float* in, const 
     for (int e = 0; e < 16; ++e) {
       const int m = m0 + acc_row(e, lane), n = n0 + l31;
       if (m < B && n < O) lds[(r * B + m) * O + n] = acc[e];
-    }
+    }  gmark(st, 26);
 }
 
 // Backward gemm tasks of one wave (32x32 output tiles, ascending FMA chains
@@ -448,10 +464,15 @@ __global__ __launch_bounds__(NT) void mlp_train_kernel(MlpArgs a) {
         for (int i = tid; i < (int)(8 * BO); i += NT) lds[i] = a.l0part[i];
       }
     } else if (tm * tn * 8 <= NWAVES && a.lds_chunks) {
+#ifdef TNS_MLP_STAMPS
+      unsigned* gst = l == 1 ? reinterpret_cast<unsigned*>(a.buf + a.stamp_off) + 128 : nullptr;
+#else
+      unsigned* gst = nullptr;
+#endif
       if (I > 64)
-        gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn, tid);
+        gemm_chunked<128>(lds, in, lay.W(), B, O, I, tm, tn, tid, gst);
       else
-        gemm_chunked<64>(lds, in, lay.W(), B, O, I, tm, tn, tid);
+        gemm_chunked<64>(lds, in, lay.W(), B, O, I, tm, tn, tid, gst);
     } else
     for (int w = wid; w < tm * tn * 8; w += NWAVES) {
       const int r = w & 7, tile = w >> 3;
