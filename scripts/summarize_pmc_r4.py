@@ -83,8 +83,28 @@ def main():
     shapes = {str(L): f"{T[L].c}x{T[L].h} k{T[L].size}s{T[L].stride}->{T[L].filters}" for L in layers}
     fwd = {"note": note, "shapes": shapes, "layers": summarise(src, "fwd", layers)}
     bwd = {"note": note, "shapes": shapes, "layers": summarise(src, "bwd", layers)}
-    (ROOT / "profiles" / "r04_conv_tile4_pmc.json").write_text(json.dumps(fwd, indent=1) + "\n")
-    (ROOT / "profiles" / "r04_conv_bwd_pmc.json").write_text(json.dumps(bwd, indent=1) + "\n")
+    tag = sys.argv[3] if len(sys.argv) > 3 else "r04"
+    if tag == "r04":
+        (ROOT / "profiles" / "r04_conv_tile4_pmc.json").write_text(json.dumps(fwd, indent=1) + "\n")
+        (ROOT / "profiles" / "r04_conv_bwd_pmc.json").write_text(json.dumps(bwd, indent=1) + "\n")
+    else:  # later rounds: one file, plus the SQ pass over the 4096^3 SGEMM if present
+        out = {"note": note.replace("gpu_r4_evidence", f"gpu_{tag[0]}{tag[2:]}_evidence"),
+               "shapes": shapes, "conv_fwd": fwd["layers"], "conv_bwd": bwd["layers"]}
+        if (src / "sgemm_sq").exists():
+            sg = {}
+            for k, cs in per_dispatch(src / "sgemm_sq").items():
+                m = {c: st.mean(v) for c, v in cs.items()}
+                e = {"dispatches": len(next(iter(cs.values()))),
+                     "counters": {c: round(v, 1) for c, v in m.items()}}
+                if m.get("GRBM_GUI_ACTIVE"):
+                    e["mfma_busy"] = round(m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) /
+                                           (1024 * m["GRBM_GUI_ACTIVE"] / 8.0), 4)
+                if m.get("SQ_INSTS_LDS"):
+                    e["lds_bank_conflict_per_lds_inst"] = round(
+                        m.get("SQ_LDS_BANK_CONFLICT", 0) / m["SQ_INSTS_LDS"], 4)
+                sg[k] = e
+            out["sgemm_4096_sq"] = sg
+        (ROOT / "profiles" / f"{tag}_pmc.json").write_text(json.dumps(out, indent=1) + "\n")
     for L in layers:
         for k, e in fwd["layers"][str(L)].items():
             print("fwd", L, k[:70], e.get("mfma_busy"), e.get("fetch_bytes"), e.get("write_bytes"))
