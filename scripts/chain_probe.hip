@@ -38,6 +38,60 @@ __global__ void chain(float* out, unsigned long long* cyc, int lanes, float x) {
   if (l == 0) cyc[0] = t1 - t0;
 }
 
+// ring: the same chain fed from LDS the way block_chains_ws feeds it (rows
+// of 768 terms, groups of 16 read by four ds_read_b128 three groups ahead,
+// s_waitcnt lgkmcnt(8) before each group), no other wave on the CU
+constexpr int RLDT = 840, RTERMS = 768, RREPS = 64;
+__global__ void ring(float* out, unsigned long long* cyc, int lanes, float x) {
+  __shared__ __attribute__((aligned(16))) float U[8 * RLDT];
+  const int l = threadIdx.x;
+  for (int i = l; i < 8 * RLDT; i += 64) U[i] = x * (float)(i & 7);
+  __syncthreads();
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  float acc = 0.f;
+  const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(U + (l & 7) * RLDT);
+  auto rd = [&](int q, f4 (&v)[4]) {
+    const unsigned a = base + 4u * (unsigned)q;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v[0]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(v[1]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(v[2]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(v[3]) : "v"(a));
+  };
+  auto wait8 = [&](f4 (&v)[4]) {
+    asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+  };
+  auto add16 = [&](const f4 (&v)[4]) {
+#pragma unroll
+    for (int z = 0; z < 16; ++z) acc = acc + v[z >> 2][z & 3];
+  };
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  if (l < lanes) {
+    for (int r = 0; r < RREPS; ++r) {
+      f4 va[4], vb[4], vc[4];
+      rd(0, va);
+      rd(16, vb);
+      rd(32, vc);
+      for (int q = 0; q < RTERMS; q += 48) {
+        wait8(va);
+        add16(va);
+        rd((q + 48) % RTERMS, va);
+        wait8(vb);
+        add16(vb);
+        rd((q + 64) % RTERMS, vb);
+        wait8(vc);
+        add16(vc);
+        rd((q + 80) % RTERMS, vc);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(va[3]),
+                   "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]), "+v"(vc[0]), "+v"(vc[1]),
+                   "+v"(vc[2]), "+v"(vc[3]));
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[l] = acc;
+  if (l == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
   float* out;
   unsigned long long* cyc;
@@ -56,6 +110,14 @@ int main() {
   run("chain1", chain<1>, 64, 1);
   run("chain2", chain<2>, 8, 2);
   run("chain4", chain<4>, 8, 4);
+  {
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(ring, dim3(1), dim3(64), 0, 0, out, cyc, 8, 1e-3f);
+    unsigned long long c = 0;
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("{\"kernel\": \"ring (ws feed)\", \"lanes\": 8, \"cycles_per_dependent_add\": %.2f}\n",
+           (double)c / (RREPS * RTERMS));
+  }
   (void)hipFree(out);
   (void)hipFree(cyc);
   return 0;
