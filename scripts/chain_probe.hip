@@ -92,6 +92,70 @@ __global__ void ring(float* out, unsigned long long* cyc, int lanes, float x) {
   if (l == 0) cyc[0] = t1 - t0;
 }
 
+// ring16: lanes 8..15 read the chain lanes' next four terms of every group
+// (one ds_read_b128 carries 8 terms of each chain), handed over by a DPP
+// row_ror:8 move off the chain: twice the terms in flight per LDS
+// instruction for four extra (independent) VALU moves per 8 adds
+__global__ void ring16(float* out, unsigned long long* cyc, int lanes, float x) {
+  __shared__ __attribute__((aligned(16))) float U[8 * RLDT];
+  const int l = threadIdx.x;
+  for (int i = l; i < 8 * RLDT; i += 64) U[i] = x * (float)(i & 7);
+  __syncthreads();
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  float acc = 0.f;
+  const int half = (l >> 3) & 1;
+  const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)(U + (l & 7) * RLDT) + 16u * half;
+  // group of 16 terms: lane l reads q..q+3 and q+8..q+11, lane l+8 reads
+  // q+4..q+7 and q+12..q+15
+  auto rd = [&](int q, f4 (&v)[2]) {
+    const unsigned a = base + 4u * (unsigned)q;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v[0]) : "v"(a));
+    asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(v[1]) : "v"(a));
+  };
+  auto wait = [&](f4 (&v)[2]) {
+    asm volatile("s_waitcnt lgkmcnt(10)" : "+v"(v[0]), "+v"(v[1]));
+  };
+  auto add16 = [&](const f4 (&v)[2]) {
+    float o[8];
+#pragma unroll
+    for (int z = 0; z < 8; ++z)
+      o[z] = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(
+                 0, __builtin_bit_cast(int, (float)v[z >> 2][z & 3]), 0x128, 0xf, 0xf, false));
+    // (the moves stay moves: folded into the adds as DPP operands they would
+    // sit on the chain)
+    asm volatile("" : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]),
+                 "+v"(o[6]), "+v"(o[7]));
+#pragma unroll
+    for (int z = 0; z < 4; ++z) acc = acc + v[0][z];
+#pragma unroll
+    for (int z = 0; z < 4; ++z) acc = acc + o[z];
+#pragma unroll
+    for (int z = 0; z < 4; ++z) acc = acc + v[1][z];
+#pragma unroll
+    for (int z = 0; z < 4; ++z) acc = acc + o[4 + z];
+  };
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  if (l < 16) {
+    for (int r = 0; r < RREPS; ++r) {
+      f4 g[6][2];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) rd(16 * i, g[i]);
+      for (int q = 0; q < RTERMS; q += 96) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          wait(g[i]);
+          add16(g[i]);
+          rd((q + 96 + 16 * i) % RTERMS, g[i]);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[l] = acc;
+  if (l == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
   float* out;
   unsigned long long* cyc;
@@ -116,6 +180,14 @@ int main() {
     (void)hipDeviceSynchronize();
     (void)hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
     printf("{\"kernel\": \"ring (ws feed)\", \"lanes\": 8, \"cycles_per_dependent_add\": %.2f}\n",
+           (double)c / (RREPS * RTERMS));
+  }
+  {
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(ring16, dim3(1), dim3(64), 0, 0, out, cyc, 16, 1e-3f);
+    unsigned long long c = 0;
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(&c, cyc, sizeof(c), hipMemcpyDeviceToHost);
+    printf("{\"kernel\": \"ring16 (reader lanes + DPP)\", \"lanes\": 16, \"cycles_per_dependent_add\": %.2f}\n",
            (double)c / (RREPS * RTERMS));
   }
   (void)hipFree(out);
