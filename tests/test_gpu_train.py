@@ -292,6 +292,7 @@ def test_fused_mlp_train_step(hip, torch_cuda, ora, bn, steps):
     ([101, 37, 70, 24, 10], [9, 0, 6, 4], 20),   # odd widths: scalar staging, 3-tile fallback gemm
     ([64, 48, 33, 10], [1, 13, 4], 40),          # two batch tiles, hardtan
     ([784, 64, 10], [1, 4], 2),                  # smallest batch
+    ([1200, 40, 10], [1, 4], 8),                 # layer 0 past 8 k-chunks: two chunks in flight
 ])
 @pytest.mark.parametrize("bn", [0, 1])
 def test_fused_mlp_irregular_shapes(hip, torch_cuda, ora, widths, acts, B, bn):
