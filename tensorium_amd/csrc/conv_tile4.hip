@@ -1311,7 +1311,10 @@ const char* conv_tile4_ta_name(int v) { return v >= 0 && v < kNumTiles4T ? kTile
 // state.delta in the epilogue) 128 x 48 on the 13^2 planes (0.087 -> 0.080)
 // and 64 x 64 on the 26^2 / 52^2 ones (0.079 -> 0.075 at 26^2).
 int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K, int64_t ks) {
-#ifdef TNS_CT4_TA_PF  // (A/B: the 13^2 planes on the PF twin of 7)
+#ifndef TNS_CT4_TA_NO_PF
+  // the 13^2 planes (N < 4096) on the PF twin of 7: whole pipelined backward
+  // 14.80 -> 14.66 ms, joined 17.13 -> 17.11 (scripts/bwd_graph.py, same box,
+  // two rounds; profiles/r05_bwd_schedules.json)
   if (N < 4096 && K % 32 == 0 && M % 64 == 0) return 12;
 #endif
   if (ks == 1) {
