@@ -25,6 +25,10 @@ Extra fields on the single JSON line:
                  (BASELINE configs[2]); images/s over all ranks.
   yolo_network — the whole YOLOv3-416 network (convolutions chained through
                  shortcut / route / upsample / yolo layers), batch 8 per GPU.
+  yolo_conv_backward  — the 75 conv layers' backward (no BN) back to back.
+  yolo_train_backward — TNet.backward over the whole network as the drop-in
+                 runs it in training (BN conv layers, shortcut / route /
+                 upsample / yolo backward calls between them).
 """
 from __future__ import annotations
 
@@ -539,6 +543,82 @@ def bench_conv_backward(torch, hip, ctx, rank, steps=2):
             "telemetry_split": split}
 
 
+def bench_train_backward(torch, hip, ctx, steps=3):
+    """The backward the drop-in runs in YOLOv3-416 training, batch 8:
+    TNet.backward over all 107 layers in the reference's order
+    (darknet.HipDarknetTrain: the 72 batch-normalized conv layers on
+    tns_hip_conv_backward_bn — Derivative, addDots, forwardScale,
+    MeansAndVarsDelta, normalizeDelta, dW, state.delta — the 3 heads on
+    tns_hip_conv_backward, each shortcut's DeriveArray + two addvv, the
+    routes' addvv, the upsamples' accumulation and the yolo layers' axpy),
+    after one training forward (BN statistics of the batch) with synthetic
+    yolo deltas (the yolo loss is out of scope).  Each pass starts from the
+    same deltas (reset outside the timed region); wall time from the first
+    call to a device synchronize after the last, pipelined (the Pascal
+    binding's default) and joined."""
+    from tensorium_amd import darknet as dn
+    net = dn.Network(dn.parse_cfg(dn.yolov3_cfg(416)), 8)
+    model = dn.HipDarknetTrain(hip, net, dn.random_params(net, seed=3), torch)
+    x = synthetic(torch, (8, 3, 416, 416), 7 * 100000 + ctx.rank, 0.0, 1.0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    model.forward(x)
+    torch.cuda.synchronize()
+    fwd_ms = (time.perf_counter() - t0) * 1e3
+    ys = [l for l in net.layers if l.kind == "yolo"]
+    yd = [synthetic(torch, (8 * l.out_size,), 7 * 200000 + l.index, -0.1, 0.1) for l in ys]
+
+    def reset():
+        hip.finish()
+        for d in model.delta:
+            d.zero_()
+        model.set_yolo_deltas(yd)
+        torch.cuda.synchronize()
+
+    def timed(mode):
+        hip.setBwdOverlap(mode)
+        reset()
+        model.backward(x)          # (warm: scratch sized, k-tables built)
+        ts = []
+        for _ in range(steps):
+            reset()
+            ctx.barrier()
+            t0 = time.perf_counter()
+            model.backward(x)
+            hip.finish()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return ctx.max(float(np.mean(ts)))
+
+    joined = timed(1)
+    piped = timed(2)
+    # which calls drained the pipeline (untimed pass: a ctypes query per layer)
+    reset()
+    trace = []
+    model.backward(x, lambda l: trace.append((l.index, l.kind, hip.pendingDw())))
+    hip.finish()
+    hip.setBwdOverlap(1)
+    drains = [(i, k) for (i, k, n), (_, _, m) in zip(trace[1:], trace[:-1])
+              if n < m and k != "convolutional"]
+    convs = net.convs()
+    gflop = sum(2 * l.filters * l.out_h * l.out_w * l.c * l.size * l.size * (2 if l.index else 1)
+                for l in convs) * 8 / 1e9
+    del model
+    torch.cuda.empty_cache()
+    return {"layers": len(net.layers), "conv_layers": len(convs),
+            "bn_conv_layers": sum(1 for l in convs if l.bn), "batch_per_gpu": 8,
+            "ms_per_batch": round(piped * 1e3, 3), "ms_per_batch_joined": round(joined * 1e3, 3),
+            "conv_gflop_per_batch": round(gflop, 2),
+            "tflops_conv": round(gflop / piped / 1e3, 2),
+            "images_per_s_total": round(ctx.world * 8 / piped, 1),
+            "training_forward_ms": round(fwd_ms, 3),
+            "max_pending_dw": max(n for _, _, n in trace),
+            "non_conv_calls_that_joined": drains,
+            "schedule": "pipelined (TNS_OPT_BWD_OVERLAP = 2, pascal/nnHip.pas initHIP default); "
+                        "ms_per_batch_joined: 1 (each call joined before it returns)",
+            "data": "synthetic input, random-init parameters, synthetic yolo deltas U[-0.1,0.1)"}
+
+
 def bench_yolo_network(torch, hip, ctx, steps):
     """The whole YOLOv3-416 network (yolov3.cfg plan: 75 convolutions chained
     through shortcut / route / upsample / yolo, darknet.HipDarknet), batch 8
@@ -779,6 +859,9 @@ def main():
     conv_bwd = None
     if not args.no_yolo and args.yolo_steps > 0:
         conv_bwd = bench_conv_backward(torch, hip, ctx, rank)
+    train_bwd = None
+    if not args.no_yolo and args.yolo_steps > 0:
+        train_bwd = bench_train_backward(torch, hip, ctx)
     ew = None if args.no_yolo else bench_elementwise_roofline(torch, hip)
     yolo_dp = None
     if not args.no_yolo and args.yolo_steps > 0:
@@ -839,6 +922,7 @@ def main():
             "yolo": yolo,
             "yolo_network": yolo_net,
             "yolo_conv_backward": conv_bwd,
+            "yolo_train_backward": train_bwd,
             "yolo_dp": yolo_dp,
             "config1_matmul": config1,
             "batched_gemm": batched,

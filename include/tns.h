@@ -146,7 +146,11 @@ int  tns_hip_set_stream(tns_ctx* ctx, void* hipStream);   /* hipStream_t */
 /* The context's stream, after it has been made to wait for any pipelined
  * conv-backward dW products still pending on the side stream
  * (TNS_OPT_BWD_OVERLAP = 2), so work enqueued on it sees their results. */
-void* tns_hip_get_stream(tns_ctx* ctx);
+void* tns_hip_get_stream(tns_ctx* ctx);   /* NULL on error: tns_last_error() */
+/* Pipelined conv backward (TNS_OPT_BWD_OVERLAP = 2): the number of dW
+ * products still pending on the side stream (0 once joined; -1 for a null
+ * context).  Diagnostic: it shows which calls left the pipeline running. */
+int  tns_hip_pending_dw(tns_ctx* ctx);
 int  tns_hip_finish(tns_ctx* ctx);                         /* nncuda.pas:1575 */
 
 /* createDeviceBuffer / freeDeviceBuffer / writeBuffer / readBuffer —
@@ -593,18 +597,31 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * caller's workspace instead of failing.  Set 0 to bound the backward's
  * memory to the workspace.  2 = pipelined: each call enqueues its dW on the
  * side stream (behind the earlier calls' dW) and returns without joining it;
- * the next call of ANY other entry point (and tns_hip_finish) first makes the
- * context's stream wait for the side stream.  The dW of layer L then runs
- * under the following calls' derive / state.delta work; a later backward
- * call that writes into a pending dW's delta or input waits for that dW
- * first.  The caller must not read or modify a pending call's weight_updates,
- * nor modify its input or delta, by other means (work enqueued on the stream
- * outside this API, or host accesses) before a join: tns_hip_finish, any
- * other entry point, or tns_hip_get_stream (which joins before it hands the
- * stream out, so work the caller then enqueues on it is ordered after every
- * pending dW).  Same results; state.delta always gets its own col buffer
+ * a later call whose operands meet a pending dW's (below), tns_hip_finish and
+ * tns_hip_get_stream first make the context's stream wait for the side
+ * stream.  The dW of layer L then runs under the following calls' derive /
+ * state.delta work and the non-conv layers' calls between them; a later
+ * backward call that writes into a pending dW's delta or input waits for that
+ * dW first.  The caller must not read or modify a pending call's
+ * weight_updates, nor modify its input or delta, by other means (work
+ * enqueued on the stream outside this API, or host accesses) before a join:
+ * tns_hip_finish, an entry point whose operands include them, or
+ * tns_hip_get_stream (which joins before it hands the stream out, so work the
+ * caller then enqueues on it is ordered after every pending dW).  Same results; state.delta always gets its own col buffer
  * (the memory note above).  pascal/nnHip.pas initHIP selects this mode by
  * default (pipelineBackward = true): there every access goes through the API.
+ * Since round 6 no entry point joins unconditionally during a pipelined
+ * pass: the non-conv ones (gemm, im2col / col2im, bias, activation, BLAS-1,
+ * addvv & co, shortcut, upsample, yolo, batch norm, softmax, sgd_update)
+ * join only when they write a pending dW's delta or input, read or write its
+ * weight_updates (or the caller's workspace that dW's im2col fills), or take
+ * a context scratch slot the side stream still uses — so TNet.backward's
+ * shortcut / route / upsample calls between two conv layers keep the
+ * pipeline running.  Context management, host copies, gemmBatched, the conv
+ * forward drivers and the fused train step still join.
+ * TNS_OPT_SCRATCH_CAP (default 0 = none): largest context scratch buffer in
+ * floats; a larger request fails as a failed allocation does (tests reach the
+ * fallback paths with it).
  * TNS_OPT_DERIVE_SUMS (default 0): 1 = the conv backward's Derivative and
  * addSums (no batch norm) in one pass where the sums' chain kernel applies
  * (planes under 16384 pixels); 0 = two passes (measured level: 15.06 vs
@@ -614,7 +631,7 @@ enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,
        TNS_OPT_DW_TILE = 9, TNS_OPT_BWD_OVERLAP = 10, TNS_OPT_DX_CONV = 11,
-       TNS_OPT_DW_RES = 12, TNS_OPT_DERIVE_SUMS = 13 };
+       TNS_OPT_DW_RES = 12, TNS_OPT_DERIVE_SUMS = 13, TNS_OPT_SCRATCH_CAP = 14 };
 int tns_set_option(int32_t opt, int64_t value);
 
 #ifdef __cplusplus

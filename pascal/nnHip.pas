@@ -65,6 +65,7 @@ const
   TNS_OPT_DX_CONV = 11;
   TNS_OPT_DW_RES = 12;
   TNS_OPT_DERIVE_SUMS = 13;
+  TNS_OPT_SCRATCH_CAP = 14;
 
 type
   PTnsCtx = pointer;
@@ -108,6 +109,7 @@ function tns_hip_create(deviceIndex: longint; ctx: PPTnsCtx): longint; cdecl; ex
 function tns_hip_destroy(ctx: PTnsCtx): longint; cdecl; external libtns;
 function tns_hip_set_stream(ctx: PTnsCtx; hipStream: pointer): longint; cdecl; external libtns;
 function tns_hip_get_stream(ctx: PTnsCtx): pointer; cdecl; external libtns;
+function tns_hip_pending_dw(ctx: PTnsCtx): longint; cdecl; external libtns;
 function tns_hip_finish(ctx: PTnsCtx): longint; cdecl; external libtns;
 function tns_hip_malloc(ctx: PTnsCtx; nElements: int64; res: PHipMem): longint; cdecl; external libtns;
 function tns_hip_free(ctx: PTnsCtx; p: THipMem): longint; cdecl; external libtns;

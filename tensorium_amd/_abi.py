@@ -38,6 +38,7 @@ TNS_OPT_BWD_OVERLAP = 10
 TNS_OPT_DX_CONV = 11
 TNS_OPT_DW_RES = 12
 TNS_OPT_DERIVE_SUMS = 13
+TNS_OPT_SCRATCH_CAP = 14
 
 _CONV = [i64] * 11  # aChannels .. dilationX
 
@@ -62,6 +63,7 @@ PROTOTYPES: dict[str, tuple] = {
     "tns_hip_destroy": (C.c_int, [vp]),
     "tns_hip_set_stream": (C.c_int, [vp, vp]),
     "tns_hip_get_stream": (vp, [vp]),
+    "tns_hip_pending_dw": (C.c_int, [vp]),
     "tns_hip_finish": (C.c_int, [vp]),
     "tns_hip_malloc": (C.c_int, [vp, i64, C.POINTER(vp)]),
     "tns_hip_free": (C.c_int, [vp, vp]),

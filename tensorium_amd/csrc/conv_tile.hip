@@ -322,6 +322,9 @@ const TileInfo kTiles[] = {
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 // the conv_tile4.hip forms picked by default (TNS_CT4_AR: their A-in-
 // registers twins, diagnostics builds only — measured slower, conv_tile4.hip)
+#if defined(TNS_CT4_AR) && !defined(TNS_DIAG_KERNELS)
+#error "TNS_CT4_AR selects kTiles4 forms 46..50, which exist only in the diagnostics build (TNS_DIAG=1)"
+#endif
 #ifdef TNS_CT4_AR
 constexpr int kT4OneByOnePF = 48;
 constexpr int kT4UnevenS2 = 49;

@@ -1314,7 +1314,9 @@ int conv_tile4_dx_pick(int64_t M, int64_t N, int64_t K, int64_t ks) {
 #ifndef TNS_CT4_TA_NO_PF
   // the 13^2 planes (N < 4096) on the PF twin of 7: whole pipelined backward
   // 14.80 -> 14.66 ms, joined 17.13 -> 17.11 (scripts/bwd_graph.py, same box,
-  // two rounds; profiles/r05_bwd_schedules.json)
+  // two rounds; profiles/r05_bwd_schedules.json).  The 1x1 layers on those
+  // planes are included on purpose (before: form 2, 128 x 48): the A/B was
+  // of the whole pass with both kinds switched together
   if (N < 4096 && K % 32 == 0 && M % 64 == 0) return 12;
 #endif
   if (ks == 1) {

@@ -15,6 +15,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -42,6 +43,10 @@ static int64_t g_dw_tile = -1;
 // conv backward: dW and state.delta concurrently on two streams (TNS_OPT_BWD_OVERLAP)
 static int64_t g_bwd_overlap = 1;
 static int64_t g_derive_sums = 0;
+// TNS_OPT_SCRATCH_CAP: largest context scratch buffer in floats (0 = none);
+// a larger request fails as an allocation failure would (tests reach the
+// fallback paths with it)
+static int64_t g_scratch_cap = 0;
 static int64_t g_tt_exact = 1;
 static int64_t g_srss_quirk = 0;
 static int64_t g_conv_variant = -1;
@@ -89,12 +94,17 @@ struct tns_ctx {
   // call's return; the next call of any other entry point joins them first
   bool side_pending = false;
   hipStream_t home_stream = nullptr;  // the context's stream while `stream` is aux
-  // the pending dW products' operand ranges (delta, input): a later call
-  // whose work on `stream` writes into one joins the side stream first
+  // the pending dW products' operand ranges: read (delta, input) and written
+  // (weight_updates; the caller's workspace when the dW's im2col fills it).
+  // A later call whose work on `stream` writes a read range, or touches a
+  // written one, joins the side stream first; so does a call that takes a
+  // scratch slot the side stream uses (side_slots)
   struct PendingDw {
-    uintptr_t lo[2], hi[2];
+    uintptr_t lo[2], hi[2];    // read by the dW
+    uintptr_t wlo[2], whi[2];  // written by the dW
   };
   std::vector<PendingDw> pending;
+  uint32_t side_slots = 0;
   // implicit-GEMM conv k-tables, one per (C, H, W, kH, kW, dY, dX)
   std::map<std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, int*> ktabs;
 };
@@ -106,8 +116,19 @@ enum { SLOT_COL = 0, SLOT_STAGE1 = 1, SLOT_STAGE2 = 2, SLOT_STAGE3 = 3, SLOT_DW 
        SLOT_RES_B = 11, SLOT_COUNT = 12 };
 static_assert(SLOT_COUNT == tns_ctx::kSlots, "one scratch buffer per slot");
 
-int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
+int join_side(tns_ctx* c);
+
+// scratch buffer `slot` of at least `elems` floats.  side: the caller is the
+// pipelined conv backward taking a slot for the dW it queues behind the
+// pending ones on the side stream (no join); any other caller of a slot the
+// side stream still uses joins it first
+int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out, bool side = false) {
   if (elems < 1) elems = 1;
+  if (!side && c->side_pending && (c->side_slots >> slot & 1u) && c->stream != c->aux_stream)
+    if (int r = join_side(c)) return r;
+  if (g_scratch_cap > 0 && elems > g_scratch_cap)
+    return set_error(TNS_ERR_NOMEM, "scratch slot %d: %lld floats exceed the cap of %lld", slot,
+                     (long long)elems, (long long)g_scratch_cap);
   if ((size_t)elems > c->scratch_elems[slot]) {
     if (c->scratch[slot]) {
       hipStreamSynchronize(c->stream);
@@ -118,9 +139,15 @@ int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out) {
       c->scratch_elems[slot] = 0;
     }
     hipError_t e = hipMalloc(&c->scratch[slot], (size_t)elems * sizeof(float));
-    if (e != hipSuccess)
+    if (e != hipSuccess) {
+      c->scratch[slot] = nullptr;
+      // (clear HIP's sticky last error: the launch helpers report
+      // hipGetLastError(), and a caller that falls back after this failure
+      // must not see it on its first launch)
+      hipGetLastError();
       return set_error(TNS_ERR_NOMEM, "hipMalloc(%lld floats) failed: %s", (long long)elems,
                        hipGetErrorString(e));
+    }
     c->scratch_elems[slot] = (size_t)elems;
   }
   *out = c->scratch[slot];
@@ -184,6 +211,7 @@ int join_side(tns_ctx* c) {
   if (!c->side_pending) return TNS_OK;
   c->side_pending = false;
   c->pending.clear();
+  c->side_slots = 0;
   hipError_t e = hipEventRecord(c->ev_join, c->aux_stream);
   if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->ev_join, 0);
   if (e != hipSuccess) return set_error(TNS_ERR_HIP, "backward join: %s", hipGetErrorString(e));
@@ -195,6 +223,49 @@ int join_side(tns_ctx* c) {
 int check_ctx(tns_ctx* c, bool join = true) {
   if (!c) return set_error(TNS_ERR_ARG, "null tns_ctx");
   return join ? join_side(c) : TNS_OK;
+}
+
+// an operand's extent: n elements every |inc| from p (empty when p is null
+// or n <= 0)
+struct Span {
+  uintptr_t lo = 0, hi = 0;
+};
+Span span(const float* p, int64_t n, int64_t inc = 1) {
+  Span s;
+  if (!p || n <= 0) return s;
+  const int64_t a = inc < 0 ? -inc : (inc == 0 ? 1 : inc);
+  s.lo = (uintptr_t)p;
+  s.hi = (uintptr_t)(p + (n - 1) * a + 1);
+  return s;
+}
+// a matrix operand of a (strided-batched) GEMM: rows x cols with leading
+// dimension ld, batch copies every stride
+Span span_mat(const float* p, int64_t rows, int64_t cols, int64_t ld, int64_t stride,
+              int64_t batch) {
+  if (rows <= 0 || cols <= 0 || batch <= 0) return Span{};
+  return span(p, (batch - 1) * (stride > 0 ? stride : 0) + (rows - 1) * ld + cols);
+}
+
+// every non-conv entry point: the context exists, and — during a pipelined
+// conv backward (TNS_OPT_BWD_OVERLAP = 2) — the side stream is joined only
+// when this call's operands meet a pending dW's: it writes that dW's delta
+// or input, or reads or writes its weight_updates / col workspace.  Calls
+// that touch none of them (the shortcut's addvv between two conv layers, a
+// route's copies, an upsample) leave the dW products running
+int check_ops(tns_ctx* c, std::initializer_list<Span> writes, std::initializer_list<Span> reads) {
+  if (!c) return set_error(TNS_ERR_ARG, "null tns_ctx");
+  if (!c->side_pending) return TNS_OK;
+  auto meet = [](const Span& a, uintptr_t lo, uintptr_t hi) {
+    return a.lo < a.hi && lo < hi && a.lo < hi && lo < a.hi;
+  };
+  for (const tns_ctx::PendingDw& d : c->pending)
+    for (int y = 0; y < 2; ++y) {
+      for (const Span& w : writes)
+        if (meet(w, d.lo[y], d.hi[y]) || meet(w, d.wlo[y], d.whi[y])) return join_side(c);
+      for (const Span& r : reads)
+        if (meet(r, d.wlo[y], d.whi[y])) return join_side(c);
+    }
+  return TNS_OK;
 }
 
 int hip_status(hipError_t e, const char* what) {
@@ -639,6 +710,9 @@ int tns_set_option(int32_t opt, int64_t value) {
     case TNS_OPT_DERIVE_SUMS:
       g_derive_sums = value ? 1 : 0;
       return TNS_OK;
+    case TNS_OPT_SCRATCH_CAP:
+      g_scratch_cap = value > 0 ? value : 0;
+      return TNS_OK;
     case TNS_OPT_DX_CONV:
       if (value >= conv_tile4_dx3_count())
         return set_error(TNS_ERR_ARG, "no dX conv form %lld", (long long)value);
@@ -712,6 +786,11 @@ void* tns_hip_get_stream(tns_ctx* c) {
   return (void*)c->stream;
 }
 
+int tns_hip_pending_dw(tns_ctx* c) {
+  if (!c) return -1;
+  return c->side_pending ? (int)c->pending.size() : 0;
+}
+
 int tns_hip_finish(tns_ctx* c) {
   if (int r = check_ctx(c)) return r;
   return hip_status(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
@@ -749,7 +828,12 @@ int tns_hip_gemm(tns_ctx* c, uint8_t transA, uint8_t transB, int64_t M, int64_t 
                  float ALPHA, const float* A, int64_t aOffset, int64_t lda, const float* B,
                  int64_t bOffset, int64_t ldb, float BETA, float* C, int64_t cOffset,
                  int64_t ldc) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span_mat(C ? C + cOffset : nullptr, M, N, ldc, 0, 1)},
+                        {transA ? span_mat(A ? A + aOffset : nullptr, K, M, lda, 0, 1)
+                                : span_mat(A ? A + aOffset : nullptr, M, K, lda, 0, 1),
+                         transB ? span_mat(B ? B + bOffset : nullptr, N, K, ldb, 0, 1)
+                                : span_mat(B ? B + bOffset : nullptr, K, N, ldb, 0, 1)}))
+    return r;
   return do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, A ? A + aOffset : nullptr, lda, 0,
                  B ? B + bOffset : nullptr, ldb, 0, BETA, C ? C + cOffset : nullptr, ldc, 0, 1,
                  EPI_NONE, nullptr, 0);
@@ -761,7 +845,13 @@ int tns_hip_gemm_strided_batched(tns_ctx* c, uint8_t transA, uint8_t transB, int
                                  int64_t bOffset, int64_t ldb, int64_t strideB, float BETA,
                                  float* C, int64_t cOffset, int64_t ldc, int64_t strideC,
                                  int64_t batchCount) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(
+          c, {span_mat(C ? C + cOffset : nullptr, M, N, ldc, strideC, batchCount)},
+          {transA ? span_mat(A ? A + aOffset : nullptr, K, M, lda, strideA, batchCount)
+                  : span_mat(A ? A + aOffset : nullptr, M, K, lda, strideA, batchCount),
+           transB ? span_mat(B ? B + bOffset : nullptr, N, K, ldb, strideB, batchCount)
+                  : span_mat(B ? B + bOffset : nullptr, K, N, ldb, strideB, batchCount)}))
+    return r;
   return do_gemm(c, transA != 0, transB != 0, M, N, K, ALPHA, A ? A + aOffset : nullptr, lda,
                  strideA, B ? B + bOffset : nullptr, ldb, strideB, BETA,
                  C ? C + cOffset : nullptr, ldc, strideC, batchCount, EPI_NONE, nullptr, 0);
@@ -834,11 +924,17 @@ int tns_hip_im2col_strided_batched(tns_ctx* c, int64_t aChannels, int64_t aHeigh
                                    const float* im, int64_t imStride, int64_t imOffset,
                                    float* col, int64_t colStride, int64_t colOffset,
                                    int64_t batchCount) {
-  if (int r = check_ctx(c)) return r;
+  if (!c) return check_ctx(c);
   ConvGeom g = geom(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
                     strideY, strideX, dilationY, dilationX);
   if (int r = check_geom(g)) return r;
   if (!im || !col) return set_error(TNS_ERR_ARG, "im2col: null pointer");
+  {
+    const int64_t nb = batchCount > 0 ? batchCount : 0, colN = g.C * g.kH * g.kW * g.oh * g.ow;
+    if (int r = check_ops(c, {span_mat(col + colOffset, 1, colN, colN, colStride, nb)},
+                          {span_mat(im + imOffset, 1, g.C * g.H * g.W, 0, imStride, nb)}))
+      return r;
+  }
   OpTimer t(c, TNS_OP_IM2COL);
   return hip_status(launch_im2col(g, im + imOffset, imStride, col + colOffset, colStride,
                                   batchCount, c->stream),
@@ -861,11 +957,17 @@ int tns_hip_col2im_strided_batched(tns_ctx* c, int64_t aChannels, int64_t aHeigh
                                    const float* col, int64_t colStride, int64_t colOffset,
                                    float* im, int64_t imStride, int64_t imOffset,
                                    int64_t batchCount) {
-  if (int r = check_ctx(c)) return r;
+  if (!c) return check_ctx(c);
   ConvGeom g = geom(aChannels, aHeight, aWidth, kernelHeight, kernelWidth, padHeight, padWidth,
                     strideY, strideX, dilationY, dilationX);
   if (int r = check_geom(g)) return r;
   if (!im || !col) return set_error(TNS_ERR_ARG, "col2im: null pointer");
+  {
+    const int64_t nb = batchCount > 0 ? batchCount : 0, colN = g.C * g.kH * g.kW * g.oh * g.ow;
+    if (int r = check_ops(c, {span_mat(im + imOffset, 1, g.C * g.H * g.W, 0, imStride, nb)},
+                          {span_mat(col + colOffset, 1, colN, colN, colStride, nb)}))
+      return r;
+  }
   if (batchCount > 1 && imStride < aChannels * aHeight * aWidth)
     return set_error(TNS_ERR_ARG, "col2im: overlapping image strides");
   OpTimer t(c, TNS_OP_COL2IM);
@@ -885,7 +987,8 @@ int tns_hip_col2im(tns_ctx* c, int64_t aChannels, int64_t aHeight, int64_t aWidt
 
 int tns_hip_forward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t offset, int64_t srcSize,
                          const float* src, int64_t incb, int64_t batch) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst ? dst + offset : nullptr, dstSize)}, {span(src, srcSize, incb)}))
+    return r;
   if (dstSize == 0) return TNS_OK;
   if (!dst || !src || srcSize <= 0 || batch <= 0 || dstSize % (srcSize * batch) != 0)
     return set_error(TNS_ERR_ARG, "forwardBias: sizes do not align");
@@ -897,7 +1000,8 @@ int tns_hip_forward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t offset
 
 int tns_hip_backward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t srcSize,
                           const float* src, int64_t srcOffset, int64_t incb, int64_t batch) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst, dstSize)}, {span(src ? src + srcOffset : nullptr, srcSize)}))
+    return r;
   if (!dst || !src || dstSize <= 0 || batch <= 0 || srcSize % (dstSize * batch) != 0)
     return set_error(TNS_ERR_ARG, "backwardBias: sizes do not align");
   const int64_t bs = srcSize / (dstSize * batch);
@@ -916,7 +1020,7 @@ int tns_hip_backward_bias(tns_ctx* c, int64_t dstSize, float* dst, int64_t srcSi
 }
 
 int tns_hip_activate_array(tns_ctx* c, int64_t N, float* x, int64_t offset, int32_t activation) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(x ? x + offset : nullptr, N)}, {})) return r;
   if (!act_supported(activation))
     return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
   if (N <= 0) return TNS_OK;
@@ -927,7 +1031,7 @@ int tns_hip_activate_array(tns_ctx* c, int64_t N, float* x, int64_t offset, int3
 
 int tns_hip_derive_array(tns_ctx* c, int64_t N, const float* x, int64_t offset,
                          int32_t activation, float* delta) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(delta, N)}, {span(x ? x + offset : nullptr, N)})) return r;
   if (!act_supported(activation))
     return set_error(TNS_ERR_UNSUPPORTED, "derivative %d not implemented", activation);
   if (N <= 0) return TNS_OK;
@@ -938,7 +1042,9 @@ int tns_hip_derive_array(tns_ctx* c, int64_t N, const float* x, int64_t offset,
 
 int tns_hip_axpy(tns_ctx* c, int64_t N, float a, const float* x, int64_t xOffset, int64_t incx,
                  float* y, int64_t yOffset, int64_t incy) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(y ? y + yOffset : nullptr, N, incy)},
+                        {span(x ? x + xOffset : nullptr, N, incx)}))
+    return r;
   return hip_status(launch_axpy(N, a, x + xOffset, incx, y + yOffset, incy, c->stream), "axpy");
 }
 
@@ -946,7 +1052,10 @@ int tns_hip_sgd_update(tns_ctx* c, int64_t nWeights, float* weights, float* weig
                        int64_t n, float* biases, float* bias_updates, float* scales,
                        float* scale_updates, float lrOverBatch, float negDecayTimesBatch,
                        float momentum) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(weights, nWeights), span(weight_updates, nWeights), span(biases, n),
+                            span(bias_updates, n), span(scales, n), span(scale_updates, n)},
+                        {}))
+    return r;
   if (nWeights < 0 || n < 0 || (nWeights > 0 && (!weights || !weight_updates)) ||
       (n > 0 && (!biases || !bias_updates)) || (!scales != !scale_updates))
     return set_error(TNS_ERR_ARG, "sgd_update: bad arguments");
@@ -957,25 +1066,29 @@ int tns_hip_sgd_update(tns_ctx* c, int64_t nWeights, float* weights, float* weig
 }
 
 int tns_hip_scale(tns_ctx* c, int64_t N, float a, float* x, int64_t stride) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(x, N, stride)}, {})) return r;
   return hip_status(launch_scale(N, a, x, stride, c->stream), "scale");
 }
 
 int tns_hip_fill(tns_ctx* c, int64_t N, float* x, int64_t offset, float val, int64_t stride) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(x ? x + offset : nullptr, N, stride)}, {})) return r;
   return hip_status(launch_fill(N, x + offset, val, stride, c->stream), "fill");
 }
 
 int tns_hip_copy(tns_ctx* c, int64_t N, const float* src, int64_t srcOffset, int64_t inca,
                  float* dst, int64_t dstOffset, int64_t incb) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst ? dst + dstOffset : nullptr, N, incb)},
+                        {span(src ? src + srcOffset : nullptr, N, inca)}))
+    return r;
   return hip_status(launch_copy(N, src + srcOffset, inca, dst + dstOffset, incb, c->stream),
                     "copy");
 }
 
 int tns_hip_shortcut(tns_ctx* c, int64_t N, const float* a, int64_t aOffset, const float* b,
                      int64_t bOffset, float* out, int64_t outOffset, int32_t activation) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(out ? out + outOffset : nullptr, N)},
+                        {span(a ? a + aOffset : nullptr, N), span(b ? b + bOffset : nullptr, N)}))
+    return r;
   if (N < 0 || (N > 0 && (!a || !b || !out))) return set_error(TNS_ERR_ARG, "shortcut: bad args");
   if (!act_supported(activation))
     return set_error(TNS_ERR_UNSUPPORTED, "activation %d not implemented", activation);
@@ -987,7 +1100,11 @@ int tns_hip_shortcut(tns_ctx* c, int64_t N, const float* a, int64_t aOffset, con
 int tns_hip_upsample(tns_ctx* c, int64_t aBatch, int64_t aChannels, int64_t outHeight,
                      int64_t outWidth, float* in, int64_t stride, int32_t isForward, float scale,
                      float* out, int32_t zeroIn) {
-  if (int r = check_ctx(c)) return r;
+  {
+    const int64_t small = aBatch * aChannels * outHeight * outWidth, big = small * stride * stride;
+    const Span si = span(in, small), so = span(out, big);
+    if (int r = isForward ? check_ops(c, {so}, {si}) : check_ops(c, {si}, {so})) return r;
+  }
   const int64_t planes = aBatch * aChannels, H = outHeight, W = outWidth;
   if (aBatch < 0 || aChannels < 0 || H < 0 || W < 0 || stride < 1 ||
       H * stride > 0x7fffffff || W * stride > 0x7fffffff ||
@@ -1007,7 +1124,10 @@ namespace {
 int vv(tns_ctx* c, int op, int64_t N, const float* a, int64_t aOff, int64_t inca, const float* b,
        int64_t bOff, int64_t incb, const float* cc, int64_t cOff, int64_t incc, float* d,
        int64_t dOff, int64_t incd, const char* what) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(d ? d + dOff : nullptr, N, incd)},
+                        {span(a ? a + aOff : nullptr, N, inca), span(b ? b + bOff : nullptr, N, incb),
+                         span(cc ? cc + cOff : nullptr, N, incc)}))
+    return r;
   if (N < 0 || (N > 0 && (!a || !b || !d || (op == 3 && !cc))))
     return set_error(TNS_ERR_ARG, "%s: bad args", what);
   return hip_status(launch_vv(op, N, a + aOff, inca, b + bOff, incb, cc ? cc + cOff : nullptr,
@@ -1047,7 +1167,9 @@ int tns_hip_fmavv(tns_ctx* c, int64_t N, const float* src1, int64_t src1Offset, 
 
 int tns_hip_fmavss(tns_ctx* c, int64_t N, const float* src, int64_t offset, float scalar,
                    float bias, float* dst) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst ? dst + offset : nullptr, N)},
+                        {span(src ? src + offset : nullptr, N)}))
+    return r;
   if (N < 0 || (N > 0 && (!src || !dst))) return set_error(TNS_ERR_ARG, "fmavss: bad args");
   return hip_status(launch_fmavss(N, src + offset, scalar, bias, dst + offset, c->stream),
                     "fmavss");
@@ -1056,7 +1178,9 @@ int tns_hip_fmavss(tns_ctx* c, int64_t N, const float* src, int64_t offset, floa
 int tns_hip_inverse_sqrt(tns_ctx* c, int64_t N, float alpha, const float* src, float* dst,
                          int64_t stride, int64_t offset) {
   (void)alpha;  // unused by the reference kernel too
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst ? dst + offset : nullptr, N, stride)},
+                        {span(src ? src + offset : nullptr, N, stride)}))
+    return r;
   if (N < 0 || stride < 1 || (N > 0 && (!src || !dst)))
     return set_error(TNS_ERR_ARG, "inverseSqrt: bad args");
   return hip_status(launch_inverse_sqrt(N, src + offset, dst + offset, stride, c->stream),
@@ -1095,7 +1219,10 @@ int tns_set_op_devices(const int32_t* devices, int32_t n) {
 
 int tns_hip_yolo_forward(tns_ctx* c, int64_t batch, int64_t anchors, int64_t classes, int64_t hw,
                          const float* in, float* out) {
-  if (int r = check_ctx(c)) return r;
+  {
+    const int64_t n = batch * anchors * (classes + 5) * hw;
+    if (int r = check_ops(c, {span(out, n)}, {span(in, n)})) return r;
+  }
   if (batch < 0 || anchors < 0 || classes < 0 || hw < 0 ||
       (batch * anchors * hw > 0 && (!in || !out)))
     return set_error(TNS_ERR_ARG, "yolo: bad args");
@@ -1104,7 +1231,9 @@ int tns_hip_yolo_forward(tns_ctx* c, int64_t batch, int64_t anchors, int64_t cla
 
 int tns_hip_clamp(tns_ctx* c, int64_t N, float alpha, const float* src, float* dst,
                   int64_t stride, int64_t offset) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst ? dst + offset : nullptr, N, stride)},
+                        {span(src ? src + offset : nullptr, N, stride)}))
+    return r;
   return hip_status(launch_clamp(N, alpha, src + offset, dst + offset, stride, c->stream),
                     "clamp");
 }
@@ -1122,7 +1251,9 @@ int blocks_of(int64_t total, int64_t channels, int64_t groups, int64_t* bs, cons
 
 int tns_hip_means_and_vars(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
                            const float* src, int64_t offset, float* means, float* vars) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(means, dstSize), span(vars, dstSize)},
+                        {span(src ? src + offset : nullptr, srcSize)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(srcSize, dstSize, groups, &bs, "meansAndVars")) return r;
   if (!src || !means || !vars) return set_error(TNS_ERR_ARG, "meansAndVars: null pointer");
@@ -1135,7 +1266,8 @@ int tns_hip_means_and_vars(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t
 
 int tns_hip_means(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
                   const float* src, int64_t offset, float* means) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(means, dstSize)}, {span(src ? src + offset : nullptr, srcSize)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(srcSize, dstSize, groups, &bs, "means")) return r;
   if (!src || !means) return set_error(TNS_ERR_ARG, "means: null pointer");
@@ -1148,7 +1280,9 @@ int tns_hip_means(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
 
 int tns_hip_variances(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
                       const float* src, int64_t offset, const float* means, float* vars) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(vars, dstSize)},
+                        {span(src ? src + offset : nullptr, srcSize), span(means, dstSize)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(srcSize, dstSize, groups, &bs, "variances")) return r;
   if (!src || !means || !vars) return set_error(TNS_ERR_ARG, "variances: null pointer");
@@ -1163,7 +1297,9 @@ int tns_hip_variances(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t grou
 int tns_hip_normalize(tns_ctx* c, int64_t srcSize, int64_t dstSize, int64_t groups,
                       const float* means, int64_t meansStride, const float* vars,
                       int64_t varsStride, float* dst, int64_t dstOffset) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst ? dst + dstOffset : nullptr, dstSize)},
+                        {span(means, srcSize, meansStride), span(vars, srcSize, varsStride)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(dstSize, srcSize, groups, &bs, "normalize")) return r;
   if (!dst || !means || !vars) return set_error(TNS_ERR_ARG, "normalize: null pointer");
@@ -1181,7 +1317,9 @@ int tns_hip_forward_scale(tns_ctx* c, int64_t dstSize, float* dst, int64_t offse
 int tns_hip_forward_scale_add(tns_ctx* c, int64_t dstSize, float* dst, int64_t offset,
                               int64_t scaleSize, const float* scales, const float* biases,
                               int64_t incb, int64_t batch) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst ? dst + offset : nullptr, dstSize)},
+                        {span(scales, scaleSize, incb), span(biases, scaleSize, incb)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(dstSize, scaleSize, batch, &bs, "forwardScale")) return r;
   if (!dst || !scales) return set_error(TNS_ERR_ARG, "forwardScale: null pointer");
@@ -1194,7 +1332,11 @@ int tns_hip_means_and_vars_delta(tns_ctx* c, int64_t srcSize, int64_t dstSize, i
                                  const float* delta, const float* x, int64_t offset,
                                  const float* mean, const float* variance, float* mean_delta,
                                  float* variance_delta) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(mean_delta, dstSize), span(variance_delta, dstSize)},
+                        {span(delta ? delta + offset : nullptr, srcSize),
+                         span(x ? x + offset : nullptr, srcSize), span(mean, dstSize),
+                         span(variance, dstSize)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(srcSize, dstSize, groups, &bs, "meansAndVarsDelta")) return r;
   if (!delta || !x || !mean || !variance || !mean_delta || !variance_delta)
@@ -1211,7 +1353,11 @@ int tns_hip_normalize_delta(tns_ctx* c, int64_t deltaSize, int64_t meanSize, int
                             float* delta, const float* x, int64_t offset, const float* mean,
                             const float* variance, const float* mean_delta,
                             const float* variance_delta) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(delta ? delta + offset : nullptr, deltaSize)},
+                        {span(x ? x + offset : nullptr, deltaSize), span(mean, meanSize),
+                         span(variance, meanSize), span(mean_delta, meanSize),
+                         span(variance_delta, meanSize)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(deltaSize, meanSize, groups, &bs, "normalizeDelta")) return r;
   if (!delta || !x || !mean || !variance || !mean_delta || !variance_delta)
@@ -1224,7 +1370,10 @@ int tns_hip_normalize_delta(tns_ctx* c, int64_t deltaSize, int64_t meanSize, int
 
 int tns_hip_add_dots(tns_ctx* c, int64_t N, int64_t dstSize, int64_t groups, const float* src1,
                      const float* src2, int64_t srcOffset, float* dst) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(dst, dstSize)},
+                        {span(src1 ? src1 + srcOffset : nullptr, N),
+                         span(src2 ? src2 + srcOffset : nullptr, N)}))
+    return r;
   int64_t bs;
   if (int r = blocks_of(N, dstSize, groups, &bs, "addDots")) return r;
   if (!dst || !src1 || !src2) return set_error(TNS_ERR_ARG, "addDots: null pointer");
@@ -1238,7 +1387,9 @@ int tns_hip_add_dots(tns_ctx* c, int64_t N, int64_t dstSize, int64_t groups, con
 int tns_hip_softmax_batch(tns_ctx* c, int64_t N, const float* input, int64_t iOffset,
                           int64_t batch, int64_t batch_size, int64_t groups, int64_t group_size,
                           int64_t stride, float temp, float* output, int64_t oOffset) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(output ? output + oOffset : nullptr, N)},
+                        {span(input ? input + iOffset : nullptr, N)}))
+    return r;
   if (!input || !output || N < 0) return set_error(TNS_ERR_ARG, "softmaxBatch: bad args");
   return hip_status(launch_softmax_batch(N, input + iOffset, batch, batch_size, groups,
                                          group_size, stride, temp, output + oOffset, c->stream),
@@ -1247,13 +1398,14 @@ int tns_hip_softmax_batch(tns_ctx* c, int64_t N, const float* input, int64_t iOf
 
 int tns_hip_cross_entropy_softmax(tns_ctx* c, int64_t N, const float* pred, const float* truth,
                                   float* delta, float* error) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(delta, N), span(error, N)}, {span(pred, N), span(truth, N)}))
+    return r;
   if (!pred || !truth || !delta || !error) return set_error(TNS_ERR_ARG, "xent: null pointer");
   return hip_status(launch_xent_softmax(N, pred, truth, delta, error, c->stream), "xent");
 }
 
 int tns_hip_sum(tns_ctx* c, int64_t N, const float* src, int64_t offset, float* out) {
-  if (int r = check_ctx(c)) return r;
+  if (int r = check_ops(c, {span(out, 1)}, {span(src ? src + offset : nullptr, N)})) return r;
   if (!src || !out || N < 0) return set_error(TNS_ERR_ARG, "sum: bad args");
   return hip_status(launch_vssum(N, src + offset, out, c->stream), "sum");
 }
@@ -1282,6 +1434,13 @@ int tns_hip_mlp_train_step(tns_ctx* c, int32_t nlayers, const int64_t* widths,
   }
   if (9 * batch * omax > 40960)
     return set_error(TNS_ERR_ARG, "mlp_train_step: 9*batch*max(width) exceeds LDS staging");
+  // (the kernels index a layer's weights and activations with 32-bit ints)
+  for (int l = 0; l < nlayers; ++l)
+    if (widths[l] * widths[l + 1] > 0x7fffffffLL)
+      return set_error(TNS_ERR_ARG, "mlp_train_step: layer %d has %lld weights (32-bit indexing)",
+                       l, (long long)(widths[l] * widths[l + 1]));
+  if (batch * widths[0] > 0x7fffffffLL)
+    return set_error(TNS_ERR_ARG, "mlp_train_step: batch x input width exceeds 32-bit indexing");
   for (int l = 0; l < nlayers; ++l) {
     if (!act_supported(acts[l]))
       return set_error(TNS_ERR_UNSUPPORTED, "mlp_train_step: activation %d", acts[l]);
@@ -1679,15 +1838,18 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     // stream: if a pending dW reads either (an earlier call on the same
     // layers, e.g. the previous pass), the side stream is joined first (no
     // per-call event: the join is only paid where the ranges meet)
-    const uintptr_t w0[2] = {(uintptr_t)delta, (uintptr_t)state_delta};
-    const uintptr_t w1[2] = {(uintptr_t)(delta + batch * filters * i_k),
-                             (uintptr_t)(state_delta ? state_delta + batch * C * H * W : nullptr)};
-    bool hit = false;
-    for (const tns_ctx::PendingDw& d : c->pending)
-      for (int x = 0; x < 2; ++x)
-        for (int y = 0; y < 2; ++y) hit |= w0[x] < w1[x] && d.lo[y] < w1[x] && w0[x] < d.hi[y];
-    if (hit)
-      if (int r = join_side(c)) return r;
+    // (the same test as every other entry point's, over this call's
+    // context-stream operands; its own dW queues on the side stream)
+    const int64_t nf = bn.scales ? filters : 0;
+    if (int r = check_ops(c,
+                          {span(delta, batch * filters * i_k), span(state_delta, batch * C * H * W),
+                           span(bias_updates, bn.scales ? 0 : filters), span(bn.scale_updates, nf),
+                           span(bn.mean_delta, nf), span(bn.variance_delta, nf)},
+                          {span(output, batch * filters * i_k), span(weights, filters * i_n),
+                           span(bn.x, nf ? batch * filters * i_k : 0),
+                           span(bn.x_norm, nf ? batch * filters * i_k : 0),
+                           span(bn.scales, nf), span(bn.mean, nf), span(bn.variance, nf)}))
+      return r;
   }
   float* part;
   if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
@@ -1769,9 +1931,11 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   DwResArgs dres{};
   if (dwr >= 0) {
     const int64_t rowlen = 8 * dw_res_k4(i_k);
-    int r = ensure_scratch(c, SLOT_RES_A, batch * i_m * rowlen + 32, &dres.dA);
-    if (!r) r = ensure_scratch(c, SLOT_RES_B, batch * dw_res_b_rows(dwr, i_n) * rowlen + 32, &dres.dB);
-    if (!r) r = ensure_scratch(c, SLOT_DW, batch * dw_res_groups(dwr) * i_m * i_n, &dres.part);
+    int r = ensure_scratch(c, SLOT_RES_A, batch * i_m * rowlen + 32, &dres.dA, pipe);
+    if (!r)
+      r = ensure_scratch(c, SLOT_RES_B, batch * dw_res_b_rows(dwr, i_n) * rowlen + 32, &dres.dB,
+                         pipe);
+    if (!r) r = ensure_scratch(c, SLOT_DW, batch * dw_res_groups(dwr) * i_m * i_n, &dres.part, pipe);
     if (r) {
       if (g_dw_res >= 0) return r;  // (forced: the error stands)
       tns_clear_error();
@@ -1826,7 +1990,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   }
   float* ws = workspace;
   if (!ws && (dw_col || (dx_col && !dx_ws && !(overlap && dw_col))))
-    if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws)) return r;
+    if (int r = ensure_scratch(c, SLOT_COL, batch * colSize, &ws, pipe)) return r;
   if (!dx_ws) dx_ws = ws;  // col buffer of state.delta's chain
   // scratch of the fused state.delta kernel, sized before any fork (a growth
   // inside the side-stream chain would free a buffer the main stream may use)
@@ -1851,7 +2015,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     }
     if (dwv >= 0) {
       float* part = nullptr;
-      if (int r = ensure_scratch(c, SLOT_DW, batch * i_m * i_n, &part)) return r;
+      if (int r = ensure_scratch(c, SLOT_DW, batch * i_m * i_n, &part, pipe)) return r;
       da.part = part;
       {
         OpTimer t(c, TNS_OP_GEMM);
@@ -1879,7 +2043,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     // the few-tile, long-k dW shapes.
     if (g_nt_sdot && batch > 1) {
       float* part = nullptr;
-      if (int r = ensure_scratch(c, SLOT_DW, batch * i_m * i_n, &part)) return r;
+      if (int r = ensure_scratch(c, SLOT_DW, batch * i_m * i_n, &part, pipe)) return r;
       GemmArgs a{};
       a.M = i_m; a.N = i_n; a.K = i_k;
       a.alpha = 1.0f; a.beta = 0.0f; a.beta_mode = BETA_STORE;
@@ -1975,14 +2139,20 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     c->stream = main;
     c->home_stream = nullptr;
     c->side_pending = true;
-    if (rw) return rw;
-    // the record of this dW's operands
+    // the record of this dW's operands and of the scratch slots it uses
+    // (kept after a failed launch too: whatever it enqueued stays ordered)
     tns_ctx::PendingDw d;
-    d.lo[0] = (uintptr_t)delta;
-    d.hi[0] = (uintptr_t)(delta + batch * filters * i_k);
-    d.lo[1] = (uintptr_t)input;
-    d.hi[1] = (uintptr_t)(input + batch * C * H * W);
+    const Span rd = span(delta, batch * filters * i_k), ri = span(input, batch * C * H * W);
+    const Span wu = span(weight_updates, i_m * i_n);
+    const Span wc = dw_col && ws == workspace ? span(ws, batch * colSize) : Span{};
+    d.lo[0] = rd.lo; d.hi[0] = rd.hi;
+    d.lo[1] = ri.lo; d.hi[1] = ri.hi;
+    d.wlo[0] = wu.lo; d.whi[0] = wu.hi;
+    d.wlo[1] = wc.lo; d.whi[1] = wc.hi;
     c->pending.push_back(d);
+    c->side_slots |= 1u << SLOT_RES_A | 1u << SLOT_RES_B | 1u << SLOT_DW |
+                     (dw_col && ws != workspace ? 1u << SLOT_COL : 0u);
+    if (rw) return rw;
     return state_delta ? run_dx() : TNS_OK;
   }
   if (!overlap) {

@@ -323,3 +323,140 @@ class HipDarknet:
                 hip.yoloForward(B, l.anchors, l.classes, l.h * l.w, prev, out)
             prev = out
         return self.out
+
+
+class HipDarknetTrain:
+    """One training pass of a darknet network on the HIP backend, in the
+    reference's call order: TNet.forward in training (nnet.pas:275-322; each
+    layer's delta zeroed by ``cuda.scale(size, 0, delta, 1)`` before its
+    forward) and TNet.backward (nnet.pas:323-366: layers from the last to the
+    first, layer i's state.delta = layer i-1's delta, none for layer 0),
+    each layer through the TNNHip call its backwardGPU makes:
+
+    * convolutional: ``convBackwardBN`` (batch-normalized layers:
+      Derivative + batchNormBack + dW + state.delta, nConvolutionLayer.pas:
+      571-671 -> nbaselayer.pas:372-395) or ``convBackward`` (the 1x1
+      detection heads: Derivative + addSums + dW + state.delta);
+    * shortcut (TAddLayer.backwardGPU, naddlayer.pas:924-949): DeriveArray,
+      then ``addvv`` of its delta into state.delta and into the from-layer's
+      delta;
+    * route (TConcatLayer.backwardGPU, nconcatlayer.pas:234-256): ``addvv`` of
+      its delta slices into each input layer's delta;
+    * upsample (TUpSampleLayer.backwardGPU, nupsamplelayer.pas:214-228):
+      ``upSample(..., isForward = 0)`` accumulating into state.delta;
+    * yolo (TYoloLayer.backwardGPU, nyololayer.pas:1112-1125): ``axpy`` of its
+      delta (scaled by lossScale*deltaNormalizer) into state.delta.  The yolo
+      loss that fills that delta during the training forward is out of scope
+      (DESIGN.md); ``set_yolo_deltas`` supplies it.
+
+    Convolutions with batch norm run ``convForwardTrain`` (training-time BN,
+    nbaselayer.pas:336-370) in the forward, the heads ``convForward``.  No
+    weight update is made here (TNet.update is a separate call per layer,
+    ``sgdUpdate``)."""
+
+    def __init__(self, hip, net: Network, params: list[ConvParams], torch, loss_scale: float = 1.0):
+        self.hip, self.net, self.torch = hip, net, torch
+        self.loss_scale = float(loss_scale)
+        B = net.batch
+        dev = "cuda"
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)  # noqa: E731
+        self.out = [torch.zeros(B * l.out_size, device=dev) for l in net.layers]
+        self.delta = [torch.zeros(B * l.out_size, device=dev) for l in net.layers]
+        self.conv = {}
+        ws = 1
+        for l, p in zip(net.convs(), params):
+            n = B * l.out_size
+            st = {"w": t(p.weights), "b": t(p.biases),
+                  "wu": torch.zeros(p.weights.size, device=dev),
+                  "bu": torch.zeros(l.filters, device=dev)}
+            if l.bn:
+                st.update(scales=t(p.scales), rm=t(p.rolling_mean), rv=t(p.rolling_var),
+                          mean=torch.zeros(l.filters, device=dev),
+                          var=torch.zeros(l.filters, device=dev),
+                          x=torch.zeros(n, device=dev), xn=torch.zeros(n, device=dev),
+                          su=torch.zeros(l.filters, device=dev),
+                          md=torch.zeros(l.filters, device=dev),
+                          vd=torch.zeros(l.filters, device=dev))
+            self.conv[l.index] = st
+            ws = max(ws, B * l.c * l.size * l.size * l.out_h * l.out_w)
+        self.ws = torch.empty(ws, device=dev)
+
+    def forward(self, x):
+        """TNet.forward with state.isTraining (BN statistics of the batch,
+        rolling statistics updated with bnMomentum 0.1)."""
+        hip, B = self.hip, self.net.batch
+        prev = x
+        for l in self.net.layers:
+            hip.scale(self.delta[l.index].numel(), 0.0, self.delta[l.index], 1)
+            out = self.out[l.index]
+            if l.kind == "convolutional":
+                st = self.conv[l.index]
+                if l.bn:
+                    hip.convForwardTrain(B, l.c, l.h, l.w, prev, st["w"], l.filters, l.size,
+                                         l.stride, l.pad, 1, l.activation, st["scales"], st["b"],
+                                         st["rm"], st["rv"], 0.1, True, st["mean"], st["var"],
+                                         st["x"], st["xn"], self.ws, out)
+                else:
+                    hip.convForward(B, l.c, l.h, l.w, prev, st["w"], st["b"], l.filters, l.size,
+                                    l.stride, l.pad, 1, l.activation, self.ws, out, fused=True)
+            elif l.kind == "shortcut":
+                hip.shortcut(B * l.out_size, prev, 0, self.out[l.inputs[0]], 0, out, 0,
+                             l.activation)
+            elif l.kind == "route":
+                off = 0
+                for s in l.inputs:
+                    n = B * self.net.layers[s].out_size
+                    hip.copy(n, self.out[s], 0, 1, out, off, 1)
+                    off += n
+            elif l.kind == "upsample":
+                hip.upSample(B, l.c, l.h, l.w, prev, l.stride, 1, 1.0, out)
+            elif l.kind == "yolo":
+                hip.yoloForward(B, l.anchors, l.classes, l.h * l.w, prev, out)
+            prev = out
+        return self.out
+
+    def set_yolo_deltas(self, deltas):
+        """The yolo layers' deltas (what their training forward's loss would
+        leave), in layer order."""
+        ys = [l for l in self.net.layers if l.kind == "yolo"]
+        for l, d in zip(ys, deltas):
+            self.delta[l.index].copy_(d.reshape(-1))
+
+    def backward(self, x, on_backward=None):
+        """TNet.backward (nnet.pas:323-366) over every layer; on_backward(l)
+        after each layer's calls (TNet.OnBackward, nnet.pas:361-362)."""
+        hip, B, L = self.hip, self.net.batch, self.net.layers
+        for l in reversed(L):
+            i = l.index
+            inp = x if i == 0 else self.out[i - 1]
+            sd = None if i == 0 else self.delta[i - 1]
+            d = self.delta[i]
+            if l.kind == "convolutional":
+                st = self.conv[i]
+                if l.bn:
+                    hip.convBackwardBN(B, l.c, l.h, l.w, inp, st["w"], l.filters, l.size,
+                                       l.stride, l.pad, 1, l.activation, self.out[i], d,
+                                       st["scales"], st["x"], st["xn"], st["mean"], st["var"],
+                                       st["su"], st["md"], st["vd"], st["wu"], self.ws, sd)
+                else:
+                    hip.convBackward(B, l.c, l.h, l.w, inp, st["w"], l.filters, l.size, l.stride,
+                                     l.pad, 1, l.activation, self.out[i], d, st["bu"], st["wu"],
+                                     self.ws, sd)
+            elif l.kind == "shortcut":
+                n = d.numel()
+                hip.DeriveArray(n, self.out[i], 0, l.activation, d)
+                hip.addvv(n, d, 0, 1, sd, 0, 1, sd, 0, 1)
+                src = self.delta[l.inputs[0]]
+                hip.addvv(n, src, 0, 1, d, 0, 1, src, 0, 1)
+            elif l.kind == "route":
+                off = 0
+                for s in l.inputs:
+                    pt = self.delta[s]
+                    hip.addvv(pt.numel(), pt, 0, 1, d, off, 1, pt, 0, 1)
+                    off += pt.numel()
+            elif l.kind == "upsample":
+                hip.upSample(B, l.c, l.h, l.w, sd, l.stride, 0, 1.0, d)
+            elif l.kind == "yolo":
+                hip.axpy(sd.numel(), self.loss_scale, d, 0, 1, sd, 0, 1)
+            if on_backward is not None:
+                on_backward(l)

@@ -70,7 +70,22 @@ class TNNHip:
 
     @property
     def stream(self) -> int:
-        return int(self.lib.tns_hip_get_stream(self.ctx) or 0)
+        # (NULL with an error set: the join of pending dW products failed —
+        # handing out 0, the null stream, would order nothing after them;
+        # NULL without one is the legacy default stream the context runs on)
+        self.lib.tns_clear_error()
+        s = self.lib.tns_hip_get_stream(self.ctx)
+        if not s:
+            msg = self.lib.tns_last_error().decode(errors="replace")
+            if msg:
+                self.lib.tns_clear_error()
+                raise TnsError(f"tns_hip_get_stream: {msg}")
+        return int(s or 0)
+
+    def pendingDw(self) -> int:
+        """dW products of a pipelined conv backward still on the side stream
+        (tns_hip_pending_dw; 0 once joined)."""
+        return int(self.lib.tns_hip_pending_dw(self.ctx))
 
     def finish(self):  # TNNCuda.finish, nncuda.pas:1575
         check(self.lib.tns_hip_finish(self.ctx))
@@ -359,10 +374,16 @@ class TNNHip:
         """Conv backward: dW and state.delta concurrently on two streams,
         joined before the call returns (1 / True), in sequence (0 / False), or
         pipelined (2: each call's dW left running on the side stream behind
-        the earlier ones, joined by the next call of any other entry point);
-        same results; process-wide."""
+        the earlier ones, joined by a later call whose operands meet a pending
+        dW's, by finish() or by the stream property); same results;
+        process-wide."""
         m = int(mode) if not isinstance(mode, bool) else (1 if mode else 0)
         check(self.lib.tns_set_option(10, m))
+
+    def setScratchCap(self, floats: int = 0):
+        """Largest context scratch buffer in floats (0 = none); a larger
+        request fails as a failed allocation does; process-wide."""
+        check(self.lib.tns_set_option(14, int(floats)))
 
     def setDeriveSums(self, on: bool = False):
         """Conv backward (no batch norm): Derivative fused into addSums'
