@@ -1562,6 +1562,40 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
                                            ow, activation, c->stream),
                         "direct conv launch");
     }
+    // the two-pass slab form (conv_slab.hip) where picked, or forced by
+    // TNS_OPT_CONV_VARIANT = 500 + v
+    {
+      const int64_t N = batch * outImg;
+      int sv = -1;
+      if (g_conv_variant >= 500)
+        sv = (int)(g_conv_variant - 500);
+      else if (g_conv_variant < 0 && dilation == 1)
+        sv = conv_slab_pick(filters, N, k, kSize);
+      if (sv >= 0) {
+        const int64_t need = conv_slab_floats(sv, N, k);
+        if (need < 0) return set_error(TNS_ERR_ARG, "no conv slab form %d", sv);
+        float* slab = nullptr;
+        if (int r = ensure_scratch(c, SLOT_COL, need, &slab)) return r;
+        ConvSlabArgs sa{};
+        sa.input = input; sa.weights = weights; sa.bias = bias_act ? biases : nullptr; sa.out = out;
+        sa.batch = batch; sa.C = C; sa.H = H; sa.W = W; sa.M = filters; sa.K = k; sa.ks = kSize;
+        sa.stride = stride; sa.pad = padding; sa.dil = dilation; sa.ow = ow; sa.ohw = outImg;
+        sa.act = act_transcendental(activation) ? 4 : activation;
+        {
+          OpTimer t(c, TNS_OP_GEMM);
+          const hipError_t e = launch_conv_slab(sv, sa, slab, c->stream);
+          if (e == hipErrorInvalidValue)
+            return set_error(TNS_ERR_UNSUPPORTED, "conv slab form %d does not fit this layer", sv);
+          if (int r = hip_status(e, "conv slab launch")) return r;
+        }
+        if (bias_act && act_transcendental(activation)) {
+          OpTimer t(c, TNS_OP_ACTIVATE);
+          return hip_status(launch_activate(out, batch * filters * outImg, activation, c->stream),
+                            "activate launch");
+        }
+        return TNS_OK;
+      }
+    }
     // tiles with a bounds-checked gather from the unpadded images where they
     // apply: the LDS-DMA ring (conv_dma.hip), the ping-pong schedule
     // (conv_pp.hip) or the plane-sized lock-step tiles (conv_tile.hip);
@@ -2209,6 +2243,8 @@ int tns_hip_conv_backward_bn(tns_ctx* c, int64_t batch, int64_t C, int64_t H, in
 int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
+int tns_conv_slab_count(void) { return conv_slab_count(); }
+const char* tns_conv_slab_name(int32_t v) { return conv_slab_name(v); }
 int tns_conv_dx_tile_count(void) { return conv_tile4_ta_count(); }
 int tns_conv_dx_conv_count(void) { return conv_tile4_dx3_count(); }
 int tns_conv_dw_res_count(void) { return dw_res_count(); }

@@ -130,6 +130,22 @@ int conv_tile_count();
 const char* conv_tile_name(int v);
 int conv_tile_pick(const GemmArgs& a, int ks);
 hipError_t launch_conv_tile(int v, const GemmArgs& a, int ks, int dil, hipStream_t s);
+// two-pass conv forward (conv_slab.hip): the im2col matrix written once in
+// the GEMM's LDS slot order, then a GEMM with B by LDS-DMA; form v of
+// conv_slab_count(); conv_slab_pick = -1 where conv_tile4 stays
+struct ConvSlabArgs {
+  const float* input;    // [batch][C][H][W]
+  const float* weights;  // [M][K], K = C*ks*ks
+  const float* bias;     // fused bias + activation when not null
+  float* out;            // [batch][M][oh*ow]
+  int64_t batch, C, H, W, M, K, ks, stride, pad, dil, ow, ohw;
+  int act;
+};
+int conv_slab_count();
+const char* conv_slab_name(int v);
+int conv_slab_pick(int64_t M, int64_t N, int64_t K, int64_t ks);
+int64_t conv_slab_floats(int v, int64_t N, int64_t K);  // slab scratch, -1: no such form
+hipError_t launch_conv_slab(int v, const ConvSlabArgs& c, float* slab, hipStream_t s);
 // the same tiles with k-permuted LDS images read by ds_read_b128
 // (conv_tile4.hip; K % the form's k-tile == 0): conv_tile variants
 // conv_tile_count() - conv_tile4_count() + v

@@ -399,6 +399,10 @@ class TNNHip:
         """k-major-A conv tiles of the backward's col = W^T . delta."""
         return int(self.lib.tns_conv_dx_tile_count())
 
+    def convSlabForms(self) -> int:
+        """Two-pass slab conv forms (setConvVariant(500 + v))."""
+        return int(self.lib.tns_conv_slab_count())
+
     def convTileVariants(self) -> int:
         """Plane-sized implicit-conv tiles (setConvVariant(100 + v))."""
         return int(self.lib.tns_conv_tile_variant_count())

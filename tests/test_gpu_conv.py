@@ -1008,3 +1008,39 @@ def test_conv_patch_variants_bit_exact(hip, torch_cuda, ora):
     finally:
         hip.setConvVariant(-1)
     assert ran >= 2 * nv
+
+
+SLAB_CASES = [
+    # (batch, C, H, F, k, s, p, act): YOLOv3 13^2 / 26^2 layers at batch 8
+    # (layers 45, 43, 28, 26, 44) and ragged / small ones (N past the last
+    # column tile, one and two k-tiles)
+    (8, 512, 13, 1024, 3, 1, 1, 9), (8, 256, 26, 1024, 3, 2, 1, 9), (8, 256, 26, 512, 3, 1, 1, 9),
+    (8, 256, 52, 512, 3, 2, 1, 9), (8, 1024, 13, 512, 1, 1, 0, 9), (3, 64, 7, 128, 3, 1, 1, 1),
+    (2, 16, 9, 64, 3, 1, 1, 4), (1, 128, 5, 64, 1, 1, 0, 0)]
+
+
+def test_conv_slab_forms_bit_exact(hip, torch_cuda, ora):
+    """Every two-pass slab form (conv_slab.hip, TNS_OPT_CONV_VARIANT = 500 +
+    v: the im2col matrix written in the GEMM's LDS slot order, B by LDS-DMA)
+    at the YOLOv3 13^2 / 26^2 shapes and ragged small ones, fused bias +
+    leaky/relu/linear and the separate logistic pass: bit-identical to the
+    oracle; forms whose tiles do not divide the filters / k report
+    UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.convSlabForms()
+    assert nv >= 2
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setConvVariant(500 + v)
+            for i, (batch, C, H, F, k, s, p, act) in enumerate(SLAB_CASES):
+                try:
+                    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, k, s, p, act, 3,
+                                         seed=40 + i)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, batch, C, H, F, k, s, p, act)
+    finally:
+        hip.setConvVariant(-1)
+    assert ran >= 3 * nv
