@@ -433,19 +433,14 @@ hipError_t launch_slab_fill(const SlabFillArgs& a, int ks, hipStream_t s) {
    "conv_slab<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",j" #JAv "x" #NAv ",s" #NSv ",dg" #DGv \
    ",map" #MAPv ">"}
 const SlabForm kSlab[] = {
-    TNS_SLAB(32, 176, 64, 2, 4, 3, 3, 3),   // 0: 13^2 planes, 1024 filters (8 x 32 blocks)
-    TNS_SLAB(64, 176, 32, 4, 2, 6, 1, 3),   // 1: 26^2 planes, 512 filters (31 x 8 blocks)
+    TNS_SLAB(32, 176, 64, 2, 4, 3, 3, 3),   // 0: form 3 with three stages (DMA two tiles ahead)
+    TNS_SLAB(64, 176, 32, 4, 2, 6, 1, 3),   // 1
     TNS_SLAB(64, 176, 32, 4, 2, 6, 1, 4),   // 2
-    TNS_SLAB(32, 176, 64, 2, 4, 3, 3, 2),   // 3: two stages
-    TNS_SLAB(64, 176, 64, 4, 2, 6, 1, 2),   // 4
+    TNS_SLAB(32, 176, 64, 2, 4, 3, 3, 2),   // 3: the 13^2 planes (8 x 32 blocks) — picked
+    TNS_SLAB(64, 176, 64, 4, 2, 6, 1, 2),   // 4: the 26^2 planes (31 x 8 blocks) — picked
     TNS_SLAB(32, 176, 32, 2, 2, 6, 1, 4),   // 5: one wave per SIMD
     TNS_SLABD(32, 176, 64, 2, 4, 3, 3, 2, 0, 1),  // 6: form 3, row tiles outer
     TNS_SLABD(64, 176, 64, 4, 2, 6, 1, 2, 0, 1),  // 7: form 4, row tiles outer
-    TNS_SLABD(32, 176, 64, 2, 4, 3, 3, 2, 1, 0),  // 8: form 3 diag: no B DMA
-    TNS_SLABD(32, 176, 64, 2, 4, 3, 3, 2, 2, 0),  // 9: no A
-    TNS_SLABD(32, 176, 64, 2, 4, 3, 3, 2, 4, 0),  // 10: no barrier
-    TNS_SLABD(32, 176, 64, 2, 4, 3, 3, 2, 7, 0),  // 11: none of them
-    TNS_SLABD(64, 176, 64, 4, 2, 6, 1, 2, 7, 0),  // 12: form 4, none of them
 };
 #undef TNS_SLAB
 #undef TNS_SLABD
@@ -456,9 +451,16 @@ constexpr int kNumSlab = sizeof(kSlab) / sizeof(kSlab[0]);
 int conv_slab_count() { return kNumSlab; }
 const char* conv_slab_name(int v) { return v >= 0 && v < kNumSlab ? kSlab[v].name : ""; }
 
-// the form for a layer, -1: conv_tile4 stays (none picked by default yet)
+// the form for a layer, -1: conv_tile4 stays.  Measured at batch 8, warm
+// clock, kernel trace (scripts/slab_prof.sh, profiles/r06_conv_slab.json):
+// the 13^2 planes (1024 filters, K = 4608 / 2304 stride 2) on 32 x 176 x 64
+// (fill 10.1 + GEMM 116.5 us against conv_tile4's 133.7), the 26^2 planes
+// (512 filters, K = 2304) on 64 x 176 x 64 (15.5 + 108.2 against 130.8); the
+// 1x1 layers stay (the fill and the short k: 13^2 0.035 against 0.023 ms)
 int conv_slab_pick(int64_t M, int64_t N, int64_t K, int64_t ks) {
-  (void)M; (void)N; (void)K; (void)ks;
+  if (ks != 3 || K % 64) return -1;
+  if (M == 1024 && N >= 1024) return 3;
+  if (M == 512 && N >= 4096) return 4;
   return -1;
 }
 

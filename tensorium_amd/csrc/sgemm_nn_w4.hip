@@ -205,19 +205,11 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
   // A tile i: row wm*128 + 32 i + lc, chunk (k >> 2) ^ swz, swz = (lc >> 1) & 7
   // B tile j: n = wn*128 + 32 j + lc at LDS column (n - 32 h) & 255 of row k
   const int swz = (lc >> 1) & 7;
-  const int a_lane = (wm * 128 + lc) * BK + h;
   int b_col[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
     b_col[j] = A_TILE + h * BN + ((wn * 128 + 4 * lc + j - 32 * h) & 255);
   const float alpha = p.alpha;
-  auto frag = [&](const float* st, int s, float (&a)[4], float (&b)[4]) {
-    const int ka = 4 * ((s >> 1) ^ swz) + 2 * (s & 1);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = st[a_lane + 32 * BK * i + ka];
-    const floatx4 v = *reinterpret_cast<const floatx4*>(st + b_col[0] + 2 * s * BN);
-    b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; b[3] = v[3];
-  };
   auto mma = [&](const float (&a)[4], const float (&b)[4]) {
     float aa[4];
 #pragma unroll
@@ -244,6 +236,14 @@ __global__ __launch_bounds__(NT, 1) void sgemm_nn_w4_kernel(GemmArgs p) {
     }
   };
 
+  const int a_lane = (wm * 128 + lc) * BK + h;
+  auto frag = [&](const float* st, int s, float (&a)[4], float (&b)[4]) {
+    const int ka = 4 * ((s >> 1) ^ swz) + 2 * (s & 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = st[a_lane + 32 * BK * i + ka];
+    const floatx4 v = *reinterpret_cast<const floatx4*>(st + b_col[0] + 2 * s * BN);
+    b[0] = v[0]; b[1] = v[1]; b[2] = v[2]; b[3] = v[3];
+  };
   float a0[4], b0[4], a1[4], b1[4];
   {
     // the barrier that publishes tile t+1 sits before step 15 of tile
