@@ -501,6 +501,10 @@ const char* tns_conv_tile_variant_name(int32_t variant);
  * then B by LDS-DMA (TNS_OPT_CONV_VARIANT = 500 + v) */
 int         tns_conv_slab_count(void);
 const char* tns_conv_slab_name(int32_t variant);
+/* 1x1 stride-1 conv forms reading the input planes by LDS-DMA (planes of a
+ * multiple of 4 pixels; TNS_OPT_CONV_VARIANT = 600 + v) */
+int         tns_conv1x1_count(void);
+const char* tns_conv1x1_name(int32_t variant);
 /* ping-pong implicit-conv tiles (TNS_OPT_CONV_VARIANT = 200 + v) */
 int         tns_conv_pp_variant_count(void);
 const char* tns_conv_pp_variant_name(int32_t variant);
@@ -532,7 +536,8 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * for plane-sized tile v of tns_conv_tile_variant_name, 200 + v for ping-pong
  * tile v of tns_conv_pp_variant_name, 300 + v for LDS-DMA-ring tile v of
  * tns_conv_dma_variant_name, 400 + v for input-patch tile v of
- * tns_conv_patch_variant_name, 500 + v for slab form v of tns_conv_slab_name).
+ * tns_conv_patch_variant_name, 500 + v for slab form v of tns_conv_slab_name,
+ * 600 + v for 1x1 form v of tns_conv1x1_name).
  * TNS_OPT_CONV_PAD (default -1 = by cost): 1 gathers from a zero-padded copy
  * of the images, 0 bounds-checks the window inside the GEMM.
  * TNS_OPT_NT_SDOT (default 1): gemm(NoTrans, Trans) sums in the reference's

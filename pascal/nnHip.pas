@@ -267,6 +267,8 @@ function tns_conv_dw_tile_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_count(): longint; cdecl; external libtns;
 function tns_conv_tile_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_conv_slab_count(): longint; cdecl; external libtns;
+function tns_conv1x1_count(): longint; cdecl; external libtns;
+function tns_conv1x1_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_conv_slab_name(variant: longint): PAnsiChar; cdecl; external libtns;
 function tns_conv_pp_variant_count(): longint; cdecl; external libtns;
 function tns_conv_pp_variant_name(variant: longint): PAnsiChar; cdecl; external libtns;

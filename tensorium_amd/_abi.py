@@ -114,6 +114,8 @@ PROTOTYPES: dict[str, tuple] = {
     "tns_conv_dw_tile_count": (C.c_int, []),
     "tns_conv_tile_variant_name": (C.c_char_p, [C.c_int32]),
     "tns_conv_slab_count": (C.c_int, []),
+    "tns_conv1x1_count": (C.c_int, []),
+    "tns_conv1x1_name": (C.c_char_p, [C.c_int32]),
     "tns_conv_slab_name": (C.c_char_p, [C.c_int32]),
     "tns_conv_pp_variant_count": (C.c_int, []),
     "tns_conv_pp_variant_name": (C.c_char_p, [C.c_int32]),

@@ -1562,12 +1562,41 @@ int conv_forward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t W
                                            ow, activation, c->stream),
                         "direct conv launch");
     }
+    // 1x1 / stride-1 layers straight from the input planes (conv1x1.hip)
+    // where picked, or forced by TNS_OPT_CONV_VARIANT = 600 + v
+    if (kSize == 1 && stride == 1 && padding == 0 && dilation == 1) {
+      int cv = -1;
+      if (g_conv_variant >= 600)
+        cv = (int)(g_conv_variant - 600);
+      else if (g_conv_variant < 0)
+        cv = conv1x1_pick(filters, batch * outImg, k, outImg);
+      if (cv >= 0) {
+        {
+          OpTimer t(c, TNS_OP_GEMM);
+          const hipError_t e = launch_conv1x1(cv, weights, input, bias_act ? biases : nullptr, out,
+                                              batch, filters, k, outImg,
+                                              act_transcendental(activation) ? 4 : activation,
+                                              c->stream);
+          if (e == hipErrorInvalidValue)
+            return set_error(TNS_ERR_UNSUPPORTED, "conv1x1 form %d does not fit this layer", cv);
+          if (int r = hip_status(e, "conv1x1 launch")) return r;
+        }
+        if (bias_act && act_transcendental(activation)) {
+          OpTimer t(c, TNS_OP_ACTIVATE);
+          return hip_status(launch_activate(out, batch * filters * outImg, activation, c->stream),
+                            "activate launch");
+        }
+        return TNS_OK;
+      }
+    } else if (g_conv_variant >= 600) {
+      return set_error(TNS_ERR_UNSUPPORTED, "conv1x1 forms need a 1x1 stride-1 unpadded layer");
+    }
     // the two-pass slab form (conv_slab.hip) where picked, or forced by
     // TNS_OPT_CONV_VARIANT = 500 + v
     {
       const int64_t N = batch * outImg;
       int sv = -1;
-      if (g_conv_variant >= 500)
+      if (g_conv_variant >= 500 && g_conv_variant < 600)
         sv = (int)(g_conv_variant - 500);
       else if (g_conv_variant < 0 && dilation == 1)
         sv = conv_slab_pick(filters, N, k, kSize);
@@ -2244,6 +2273,8 @@ int tns_gemm_variant_count(void) { return sgemm_variant_count(); }
 int tns_sdot_chains_variant_count(void) { return sdot_chains_variant_count(); }
 int tns_conv_tile_variant_count(void) { return conv_tile_count(); }
 int tns_conv_slab_count(void) { return conv_slab_count(); }
+int tns_conv1x1_count(void) { return conv1x1_count(); }
+const char* tns_conv1x1_name(int32_t v) { return conv1x1_name(v); }
 const char* tns_conv_slab_name(int32_t v) { return conv_slab_name(v); }
 int tns_conv_dx_tile_count(void) { return conv_tile4_ta_count(); }
 int tns_conv_dx_conv_count(void) { return conv_tile4_dx3_count(); }

@@ -141,6 +141,15 @@ struct ConvSlabArgs {
   int64_t batch, C, H, W, M, K, ks, stride, pad, dil, ow, ohw;
   int act;
 };
+// 1x1 / stride-1 layers with a multiple of 4 pixels per plane straight from
+// the input planes (conv1x1.hip, B by LDS-DMA): form v of conv1x1_count();
+// conv1x1_pick = -1 where the other paths stay
+int conv1x1_count();
+const char* conv1x1_name(int v);
+int conv1x1_pick(int64_t M, int64_t N, int64_t K, int64_t P);
+hipError_t launch_conv1x1(int v, const float* weights, const float* x, const float* bias,
+                          float* out, int64_t batch, int64_t M, int64_t K, int64_t P, int act,
+                          hipStream_t s);
 int conv_slab_count();
 const char* conv_slab_name(int v);
 int conv_slab_pick(int64_t M, int64_t N, int64_t K, int64_t ks);

@@ -399,6 +399,10 @@ class TNNHip:
         """k-major-A conv tiles of the backward's col = W^T . delta."""
         return int(self.lib.tns_conv_dx_tile_count())
 
+    def conv1x1Forms(self) -> int:
+        """1x1 conv forms reading the input planes by DMA (setConvVariant(600 + v))."""
+        return int(self.lib.tns_conv1x1_count())
+
     def convSlabForms(self) -> int:
         """Two-pass slab conv forms (setConvVariant(500 + v))."""
         return int(self.lib.tns_conv_slab_count())

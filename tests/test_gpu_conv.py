@@ -1044,3 +1044,40 @@ def test_conv_slab_forms_bit_exact(hip, torch_cuda, ora):
     finally:
         hip.setConvVariant(-1)
     assert ran >= 3 * nv
+
+
+C1_CASES = [
+    # (batch, C, H, F, act): YOLOv3 1x1 layers at batch 8 — 208^2 (2), 104^2
+    # (5), 52^2 (10, 68: 384 channels, 74: the 255-filter head), 26^2 (27, 60,
+    # 66: head) — and ragged small ones (N past the last column tile, one k-tile)
+    (8, 64, 208, 32, 9), (8, 128, 104, 64, 9), (8, 256, 52, 128, 9), (8, 384, 52, 128, 9),
+    (8, 256, 52, 255, 4), (8, 512, 26, 256, 9), (8, 768, 26, 256, 9), (8, 512, 26, 255, 4),
+    (3, 64, 6, 48, 1), (1, 32, 2, 16, 0), (2, 128, 10, 40, 9)]
+
+
+def test_conv1x1_forms_bit_exact(hip, torch_cuda, ora):
+    """Every DMA-fed 1x1 form (conv1x1.hip, TNS_OPT_CONV_VARIANT = 600 + v:
+    the input planes straight into LDS, interleaved fragment columns, 16-byte
+    output stores) at the YOLOv3 1x1 shapes — filter counts that are not a
+    multiple of the block (the 255-filter heads) included — and small ragged
+    ones, fused bias + leaky/relu/linear and the separate logistic pass:
+    bit-identical to the oracle; forms whose k-tile does not divide k report
+    UNSUPPORTED."""
+    from tensorium_amd._abi import TnsError
+    nv = hip.conv1x1Forms()
+    assert nv >= 2
+    ran = 0
+    try:
+        for v in range(nv):
+            hip.setConvVariant(600 + v)
+            for i, (batch, C, H, F, act) in enumerate(C1_CASES):
+                try:
+                    got, ref = conv_case(hip, torch_cuda, ora, batch, C, H, F, 1, 1, 0, act, 3,
+                                         seed=70 + i)
+                except TnsError:
+                    continue
+                ran += 1
+                assert np.array_equal(got, ref), (v, batch, C, H, F, act)
+    finally:
+        hip.setConvVariant(-1)
+    assert ran >= 6 * nv
