@@ -235,7 +235,8 @@ __global__ void normalize_delta_k(const float* __restrict__ x, const float* __re
                                   const float* __restrict__ var,
                                   const float* __restrict__ mean_delta,
                                   const float* __restrict__ var_delta, float* __restrict__ delta,
-                                  int64_t total, int64_t N, int64_t bs, float B) {
+                                  int64_t total, int64_t N, int64_t bs, float B,
+                                  const float* __restrict__ scales) {
   for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * TPB) {
     const int64_t i = (e / bs) % N;
@@ -243,7 +244,7 @@ __global__ void normalize_delta_k(const float* __restrict__ x, const float* __re
     const float vd = 2.0f * var_delta[i] / B;
     const float ve = var[i] > SEPS ? var[i] : SEPS;
     const float sd = sqrtf(ve);
-    const float a = delta[e] / sd;
+    const float a = (scales ? delta[e] * scales[i] : delta[e]) / sd;
     const float t = (x[e] - mean[i]) * vd + md;  // sNormalizeDelta_avx order
     delta[e] = a + t;
   }
@@ -306,7 +307,14 @@ __global__ void vssum_k(int64_t n, const float* __restrict__ a, float* __restric
 // fused into its bias sums: a = delta (each derived term also written back
 // through wa), b = output, act = the activation; the same product as
 // derive4_kernel, the same chains as CH_SUM
-enum ChainMode { CH_SUM = 0, CH_SRSS = 1, CH_VDELTA = 2, CH_DOT = 3, CH_DSUM = 4 };
+// CH_DDOT: CH_DOT (addDots) over delta * f'(output) and x_norm — the BN
+// conv backward's Derivative fused into its addDots: a = delta (each derived
+// term written back through wa), b = x_norm, c3 = output.
+// sc (CH_VDELTA): the per-channel scales of forwardScale applied to each delta
+// term as it is staged (one rounding, as the separate pass would store it) —
+// the BN conv backward's forwardScale folded into MeansAndVarsDelta (and
+// normalizeDelta), the scaled delta never written
+enum ChainMode { CH_SUM = 0, CH_SRSS = 1, CH_VDELTA = 2, CH_DOT = 3, CH_DSUM = 4, CH_DDOT = 5 };
 
 template <int MODE, int NT, int E>
 __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
@@ -315,10 +323,13 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
                                                    int64_t nblocks, int64_t N, int64_t bs,
                                                    int quirk, float* __restrict__ part0,
                                                    float* __restrict__ part1, int act,
-                                                   float* wa) {
+                                                   float* wa, const float* __restrict__ c3,
+                                                   const float* __restrict__ sc_arr) {
   constexpr int TILE = NT * E;
-  constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;  // two LDS streams
-  constexpr bool LB = TWO || MODE == CH_DSUM;                // b loaded
+  constexpr bool DOTF = MODE == CH_DOT || MODE == CH_DDOT;    // the fma chains
+  constexpr bool TWO = MODE == CH_VDELTA || DOTF;             // two LDS streams
+  constexpr bool LB = TWO || MODE == CH_DSUM;                 // b loaded
+  constexpr bool LC = MODE == CH_DDOT;                        // c3 loaded
   // tiles stored lane-major: element e of the tile at (e & 7) * LDT + e / 8,
   // so a chain lane's consecutive terms are contiguous (ds_read_b128 reads
   // four); rows padded by 8 floats (conflict-free staging stores)
@@ -335,9 +346,12 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
     const int64_t i = blk % N;
     const float* pa = a + blk * bs;
     const float* pb = LB ? b + blk * bs : nullptr;
-    float* pw = MODE == CH_DSUM ? wa + blk * bs : nullptr;
+    const float* pc = LC ? c3 + blk * bs : nullptr;
+    float* pw = (MODE == CH_DSUM || MODE == CH_DDOT) ? wa + blk * bs : nullptr;
     const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA) ? mu_arr[i] : 0.0f;
-    float ra[E], rb[LB ? E : 1];
+    const bool scaled = MODE == CH_VDELTA && sc_arr != nullptr;
+    const float scl = scaled ? sc_arr[i] : 1.0f;
+    float ra[E], rb[LB ? E : 1], rc[LC ? E : 1];
     auto load = [&](int t) {
       const int64_t base = (int64_t)t * TILE + tid;
 #pragma unroll
@@ -345,6 +359,7 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
         const int64_t k = base + NT * u;
         ra[u] = k < nb8 ? pa[k] : 0.0f;
         if constexpr (LB) rb[u] = k < nb8 ? pb[k] : 0.0f;
+        if constexpr (LC) rc[u] = k < nb8 ? pc[k] : 0.0f;
       }
     };
     auto store = [&](int buf, int t) {
@@ -356,14 +371,21 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
           U[buf][e] = d;
           const int64_t k = (int64_t)t * TILE + tid + NT * u;
           if (k < nb8) pw[k] = d;
+        } else if constexpr (MODE == CH_DDOT) {
+          const float d = ra[u] * grad_apply(rc[u], act);
+          U[buf][e] = d;
+          V[buf][e] = rb[u];
+          const int64_t k = (int64_t)t * TILE + tid + NT * u;
+          if (k < nb8) pw[k] = d;
         } else if constexpr (MODE == CH_SUM) {
           U[buf][e] = ra[u];
         } else if constexpr (MODE == CH_SRSS) {  // srss: vsubps (mean - a), vmulps
           const float d = mu - ra[u];
           U[buf][e] = d * d;
         } else if constexpr (MODE == CH_VDELTA) {  // a = delta, b = x
-          U[buf][e] = ra[u];
-          V[buf][e] = (rb[u] - mu) * ra[u];
+          const float d = scaled ? ra[u] * scl : ra[u];
+          U[buf][e] = d;
+          V[buf][e] = (rb[u] - mu) * d;
         } else {
           U[buf][e] = ra[u];
           V[buf][e] = rb[u];
@@ -391,19 +413,19 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
           for (int z = 0; z < 16; z += 4) {
             const float4 x4 = *reinterpret_cast<const float4*>(row + q + z);
             v[z] = x4.x; v[z + 1] = x4.y; v[z + 2] = x4.z; v[z + 3] = x4.w;
-            if constexpr (MODE == CH_DOT) {
+            if constexpr (DOTF) {
               const float4 y4 = *reinterpret_cast<const float4*>(rowb + q + z);
               w[z] = y4.x; w[z + 1] = y4.y; w[z + 2] = y4.z; w[z + 3] = y4.w;
             }
           }
 #pragma unroll
           for (int z = 0; z < 16; ++z) {
-            if constexpr (MODE == CH_DOT) acc = fmaf(v[z], w[z], acc);
+            if constexpr (DOTF) acc = fmaf(v[z], w[z], acc);
             else acc = acc + v[z];
           }
         }
         for (; q < cnt; ++q) {
-          if constexpr (MODE == CH_DOT) acc = fmaf(row[q], rowb[q], acc);
+          if constexpr (DOTF) acc = fmaf(row[q], rowb[q], acc);
           else acc = acc + row[q];
         }
       }
@@ -416,10 +438,16 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
       //   lane 0, hadd, hadd
       // sdot_avx2: masked-FMA tail into lanes 0..tail-1, fold, hadd, hadd
       const bool lanes_form = MODE == CH_SRSS || (MODE == CH_VDELTA && grp == 1);
-      if constexpr (MODE == CH_DOT) {
+      if constexpr (DOTF) {
         if (tail && grp == 0) {
-          const float xa = l < tail ? pa[nb8 + l] : 0.0f;
+          float xa = l < tail ? pa[nb8 + l] : 0.0f;
           const float xb = l < tail ? pb[nb8 + l] : 0.0f;
+          if constexpr (MODE == CH_DDOT) {
+            if (l < tail) {
+              xa = xa * grad_apply(pc[nb8 + l], act);
+              pw[nb8 + l] = xa;
+            }
+          }
           acc = fmaf(xa, xb, acc);
         }
       }
@@ -431,7 +459,8 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
             const float d = mu - pa[nb8 + k];
             x0 = x0 + d * d;
           } else {
-            x0 = x0 + (pb[nb8 + k] - mu) * pa[nb8 + k];
+            const float d = scaled ? pa[nb8 + k] * scl : pa[nb8 + k];
+            x0 = x0 + (pb[nb8 + k] - mu) * d;
           }
         }
       const float h = x0 + __shfl_down(x0, 1, 8);
@@ -443,8 +472,8 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
             pw[nb8 + k] = d;
             r = r + d;
           }
-        } else if (!lanes_form && MODE != CH_DOT) {
-          for (int k = 0; k < tail; ++k) r = r + pa[nb8 + k];
+        } else if (!lanes_form && !DOTF) {
+          for (int k = 0; k < tail; ++k) r = r + (scaled ? pa[nb8 + k] * scl : pa[nb8 + k]);
         }
         if (grp == 0) part0[blk] = r;
         else part1[blk] = r;
@@ -472,7 +501,10 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
                                                        int64_t nblocks, int64_t N, int64_t bs,
                                                        int quirk, float* __restrict__ part0,
                                                        float* __restrict__ part1, int act,
-                                                       float* wa) {
+                                                       float* wa, const float* __restrict__ c3,
+                                                       const float* __restrict__ sc_arr) {
+  static_assert(MODE != CH_DDOT, "the specialised-wave form stages two load streams");
+  (void)c3;
   constexpr int SNT = 192, E = 32, TILE = SNT * E, NBUF = 3;
   constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;
   constexpr bool LB = TWO || MODE == CH_DSUM;
@@ -497,6 +529,8 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
     const float* pb = LB ? b + blk * bs : nullptr;
     float* pw = MODE == CH_DSUM ? wa + blk * bs : nullptr;
     const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA) ? mu_arr[i] : 0.0f;
+    const bool scaled = MODE == CH_VDELTA && sc_arr != nullptr;
+    const float scl = scaled ? sc_arr[i] : 1.0f;
     float acc = 0.0f;
     if (!chainwave) {
       // float4 staging where the block is 16-byte aligned (nb8 % 8 == 0: a
@@ -547,8 +581,9 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
               const float d = mu - va;
               U[buf][e] = d * d;
             } else if constexpr (MODE == CH_VDELTA) {  // a = delta, b = x
-              U[buf][e] = va;
-              V[buf][e] = (rb[4 * u + c] - mu) * va;
+              const float d = scaled ? va * scl : va;
+              U[buf][e] = d;
+              V[buf][e] = (rb[4 * u + c] - mu) * d;
             } else {
               U[buf][e] = va;
               V[buf][e] = rb[4 * u + c];
@@ -687,7 +722,8 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
             const float d = mu - pa[nb8 + k];
             x0 = x0 + d * d;
           } else {
-            x0 = x0 + (pb[nb8 + k] - mu) * pa[nb8 + k];
+            const float d = scaled ? pa[nb8 + k] * scl : pa[nb8 + k];
+            x0 = x0 + (pb[nb8 + k] - mu) * d;
           }
         }
       const float h = x0 + __shfl_down(x0, 1, 8);
@@ -700,7 +736,7 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
             r = r + d;
           }
         } else if (!lanes_form && MODE != CH_DOT) {
-          for (int k = 0; k < tail; ++k) r = r + pa[nb8 + k];
+          for (int k = 0; k < tail; ++k) r = r + (scaled ? pa[nb8 + k] * scl : pa[nb8 + k]);
         }
         if (grp == 0) part0[blk] = r;
         else part1[blk] = r;
@@ -740,18 +776,23 @@ __global__ void chains_finish(const float* __restrict__ part0, const float* __re
 template <int MODE>
 hipError_t run_chains(const float* a, const float* b, const float* mu, int64_t groups, int64_t N,
                       int64_t bs, int quirk, float* part0, float* part1, hipStream_t s,
-                      int act = 0, float* wa = nullptr) {
+                      int act = 0, float* wa = nullptr, const float* c3 = nullptr,
+                      const float* sc = nullptr) {
   const int64_t nblocks = groups * N;
   const unsigned grid = (unsigned)(nblocks < (1 << 20) ? nblocks : (1 << 20));
-  if (bs >= 16384)
-    hipLaunchKernelGGL((block_chains_ws<MODE>), dim3(grid), dim3(256), 0, s, a, b, mu, nblocks,
-                       N, bs, quirk, part0, part1, act, wa);
-  else if (bs >= 4096)
+  if constexpr (MODE != CH_DDOT) {
+    if (bs >= 16384) {
+      hipLaunchKernelGGL((block_chains_ws<MODE>), dim3(grid), dim3(256), 0, s, a, b, mu, nblocks,
+                         N, bs, quirk, part0, part1, act, wa, c3, sc);
+      return hipGetLastError();
+    }
+  }
+  if (bs >= 4096)
     hipLaunchKernelGGL((block_chains<MODE, 256, 16>), dim3(grid), dim3(256), 0, s, a, b, mu,
-                       nblocks, N, bs, quirk, part0, part1, act, wa);
+                       nblocks, N, bs, quirk, part0, part1, act, wa, c3, sc);
   else
     hipLaunchKernelGGL((block_chains<MODE, 64, 8>), dim3(grid), dim3(64), 0, s, a, b, mu, nblocks,
-                       N, bs, quirk, part0, part1, act, wa);
+                       N, bs, quirk, part0, part1, act, wa, c3, sc);
   return hipGetLastError();
 }
 
@@ -766,6 +807,9 @@ hipError_t run_finish(const float* part0, const float* part1, int64_t groups, in
 // blocks long enough for the chain kernels (shorter ones: one thread per
 // channel, which is also the only form for blockSize 1)
 bool use_chains(int64_t bs, const float* part) { return part != nullptr && bs >= 64; }
+}  // namespace
+bool bn_folds_scale(int64_t bs) { return use_chains(bs, reinterpret_cast<const float*>(1)); }
+namespace {
 
 // ---- conv layer batch norm, forward (TBaseLayer.batchNorm + activate) -----
 // One pass instead of the reference's six (CopyTo(x), blockNormalize,
@@ -855,10 +899,13 @@ template <int V>
 __global__ __launch_bounds__(TPB) void normalize_delta_rows(
     const float* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ var,
     const float* __restrict__ mean_delta, const float* __restrict__ var_delta,
-    float* __restrict__ delta, int64_t N, int64_t bs, int bpr, float B) {
+    float* __restrict__ delta, int64_t N, int64_t bs, int bpr, float B,
+    const float* __restrict__ scales) {
   int64_t row, i;
   int seg;
   row_of(bpr, N, row, i, seg);
+  const bool scaled = scales != nullptr;  // (forwardScale folded in: delta * scale first)
+  const float scl = scaled ? scales[i] : 1.0f;
   const float md = mean_delta[i] / B;
   const float vd = 2.0f * var_delta[i] / B;
   const float ve = var[i] > SEPS ? var[i] : SEPS;
@@ -874,7 +921,8 @@ __global__ __launch_bounds__(TPB) void normalize_delta_rows(
     ld<V>(x + base + j, xv);
 #pragma unroll
     for (int c = 0; c < V; ++c) {
-      const float a = d[c] / sd;
+      const float dv = scaled ? d[c] * scl : d[c];
+      const float a = dv / sd;
       const float t = (xv[c] - m) * vd + md;  // sNormalizeDelta_avx order
       d[c] = a + t;
     }
@@ -1137,26 +1185,47 @@ hipError_t launch_derive_add_sums(float* dst, float* delta, const float* output,
   return run_finish<FIN_ADD>(part, nullptr, groups, N, bs, nullptr, dst, nullptr, s);
 }
 
+// the BN conv backward's Derivative and addDots in one pass (CH_DDOT): delta
+// *= f'(output) written back, dst += sum x_norm * delta in the sdot order;
+// the planes of >= 16384 pixels (the specialised-wave chain form stages two
+// streams) and the short blocks keep the two passes
+hipError_t launch_add_dots_derive(float* dst, const float* x_norm, float* delta,
+                                  const float* output, int act, int64_t groups, int64_t N,
+                                  int64_t bs, float* part, hipStream_t s) {
+  if (N <= 0 || groups <= 0 || bs <= 0) return hipSuccess;
+  if (act == TNS_acLINEAR || bs >= 16384 || !use_chains(bs, part)) {
+    if (hipError_t e = launch_derive(output, groups * N * bs, act, delta, s)) return e;
+    return launch_add_dots(dst, x_norm, delta, groups, N, bs, part, s);
+  }
+  if (hipError_t e = run_chains<CH_DDOT>(delta, x_norm, nullptr, groups, N, bs, 0, part, nullptr,
+                                         s, act, delta, output))
+    return e;
+  return run_finish<FIN_ADD>(part, nullptr, groups, N, bs, nullptr, dst, nullptr, s);
+}
 hipError_t launch_mean_var_delta(const float* delta, const float* x, const float* mean,
                                  const float* var, int64_t groups, int64_t N, int64_t bs,
                                  float* mean_delta, float* var_delta, int quirk, float* part,
-                                 hipStream_t s) {
+                                 hipStream_t s, const float* scales) {
   if (N <= 0) return hipSuccess;
+  // (the one-thread-per-channel form has no folded scale: the caller runs
+  // forwardScale first there — bn_folds_scale says which)
+  if (scales && !use_chains(bs, part)) return hipErrorInvalidValue;
   if (!use_chains(bs, part)) {
     hipLaunchKernelGGL(mean_var_delta_seq, dim3(nblk(N)), dim3(TPB), 0, s, delta, x, mean, var,
                        groups, N, bs, mean_delta, var_delta, quirk);
     return hipGetLastError();
   }
   float* part1 = part + groups * N;
-  if (hipError_t e =
-          run_chains<CH_VDELTA>(delta, x, mean, groups, N, bs, quirk, part, part1, s))
+  if (hipError_t e = run_chains<CH_VDELTA>(delta, x, mean, groups, N, bs, quirk, part, part1, s,
+                                           0, nullptr, nullptr, scales))
     return e;
   return run_finish<FIN_VDELTA>(part, part1, groups, N, bs, var, mean_delta, var_delta, s);
 }
 
 hipError_t launch_normalize_delta(const float* x, const float* mean, const float* var,
                                   const float* mean_delta, const float* var_delta, float* delta,
-                                  int64_t groups, int64_t N, int64_t bs, hipStream_t s) {
+                                  int64_t groups, int64_t N, int64_t bs, hipStream_t s,
+                                  const float* scales) {
   const int64_t total = groups * N * bs;
   if (total <= 0) return hipSuccess;
   const bool v4 = bs % 4 == 0 && al16(x) && al16(delta);
@@ -1164,15 +1233,15 @@ hipError_t launch_normalize_delta(const float* x, const float* mean, const float
     if (v4)
       hipLaunchKernelGGL(normalize_delta_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
                          s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                         (float)(groups * bs));
+                         (float)(groups * bs), scales);
     else
       hipLaunchKernelGGL(normalize_delta_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
                          s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                         (float)(groups * bs));
+                         (float)(groups * bs), scales);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(normalize_delta_k, dim3(nblk(total)), dim3(TPB), 0, s, x, mean, var,
-                     mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs));
+                     mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs), scales);
   return hipGetLastError();
 }
 

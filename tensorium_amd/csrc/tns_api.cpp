@@ -1917,27 +1917,31 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   float* part;
   if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
   if (bn.scales) {
-    // Derivative(): delta *= f'(output)
-    if (int r = hip_status(launch_derive(output, batch * filters * i_k, activation, delta,
-                                         c->stream), "derive launch"))
+    // Derivative(): delta *= f'(output), then batchNormBack:
+    // scale_updates.addDots(x_norm, delta); delta.forwardScale(scales);
+    // MeansAndVarsDelta; normalizeDelta — and no bias_updates term
+    // (nConvolutionLayer.pas:601-604).  Three passes instead of five: the
+    // derive rides addDots' loads (each derived term written back), and the
+    // scale is applied to each delta term as MeansAndVarsDelta and
+    // normalizeDelta load it (the same one rounding forwardScale would store)
+    if (int r = hip_status(launch_add_dots_derive(bn.scale_updates, bn.x_norm, delta, output,
+                                                  activation, batch, filters, i_k, part,
+                                                  c->stream),
+                           "derive + addDots launch"))
       return r;
-    // batchNormBack: scale_updates.addDots(x_norm, delta); delta.forwardScale
-    // (scales); MeansAndVarsDelta; normalizeDelta — and no bias_updates term
-    // (nConvolutionLayer.pas:601-604)
-    if (int r = hip_status(launch_add_dots(bn.scale_updates, bn.x_norm, delta, batch, filters, i_k,
-                                           part, c->stream), "addDots launch"))
-      return r;
-    if (int r = hip_status(launch_scale_add(delta, batch, filters, i_k, bn.scales, nullptr, 1,
-                                            c->stream), "forwardScale launch"))
-      return r;
+    const float* fold = bn_folds_scale(i_k) ? bn.scales : nullptr;
+    if (!fold)
+      if (int r = hip_status(launch_scale_add(delta, batch, filters, i_k, bn.scales, nullptr, 1,
+                                              c->stream), "forwardScale launch"))
+        return r;
     if (int r = hip_status(launch_mean_var_delta(delta, bn.x, bn.mean, bn.variance, batch, filters,
                                                  i_k, bn.mean_delta, bn.variance_delta,
-                                                 (int)g_srss_quirk, part, c->stream),
+                                                 (int)g_srss_quirk, part, c->stream, fold),
                            "meansAndVarsDelta launch"))
       return r;
     if (int r = hip_status(launch_normalize_delta(bn.x, bn.mean, bn.variance, bn.mean_delta,
                                                   bn.variance_delta, delta, batch, filters, i_k,
-                                                  c->stream), "normalizeDelta launch"))
+                                                  c->stream, fold), "normalizeDelta launch"))
       return r;
   } else {
     // Derivative(): delta *= f'(output), then bias_updates.addSums(delta) —

@@ -367,10 +367,18 @@ hipError_t launch_derive_add_sums(float* dst, float* delta, const float* output,
 hipError_t launch_mean_var_delta(const float* delta, const float* x, const float* mean,
                                  const float* var, int64_t groups, int64_t N, int64_t bs,
                                  float* mean_delta, float* var_delta, int quirk, float* part,
-                                 hipStream_t s);
+                                 hipStream_t s, const float* scales = nullptr);
 hipError_t launch_normalize_delta(const float* x, const float* mean, const float* var,
                                   const float* mean_delta, const float* var_delta, float* delta,
-                                  int64_t groups, int64_t N, int64_t bs, hipStream_t s);
+                                  int64_t groups, int64_t N, int64_t bs, hipStream_t s, const float* scales = nullptr); 
+// whether launch_mean_var_delta / launch_normalize_delta can fold the BN
+// scales into their loads for planes of bs pixels (else forwardScale first)
+bool bn_folds_scale(int64_t bs);
+// the BN conv backward's Derivative + addDots in one pass where the chain
+// kernels allow (else the two passes)
+hipError_t launch_add_dots_derive(float* dst, const float* x_norm, float* delta,
+                                  const float* output, int act, int64_t groups, int64_t N,
+                                  int64_t bs, float* part, hipStream_t s);
 // fused conv-layer BN forward: x := y, xn := normalize(y), out :=
 // act(xn*scale + bias); x / xn may be nullptr (inference); out may alias y
 hipError_t launch_bn_apply(const float* y, float* x, float* xn, float* out, int64_t groups,
