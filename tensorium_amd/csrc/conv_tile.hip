@@ -320,20 +320,8 @@ const TileInfo kTiles[] = {
 };
 #undef TNS_CT
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
-// the conv_tile4.hip forms picked by default (TNS_CT4_AR: their A-in-
-// registers twins, diagnostics builds only — measured slower, conv_tile4.hip)
-#if defined(TNS_CT4_AR) && !defined(TNS_DIAG_KERNELS)
-#error "TNS_CT4_AR selects kTiles4 forms 46..50, which exist only in the diagnostics build (TNS_DIAG=1)"
-#endif
-#ifdef TNS_CT4_AR
-constexpr int kT4OneByOnePF = 48;
-constexpr int kT4UnevenS2 = 49;
-constexpr int kT4Big = 46;       // (3) 128 x 176 x 64, stores after group 1, reads interleaved
-constexpr int kT4Small = 47;     // (8) 64 x 96 x 32, reads interleaved
-constexpr int kT4OneByOne = 48;  // (13) 64 x 32 x 32, 4 waves (1x1 layers)
-constexpr int kT4Uneven = 49;    // (18) 64 x 176 x 32, wave columns 6 + 5 fragments
-constexpr int kT4Narrow = 50;    // (21) 128 x 48 x 64, stores and reads interleaved
-#elif !defined(TNS_CT4_NO_PF)
+// the conv_tile4.hip forms picked by default
+#ifndef TNS_CT4_NO_PF
 // the 2-group 26^2 and the 13^2 forms as their loads-two-tiles-ahead twins
 // (PF); the others keep one register set (PF: 128 x 176 spills, 64 x 96 and
 // 64 x 32 lose blocks per CU)

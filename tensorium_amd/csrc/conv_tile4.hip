@@ -80,35 +80,14 @@ struct Frag4 {
 template <int BM_, int BN_, int WM_, int WN_, int BK_, int SG_, int IL_ = 0, bool SI_ = false,
           int RI_ = 0, bool ST_ = false, int JA_ = 0, int NA_ = 0, bool TA_ = false,
           bool BD_ = false, bool BW_ = false, bool AP_ = false, bool AT_ = false,
-          bool DX_ = false, bool AR_ = false, bool PF_ = false, bool AB_ = false>
+          bool DX_ = false, bool PF_ = false>
 struct Geo4 {
-  // AB: no workgroup barrier in the k-loop.  Three LDS stages and per-stage
-  // counters in LDS: a wave adds 1 to stored[s] once its stores of a tile
-  // into stage s are issued, and a reader of tile j waits for stored[j % 3]
-  // to reach NW * (j / 3 + 1) (LDS operations of one wave complete in order,
-  // so a count seen implies the data it covers); a stage is rewritten only
-  // by a wave that has seen the previous tile's count, i.e. once every wave
-  // has issued its stores of that tile — after its last read two tiles back.  The older wave of a SIMD, which the
-  // issue arbiter favours, then runs up to a tile ahead instead of waiting
-  // at a barrier for its partner (block stamps: waves w + NW/2 always arrive
-  // last, profiles/r05_conv_fwd_stamps.json).  With PF; the tile's stores
-  // at its top
-  static constexpr bool AB = AB_;
-  static constexpr int NSTG = AB_ ? 3 : 2;
   // PF: the register-staged operands of tile t+2 are loaded at the top of
   // tile t (two register sets, the tile pairs unrolled), so a gather has a
   // whole tile to land before its stores (the 2-group 26^2 / 13^2 forms
   // otherwise wait at the barrier for their loads: block stamps,
   // profiles/r05_conv_fwd_stamps.json)
   static constexpr bool PF = PF_;
-  // AR: A (the weights, [M][K]) never goes through LDS: lane (r16, q) of a
-  // wave loads, per 4-step group g, the float4 A[row][16g + 4q .. 16g + 4q + 3]
-  // of its strip row, and the four lanes (r16, 0..3) of a row transpose their
-  // four float4s by two v_permlane32_swap + two v_permlane16_swap, after which
-  // lane (r16, q) holds A[row][16g + 4i + q], i = 0..3 — exactly the slot the
-  // LDS image gave it.  No A staging stores, no A fragment reads, and the LDS
-  // holds B only (every wave reads its own 16 rows: nothing to share)
-  static constexpr bool AR = AR_;
   // DX: the conv backward's state.delta of a stride-1 layer as one implicit
   // transposed convolution — A = the weights tap-major, wt[t][f][c] (k-major,
   // TA), B = the delta planes gathered through the flipped window, k = t*F + f:
@@ -167,8 +146,8 @@ struct Geo4 {
   static constexpr int JB = NA < WN ? (J - NA * JA) / (WN - NA) : 0;  // ... of the others
   static constexpr int NG = BK / 16;            // 4-step groups per k-tile
   static constexpr int ROWS = BK / 4;           // slot rows per image (4g + q)
-  static constexpr int A_TILE = AR ? 0 : ROWS * BM * 4;  // floats
-  static constexpr int STAGE = ROWS * ((AR ? 0 : BM) + BN) * 4;
+  static constexpr int A_TILE = ROWS * BM * 4;  // floats
+  static constexpr int STAGE = ROWS * (BM + BN) * 4;
   static constexpr int B_TILE = ROWS * BN * 4;  // floats
   static constexpr int AU = BM * BK / 4 / NT;   // float4 A units per thread
   static constexpr int KI = BK / 4 / NW;        // B k-slots per thread
@@ -185,7 +164,7 @@ struct Geo4 {
   static_assert(!ST || (!IL && !SI && SG + 1 <= NG - 2 && NW % 2 == 0), "staggered staging");
   static_assert(AU >= 1 && BM * BK / 4 % NT == 0 && KI >= 1 && BK / 4 % NW == 0, "geometry");
   static_assert(NA * JA + (WN - NA) * JB == J && NA >= 1 && NA <= WN, "wave column split");
-  static_assert(NSTG * STAGE * 4 + 64 <= 163840, "LDS");
+  static_assert(2 * STAGE * 4 + 64 <= 163840, "LDS");
   static_assert(!BD || (!IL && !ST && !TA), "DMA gather: tile-top issue only");
   static_assert(!(BD && BW), "one gather form");
   static_assert(!AT || (!BD && !BW && !TA && !AP && !SI && 2 * B_TILE * 4 <= 98304),
@@ -193,9 +172,7 @@ struct Geo4 {
   static_assert(!AP || (!IL && !ST && !TA && BM % 64 == 0 && ROWS * BM % (64 * NW) == 0),
                 "A DMA: tile-top issue, whole 64-slot pieces");
   static_assert(!DX || (TA && !AT && !BD && !BW && !AP), "DX: k-major weights, b32 gather");
-  static_assert(!AR || (!TA && !AT && !AP && !DX && !IL && !ST), "AR: [M][K] weights, block staging");
   static_assert(!PF || (!AT && !AP && !BD && !BW && !ST), "PF: register staging");
-  static_assert(!AB || (PF && !AR && !IL && !SI && !ST), "AB: PF, stores at the tile top");
   static constexpr int ADM = AP ? ROWS * BM / 64 / NW : 0;  // A DMA instructions per wave
   static constexpr int AST = AP ? 0 : 4 * AU;                // A LDS stores per thread
   static constexpr int CH = (BN + 63) / 64;  // (BW) 64-pixel chunks of a slot row
@@ -207,10 +184,7 @@ template <class G, int KS>
 __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) {
   constexpr int BM = G::BM, BN = G::BN, BK = G::BK, J = G::J, NG = G::NG;
   constexpr int A_TILE = G::A_TILE, STAGE = G::STAGE, AU = G::AU, KI = G::KI;
-  __shared__ __attribute__((aligned(16))) float smem[G::NSTG * STAGE];
-  // (AB) stored[3]: stage s is read by a wave only once stored[s] counts
-  // every wave's stores of its tile
-  __shared__ unsigned abc[G::AB ? 3 : 1];
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 #ifdef TNS_CT4_STAMPS
   const unsigned long long rt_entry = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -473,44 +447,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       a_dst[u] = (4 * (kq4 >> 2)) * BM * 4 + m * 4 + (kq4 & 3);
     }
   }
-  float4 ras[G::PF ? 2 : 1][G::AR ? 1 : AU];  // (unused with AP / AR)
-  // (AR) this tile's A fragments (acur) and the next tile's loads (rar,
-  // transposed in place before the tile's last group)
-  floatx4 acur[G::AR ? NG : 1], rar[G::AR ? NG : 1];
-  // (AR + PF) the raw loads of the next two tiles, one set a tile parity
-  floatx4 rpf[G::AR && G::PF ? 2 : 1][G::AR && G::PF ? NG : 1];
-  const float* ar_src =
-      G::AR ? p.A + (m0 + (w % G::WM) * 16 + (lane & 15)) * p.lda + 4 * (lane >> 4) : nullptr;
-  auto load_ar = [&](int k0, floatx4* dst) {
-#pragma unroll
-    for (int g = 0; g < NG; ++g) dst[g] = *reinterpret_cast<const floatx4*>(ar_src + k0 + 16 * g);
-  };
-  auto xpose_ar = [&]() {
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      // lane (r16, q) holds A[row][16g + 4q + c]; afterwards component i
-      // holds A[row][16g + 4i + q] (a 4 x 4 transpose over the lane quarters)
-      // (components through scalars: hipcc's __builtin_bit_cast of a vector
-      // element reads element 0)
-      float x0 = rar[g][0], x1 = rar[g][1], x2 = rar[g][2], x3 = rar[g][3];
-      auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x0), __float_as_uint(x2), false, false);
-      x0 = __uint_as_float(r[0]);
-      x2 = __uint_as_float(r[1]);
-      r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x1), __float_as_uint(x3), false, false);
-      x1 = __uint_as_float(r[0]);
-      x3 = __uint_as_float(r[1]);
-      r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x0), __float_as_uint(x1), false, false);
-      x0 = __uint_as_float(r[0]);
-      x1 = __uint_as_float(r[1]);
-      r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x2), __float_as_uint(x3), false, false);
-      x2 = __uint_as_float(r[0]);
-      x3 = __uint_as_float(r[1]);
-      rar[g] = floatx4{x0, x1, x2, x3};
-    }
-  };
+  float4 ras[G::PF ? 2 : 1][AU];  // (unused with AP)
   auto load_a = [&](int k0, float* as, auto SET) {
     auto& ra = ras[decltype(SET)::value];
-    if constexpr (G::AR) return;  // (load_ar, after the tile's stores)
     if constexpr (G::AP) {
 #pragma unroll
       for (int u = 0; u < G::ADM; ++u) {
@@ -545,7 +484,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   };
   auto store_a = [&](float* as, auto SET) {
     auto& ra = ras[decltype(SET)::value];
-    if constexpr (G::AP || G::AR) return;  // (landed by the DMA / in registers)
+    if constexpr (G::AP) return;  // (landed by the DMA)
 #if defined(TNS_CT4_DIAG) && (TNS_CT4_DIAG & 8)
     return;  // diagnostic build: no A stores (timing only)
 #endif
@@ -614,14 +553,9 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     }
   };
   using Frag = Frag4<JW>;
-  // (AR: f.a from acur, or from rar for the next tile's first group)
-  auto frag = [&](int stg, int g, Frag& f, bool next = false) {
-    if constexpr (G::AR) {
-      f.a = next ? rar[g] : acur[g];
-    } else {
-      const float* ap = a_st(stg) + ((4 * g + q) * BM + wm * 16 + r16) * 4;
-      f.a = *reinterpret_cast<const floatx4*>(ap);
-    }
+  auto frag = [&](int stg, int g, Frag& f) {
+    const float* ap = a_st(stg) + ((4 * g + q) * BM + wm * 16 + r16) * 4;
+    f.a = *reinterpret_cast<const floatx4*>(ap);
     const float* bp = b_st(stg) + ((4 * g + q) * BN + coff * 16 + r16) * 4;
 #pragma unroll
     for (int j = 0; j < JW; ++j) f.b[j] = *reinterpret_cast<const floatx4*>(bp + 64 * j);
@@ -656,32 +590,6 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
   const int nt = K / BK;
   Frag f0, f1;
   if (nt > 0) {
-    if constexpr (G::AR) {
-      if constexpr (G::PF) {
-        load_ar(0, rpf[0]);
-        gather_b(b_st(0), S0{});
-        if (nt > 1) {  // (tile 1 into set 1, in flight past the barrier)
-          advance();
-          load_ar(BK, rpf[G::PF ? 1 : 0]);
-          gather_b(nullptr, S1{});
-        }
-#pragma unroll
-        for (int g = 0; g < NG; ++g) rar[g] = rpf[0][g];
-      } else {
-        load_ar(0, rar);
-        gather_b(b_st(0), S0{});
-      }
-      store_b(b_st(0), S0{});
-      xpose_ar();
-#pragma unroll
-      for (int g = 0; g < NG; ++g) acur[g] = rar[g];
-      __syncthreads();
-      frag(0, 0, f0);
-    }
-  }
-  if constexpr (G::AB)  // (tile 0: stored by every wave before the prologue's barrier)
-    if (tid < 3) abc[tid] = tid == 0 ? (unsigned)G::NW : 0u;
-  if (nt > 0 && !G::AR) {
     load_a(0, a_st(0), S0{});
     gather_b(b_st(0), S0{});
     if constexpr (G::PF) {  // (tile 1 into set 1, in flight past the barrier)
@@ -705,41 +613,15 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
     constexpr int par = decltype(PAR)::value;
     using SL = std::integral_constant<int, G::PF ? par : 0>;
     using SS = std::integral_constant<int, G::PF ? par ^ 1 : 0>;
-    const int tc = G::AB ? t % 3 : t & 1, tx = G::AB ? (t + 1) % 3 : (t + 1) & 1;
-    // (AB) counter waits and signals: relaxed LDS atomics between compiler
-    // fences (the hardware keeps a wave's LDS operations in order)
-    auto ab_wait = [&](int c, unsigned target) {
-      asm volatile("" ::: "memory");
-      while (__hip_atomic_load(&abc[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) {
-#ifndef TNS_CT4_AB_SPIN  // (A/B: a bare spin)
-        __builtin_amdgcn_s_sleep(1);
-#endif
-      }
-      asm volatile("" ::: "memory");
-    };
-    auto ab_signal = [&](int c) {
-      asm volatile("" ::: "memory");
-      if (lane == 0) __hip_atomic_fetch_add(&abc[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      asm volatile("" ::: "memory");
-    };
+    const int tc = t & 1, tx = (t + 1) & 1;
     TNS_PH(5);
     if constexpr (more && G::PF && !G::IL) {
       // (unconditional: past the last tile the weight rows' k is clamped
       // and the gather's offsets run past the images' range — read, unused)
       advance();
       load_a(min((t + 2) * BK, K - BK), nullptr, SL{});
-      if constexpr (G::AR) load_ar(min((t + 2) * BK, K - BK), rpf[SL::value]);
       gather_b(nullptr, SL{});
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
-      if constexpr (G::AB) {
-        // tile t+1 into stage tx, whose previous tile (t-2) every wave has
-        // read: this wave passed the wait for tile t's stores, which every
-        // wave issues at the top of its tile t-1, after its last read of t-2
-        store_a(a_st(tx), SS{});
-        store_b(b_st(tx), SS{});
-        ab_signal(tx);
-        __builtin_amdgcn_sched_barrier(0);
-      }
     } else if constexpr (more && !G::IL && !G::ST && !G::PF) {
       advance();
       if constexpr (G::BD) {
@@ -747,9 +629,6 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
         load_a((t + 1) * BK, a_st(tx), S0{});
       } else {
         load_a((t + 1) * BK, a_st(tx), S0{});
-        // (AR, two groups a tile: the next tile's A at the top, a whole tile
-        // ahead of its transpose; deeper tiles load it after their stores)
-        if constexpr (G::AR && NG <= 2) load_ar((t + 1) * BK, rar);
         gather_b(b_st(tx), S0{});
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads at the top of the tile
@@ -773,11 +652,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
             p.stamps[32 * blockIdx.x + 16 + w] =
                 (unsigned)(__builtin_amdgcn_s_memtime() & 0xffffffffu);
 #endif
-          if constexpr (G::AB) {
-            ab_wait(tx, (unsigned)(G::NW * ((t + 1) / 3 + 1)));
-          } else {
-            __syncthreads();
-          }
+          __syncthreads();
           TNS_PH(4);
         }
       __builtin_amdgcn_sched_barrier(0);
@@ -791,24 +666,15 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
       // one scheduling region per group: the next group's fragment reads,
       // interleaved staging (LI / SI) and this group's MFMAs
       const bool reads = g + 1 < NG || more;
-      if constexpr (more && G::AR)
-        if (g == NG - 1) {  // (the next tile's A, loaded after the stores / PF: a tile before)
-          if constexpr (G::PF) {
-#pragma unroll
-            for (int u = 0; u < NG; ++u) rar[u] = rpf[SS::value][u];
-          }
-          xpose_ar();
-        }
       if (g + 1 < NG)
         frag(tc, g + 1, fn);
       else if (more)
-        frag(tx, 0, fn, true);
+        frag(tx, 0, fn);
       if constexpr (more && G::IL) {
         if (g == 0) {
           advance();
           if constexpr (G::PF) {  // (tile t+2 into this tile's set, as above)
             load_a(min((t + 2) * BK, K - BK), nullptr, SL{});
-            if constexpr (G::AR) load_ar(min((t + 2) * BK, K - BK), rpf[SL::value]);
             gather_b(nullptr, SL{});
           } else {
             load_a((t + 1) * BK, a_st(tx), S0{});
@@ -847,7 +713,7 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           store_b(b_st(tx), S0{});
           __builtin_amdgcn_sched_barrier(0);
         }
-      if constexpr (more && !G::SI && !G::ST && !G::AB)
+      if constexpr (more && !G::SI && !G::ST)
         if (g == G::SG) {
           TNS_PH(1);
           store_a(a_st(tx), SS{});
@@ -855,17 +721,8 @@ __global__ __launch_bounds__(G::NT) void conv_tile4_kernel(GemmArgs p, int dil) 
           __builtin_amdgcn_sched_barrier(0);
           TNS_PH(2);
         }
-      if constexpr (more && G::AR && NG > 2 && !G::PF)
-        if (g == G::SG) {
-          load_ar((t + 1) * BK, rar);  // (registers free since the last tile's end)
-          __builtin_amdgcn_sched_barrier(0);
-        }
     }
     if constexpr (G::DX) flush();
-    if constexpr (more && G::AR) {
-#pragma unroll
-      for (int g = 0; g < NG; ++g) acur[g] = rar[g];
-    }
   };
   static_assert(NG % 2 == 0, "f0 holds group 0 at every tile start");
   if constexpr (G::PF) {  // (tile pairs: the set parity a compile-time constant)
@@ -1047,35 +904,18 @@ struct TileInfo4 {
                   false, false, true>>,                                                       \
    "conv_tile4_at<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",ri" #RIv ",j" #JAv   \
    "x" #NAv ">"}
-#define TNS_CT4R(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                           \
-  {BMv, BNv, BKv,                                                                             \
-   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, false, false,  \
-                  false, false, false, false, true>>,                                        \
-   "conv_tile4_ar<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv \
-   ",j" #JAv "x" #NAv ">"}
 #define TNS_CT4P(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                           \
   {BMv, BNv, BKv,                                                                             \
    launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, false, false,  \
-                  false, false, false, false, false, true>>,                                 \
+                  false, false, false, false, true>>,                                        \
    "conv_tile4_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv ",ri" #RIv \
    ",j" #JAv "x" #NAv ">"}
 #define TNS_CT4PI(BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, JAv, NAv)                     \
   {BMv, BNv, BKv,                                                                             \
    launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, false, JAv, NAv, false, false, \
-                  false, false, false, false, false, true>>,                                 \
+                  false, false, false, false, true>>,                                        \
    "conv_tile4_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si" #SIv  \
    ",ri" #RIv ",j" #JAv "x" #NAv ">"}
-#define TNS_CT4RP(BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, JAv, NAv)                     \
-  {BMv, BNv, BKv,                                                                             \
-   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, ILv, SIv, RIv, false, JAv, NAv, false, false, \
-                  false, false, false, false, true, true>>,                                  \
-   "conv_tile4_arpf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",il" #ILv ",si"   \
-   #SIv ",ri" #RIv ",j" #JAv "x" #NAv ">"}
-#define TNS_CT4AB(BMv, BNv, WMv, WNv, BKv, RIv, JAv, NAv)                                      \
-  {BMv, BNv, BKv,                                                                             \
-   launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, 0, 0, false, RIv, false, JAv, NAv, false, false,   \
-                  false, false, false, false, false, true, true>>,                           \
-   "conv_tile4_ab<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4[] = {
     TNS_CT4(128, 176, 8, 1, 32, 0, 0, false, 0, false),  // 0
     TNS_CT4(128, 176, 8, 1, 64, 2, 0, false, 0, false),  // 1
@@ -1125,57 +965,28 @@ const TileInfo4 kTiles4[] = {
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, false, 3, 0, 0), // 35 (0, PF)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 0, true, 3, 0, 0),  // 36 (0, PF + SI)
     TNS_CT4PI(128, 176, 8, 1, 32, 0, 2, false, 3, 0, 0), // 37 (0, PF + IL)
-    // no workgroup barrier in the k-loop (AB: three LDS stages, per-stage
-    // counters): bit-exact and slower on every class — 26^2 0.1267 -> 0.131,
-    // 13^2 0.134 -> 0.139, 52^2 0.1145 -> 0.119 (with s_sleep in the poll;
-    // a bare spin 0.139 / 0.144; with a second, consumed-side counter
-    // 0.137 / 0.142): the barrier the wave pairs meet at costs less than the
-    // polls that replace it
-    TNS_CT4AB(64, 176, 4, 2, 32, 3, 6, 1),               // 38 (18's shape)
-    TNS_CT4AB(128, 48, 8, 1, 64, 2, 0, 0),               // 39 (21's shape)
-    TNS_CT4AB(128, 176, 8, 1, 32, 3, 0, 0),              // 40 (0's shape, 32 deep)
-    TNS_CT4AB(64, 32, 4, 1, 32, 0, 0, 0),                // 41 (13's shape)
-    TNS_CT4AB(64, 96, 4, 1, 32, 3, 0, 0),                // 42 (8's shape)
-    // A in registers AND loaded two tiles ahead (AR + PF): slower still than
-    // the LDS-staged picks (13^2 0.1336 -> 0.1447 / 0.1472 ms, 26^2 0.1269 ->
-    // 0.1402; profiles/r05_conv_fwd_sweep.json)
-    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, true, 2, 0, 0),   // 43 (21)
-    TNS_CT4RP(128, 48, 8, 1, 64, 1, 0, false, 2, 0, 0),  // 44 (21, stores after group 1)
-    TNS_CT4RP(64, 176, 4, 2, 32, 0, 0, true, 3, 6, 1),   // 45 (31)
-    // A in registers (AR: float4 loads + a lane-quarter transpose, no A in
-    // LDS) of the picked forms 3, 8, 13, 18, 21: bit-exact, slower on every
-    // class but the stride-2 104^2 / 208^2 ones (YOLOv3 batch 8, same box,
-    // interleaved: 6.18-6.24 ms a batch against 5.94-6.03; 26^2 +4.9 %,
-    // 13^2 +8 %, 1x1 +4..11 %): every wave loads its own 16 rows, and the
-    // loads of a 64-deep tile go out after the stores, too late for the
-    // tile's last group (block stamps: profiles/r05_conv_fwd_stamps.json)
-    TNS_CT4R(128, 176, 8, 1, 64, 1, true, 2, 0, 0),      // 46 (3)
-    TNS_CT4R(64, 96, 4, 1, 32, 0, false, 3, 0, 0),       // 47 (8)
-    TNS_CT4R(64, 32, 4, 1, 32, 0, false, 0, 0, 0),       // 48 (13)
-    TNS_CT4R(64, 176, 4, 2, 32, 0, false, 3, 6, 1),      // 49 (18)
-    TNS_CT4R(128, 48, 8, 1, 64, 1, true, 2, 0, 0),       // 50 (21)
     // B by dword LDS-DMA (BD) / slot-wise (BW): bit-exact, measured slower
     // than the register-staged b32 stores on every class (kept selectable)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 51 (3, BD)
-    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 52 (3, BW)
-    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 53 (18, BW)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, true, false),          // 38 (3, BD)
+    TNS_CT4D(128, 176, 8, 1, 64, 1, true, 2, false, true),          // 39 (3, BW)
+    TNS_CT4UD(64, 176, 4, 2, 32, 0, false, 3, 6, 1, false, true),   // 40 (18, BW)
     // A by 16-byte LDS-DMA from the pre-permuted weights (AP): bit-exact,
     // slower on every class measured (52^2 0.114 -> 0.120 ms, 26^2 0.128 ->
     // 0.138, 13^2 0.138 -> 0.155, 1x1 0.021 -> 0.023; permute pass included)
-    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 54 (3)
+    TNS_CT4A(128, 176, 8, 1, 64, 1, true, 2, 0, 0),                 // 41 (3)
     // B stored by ds_write_addtid_b32 with operands swapped in the MFMA (AT:
     // gather lanes 16 pixels x 4 k, 16-byte epilogue stores), the picked
     // shapes: timed slower on every layer class (profiles/r04_conv_at_sweep.json:
     // 104^2 3x3 0.123 -> 0.137 ms, 52^2 0.117 -> 0.127,
     // 26^2 0.133 -> 0.163, 13^2 0.147 -> 0.218, 1x1 52^2 0.022 -> 0.024) —
     // the gather's 4 k rows per load instruction touch 4x the cache lines
-    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 55 (1)
-    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 56
-    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 57 (18)
-    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 58 (21)
-    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 59 (8)
-    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 60 (13)
-    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 61 (11)
+    TNS_CT4X(128, 176, 8, 1, 64, 2, 0, 0, 0),    // 42 (1)
+    TNS_CT4X(128, 176, 8, 1, 64, 1, 2, 0, 0),    // 43
+    TNS_CT4X(64, 176, 4, 2, 32, 0, 3, 6, 1),     // 44 (18)
+    TNS_CT4X(128, 48, 8, 1, 64, 1, 2, 0, 0),     // 45 (21)
+    TNS_CT4X(64, 96, 4, 1, 32, 0, 3, 0, 0),      // 46 (8)
+    TNS_CT4X(64, 32, 4, 1, 32, 0, 0, 0, 0),      // 47 (13)
+    TNS_CT4X(64, 64, 4, 2, 32, 0, 0, 0, 0),      // 48 (11)
 #endif
 };
 // A k-major (TA): col = W^T . delta of the conv backward (conv_tile4_dx_*)
@@ -1187,7 +998,7 @@ const TileInfo4 kTiles4[] = {
 #define TNS_CT4TP(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                      \
   {BMv, BNv, BKv,                                                                      \
    launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, true, false, \
-                  false, false, false, false, false, true>>,                            \
+                  false, false, false, false, true>>,                                   \
    "conv_tile4_ta_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv   \
    ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4T[] = {
@@ -1218,7 +1029,7 @@ constexpr int kNumTiles4T = sizeof(kTiles4T) / sizeof(kTiles4T[0]);
 #define TNS_CT4DXP(BMv, BNv, WMv, WNv, BKv, SGv, SIv, RIv, JAv, NAv)                         \
   {BMv, BNv, BKv,                                                                          \
    launch_g4<Geo4<BMv, BNv, WMv, WNv, BKv, SGv, 0, SIv, RIv, false, JAv, NAv, true, false,  \
-                  false, false, false, true, false, true>>,                                \
+                  false, false, false, true, true>>,                                       \
    "conv_tile4_dx_pf<" #BMv "x" #BNv "x" #BKv ",w" #WMv "x" #WNv ",g" #SGv ",si" #SIv      \
    ",ri" #RIv ",j" #JAv "x" #NAv ">"}
 const TileInfo4 kTiles4DX[] = {
@@ -1250,11 +1061,8 @@ constexpr int kNumTiles4DX = sizeof(kTiles4DX) / sizeof(kTiles4DX[0]);
 #undef TNS_CT4X
 #undef TNS_CT4T
 #undef TNS_CT4TP
-#undef TNS_CT4R
 #undef TNS_CT4P
 #undef TNS_CT4PI
-#undef TNS_CT4RP
-#undef TNS_CT4AB
 constexpr int kNumTiles4 = sizeof(kTiles4) / sizeof(kTiles4[0]);
 
 }  // namespace
