@@ -325,6 +325,9 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
                                                    float* __restrict__ part1, int act,
                                                    float* wa, const float* __restrict__ c3,
                                                    const float* __restrict__ sc_arr) {
+  // chain waves first at the SIMD issue arbiter: their dependent adds are the
+  // critical path, the MFMA waves of a concurrent dW product have slack
+  __builtin_amdgcn_s_setprio(3);
   constexpr int TILE = NT * E;
   constexpr bool DOTF = MODE == CH_DOT || MODE == CH_DDOT;    // the fma chains
   constexpr bool TWO = MODE == CH_VDELTA || DOTF;             // two LDS streams
@@ -503,6 +506,9 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
                                                        float* __restrict__ part1, int act,
                                                        float* wa, const float* __restrict__ c3,
                                                        const float* __restrict__ sc_arr) {
+  // chain waves first at the SIMD issue arbiter: their dependent adds are the
+  // critical path, the MFMA waves of a concurrent dW product have slack
+  __builtin_amdgcn_s_setprio(3);
   static_assert(MODE != CH_DDOT, "the specialised-wave form stages two load streams");
   (void)c3;
   constexpr int SNT = 192, E = 32, TILE = SNT * E, NBUF = 3;

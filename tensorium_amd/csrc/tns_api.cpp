@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <initializer_list>
 #include <map>
@@ -89,6 +90,11 @@ struct tns_ctx {
   // conv backward: state.delta's chain (TN + col2im) runs on this side
   // stream while the dW product runs on `stream` (fork / join events)
   hipStream_t aux_stream = nullptr;
+  // the joined overlap's side stream (TNS_OPT_BWD_OVERLAP = 1: state.delta's
+  // chain beside the call's dW, joined before the call returns) at the
+  // context stream's priority; aux_stream, the pipelined dW products' stream,
+  // sits at the lowest
+  hipStream_t ovl_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   // TNS_OPT_BWD_OVERLAP = 2: dW products left running on aux_stream past the
   // call's return; the next call of any other entry point joins them first
@@ -133,6 +139,7 @@ int ensure_scratch(tns_ctx* c, int slot, int64_t elems, float** out, bool side =
     if (c->scratch[slot]) {
       hipStreamSynchronize(c->stream);
       if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+      if (c->ovl_stream) hipStreamSynchronize(c->ovl_stream);
       if (c->home_stream) hipStreamSynchronize(c->home_stream);
       hipFree(c->scratch[slot]);
       c->scratch[slot] = nullptr;
@@ -159,6 +166,7 @@ void release_scratch(tns_ctx* c, int slot) {
   if (!c->scratch[slot]) return;
   hipStreamSynchronize(c->stream);
   if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+  if (c->ovl_stream) hipStreamSynchronize(c->ovl_stream);
   if (c->home_stream) hipStreamSynchronize(c->home_stream);
   hipFree(c->scratch[slot]);
   c->scratch[slot] = nullptr;
@@ -169,18 +177,32 @@ void release_scratch(tns_ctx* c, int slot) {
 // together on the context's device; false (nothing kept) if any of them
 // cannot be created, and the caller runs its sequential schedule
 bool ensure_side_stream(tns_ctx* c) {
-  if (c->aux_stream && c->ev_fork && c->ev_join) return true;
+  if (c->aux_stream && c->ovl_stream && c->ev_fork && c->ev_join) return true;
   int prev = -1;
   hipGetDevice(&prev);
+  // the pipelined dW products' stream (off the critical path) at the lowest
+  // queue priority and the context's stream at the highest: the context's
+  // work is dispatched first where both wait for CU room (YOLOv3 training
+  // backward 17.96 -> 17.81 ms with the chain waves' issue priority,
+  // batchnorm.hip; TNS_STREAM_PRIO=0 turns it off).  The joined overlap
+  // waits for both halves of a call, so its stream keeps the default
+  // priority (at the lowest, the joined conv backward lost 0.25 ms)
+  int least = 0, greatest = 0;
+  const char* sp = getenv("TNS_STREAM_PRIO");
+  const bool prio = !(sp && sp[0] == '0') &&
+                    hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
   bool ok = hipSetDevice(c->device) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking) == hipSuccess &&
+            (prio ? hipStreamCreateWithPriority(&c->aux_stream, hipStreamNonBlocking, least)
+                  : hipStreamCreateWithFlags(&c->aux_stream, hipStreamNonBlocking)) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->ovl_stream, hipStreamNonBlocking) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+    if (c->ovl_stream) hipStreamDestroy(c->ovl_stream);
     if (c->ev_fork) hipEventDestroy(c->ev_fork);
     if (c->ev_join) hipEventDestroy(c->ev_join);
-    c->aux_stream = nullptr;
+    c->aux_stream = c->ovl_stream = nullptr;
     c->ev_fork = c->ev_join = nullptr;
     hipGetLastError();
   }
@@ -736,7 +758,15 @@ int tns_hip_create(int32_t deviceIndex, tns_ctx** out) {
   TNS_HIP_TRY(hipSetDevice(deviceIndex));
   tns_ctx* c = new tns_ctx();
   c->device = deviceIndex;
-  e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  {
+    int least = 0, greatest = 0;
+    const char* sp = getenv("TNS_STREAM_PRIO");  // (see ensure_side_stream)
+    if (!(sp && sp[0] == '0') &&
+        hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+      e = hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest);
+    else
+      e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  }
   if (e != hipSuccess) {
     delete c;
     return set_error(TNS_ERR_HIP, "hipStreamCreate: %s", hipGetErrorString(e));
@@ -753,6 +783,7 @@ int tns_hip_destroy(tns_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   if (c->aux_stream) hipStreamSynchronize(c->aux_stream);
+  if (c->ovl_stream) hipStreamSynchronize(c->ovl_stream);
   for (int i = 0; i < tns_ctx::kSlots; ++i)
     if (c->scratch[i]) hipFree(c->scratch[i]);
   for (auto& kv : c->ktabs) hipFree(kv.second);
@@ -761,6 +792,7 @@ int tns_hip_destroy(tns_ctx* c) {
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
   if (c->copy_stream) hipStreamDestroy(c->copy_stream);
   if (c->aux_stream) hipStreamDestroy(c->aux_stream);
+  if (c->ovl_stream) hipStreamDestroy(c->ovl_stream);
   if (c->ev_fork) hipEventDestroy(c->ev_fork);
   if (c->ev_join) hipEventDestroy(c->ev_join);
   for (hipEvent_t e : c->pipe_ev) hipEventDestroy(e);
@@ -2227,18 +2259,18 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     return state_delta ? run_dx() : TNS_OK;
   }
   TNS_HIP_TRY(hipEventRecord(c->ev_fork, c->stream));
-  TNS_HIP_TRY(hipStreamWaitEvent(c->aux_stream, c->ev_fork, 0));
+  TNS_HIP_TRY(hipStreamWaitEvent(c->ovl_stream, c->ev_fork, 0));
   int rx;
   {
-    // state.delta's chain enqueued on the side stream (every launch inside
+    // state.delta's chain enqueued on the overlap stream (every launch inside
     // run_dx goes to c->stream), the context's stream restored after
     hipStream_t main = c->stream;
-    c->stream = c->aux_stream;
+    c->stream = c->ovl_stream;
     rx = run_dx();
     c->stream = main;
   }
   // joined even after an error, so later work on the stream stays ordered
-  const hipError_t ej = hipEventRecord(c->ev_join, c->aux_stream);
+  const hipError_t ej = hipEventRecord(c->ev_join, c->ovl_stream);
   const int rw = run_dw();
   const hipError_t ew = ej == hipSuccess ? hipStreamWaitEvent(c->stream, c->ev_join, 0) : ej;
   if (rx) return rx;
