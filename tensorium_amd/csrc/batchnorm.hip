@@ -314,7 +314,19 @@ __global__ void vssum_k(int64_t n, const float* __restrict__ a, float* __restric
 // term as it is staged (one rounding, as the separate pass would store it) —
 // the BN conv backward's forwardScale folded into MeansAndVarsDelta (and
 // normalizeDelta), the scaled delta never written
-enum ChainMode { CH_SUM = 0, CH_SRSS = 1, CH_VDELTA = 2, CH_DOT = 3, CH_DSUM = 4, CH_DDOT = 5 };
+// CH_BNB: the BN conv backward's three reductions in one pass over delta,
+// output, x_norm and x (a, c3, b, xx): d = delta * f'(output) (Derivative),
+// ds = d * scale (forwardScale); lanes 0-7 the addDots chains of d . x_norm
+// (sdot), lanes 8-15 the MeansAndVarsDelta mean chains of ds (vssum), lanes
+// 16-23 its variance chains of (x - mean) * ds (sVarinceDelta); nothing is
+// written back (normalizeDelta recomputes d and ds) — one pass and one
+// finish instead of three passes and two finishes.  All three chain groups
+// run fma(term, w, acc) so the wave executes one instruction stream: w =
+// x_norm for the dot, 1.0 (an LDS row of ones) for the sums — fma(t, 1, acc)
+// rounds t + acc exactly as the add does
+enum ChainMode {
+  CH_SUM = 0, CH_SRSS = 1, CH_VDELTA = 2, CH_DOT = 3, CH_DSUM = 4, CH_DDOT = 5, CH_BNB = 6
+};
 
 template <int MODE, int NT, int E>
 __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
@@ -324,24 +336,34 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
                                                    int quirk, float* __restrict__ part0,
                                                    float* __restrict__ part1, int act,
                                                    float* wa, const float* __restrict__ c3,
-                                                   const float* __restrict__ sc_arr) {
+                                                   const float* __restrict__ sc_arr,
+                                                   const float* __restrict__ xx,
+                                                   float* __restrict__ part2) {
   // chain waves first at the SIMD issue arbiter: their dependent adds are the
   // critical path, the MFMA waves of a concurrent dW product have slack
   __builtin_amdgcn_s_setprio(3);
   constexpr int TILE = NT * E;
-  constexpr bool DOTF = MODE == CH_DOT || MODE == CH_DDOT;    // the fma chains
+  constexpr bool BNB = MODE == CH_BNB;
+  constexpr bool DOTF = MODE == CH_DOT || MODE == CH_DDOT || BNB;  // the fma chains
   constexpr bool TWO = MODE == CH_VDELTA || DOTF;             // two LDS streams
   constexpr bool LB = TWO || MODE == CH_DSUM;                 // b loaded
-  constexpr bool LC = MODE == CH_DDOT;                        // c3 loaded
+  constexpr bool LC = MODE == CH_DDOT || BNB;                 // c3 loaded
   // tiles stored lane-major: element e of the tile at (e & 7) * LDT + e / 8,
   // so a chain lane's consecutive terms are contiguous (ds_read_b128 reads
   // four); rows padded by 8 floats (conflict-free staging stores)
   constexpr int LDT = TILE / 8 + 8;
   __shared__ __attribute__((aligned(16))) float U[2][8 * LDT];
   __shared__ __attribute__((aligned(16))) float V[TWO ? 2 : 1][TWO ? 8 * LDT : 1];
+  // (BNB) the mean and variance terms, and the row of ones the sum chains
+  // multiply by
+  __shared__ __attribute__((aligned(16))) float Mt[BNB ? 2 : 1][BNB ? 8 * LDT : 1];
+  __shared__ __attribute__((aligned(16))) float Qt[BNB ? 2 : 1][BNB ? 8 * LDT : 1];
+  __shared__ __attribute__((aligned(16))) float ONES[BNB ? LDT : 1];
   const int tid = threadIdx.x;
   const int l = tid & 7, grp = tid >> 3;  // chain lane, chain set (wave 0)
-  const bool chain = grp == 0 || (MODE == CH_VDELTA && grp == 1);
+  const bool chain = grp == 0 || (MODE == CH_VDELTA && grp == 1) || (BNB && grp <= 2);
+  if constexpr (BNB)
+    for (int q = tid; q < LDT; q += NT) ONES[q] = 1.0f;  // (published by the first barrier)
   const int64_t nb8 = (bs >> 3) << 3;  // elements in full 8-blocks
   const int ntile = (int)((nb8 + TILE - 1) / TILE);
   const int tail = (int)(bs & 7);
@@ -350,11 +372,12 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
     const float* pa = a + blk * bs;
     const float* pb = LB ? b + blk * bs : nullptr;
     const float* pc = LC ? c3 + blk * bs : nullptr;
+    const float* px = BNB ? xx + blk * bs : nullptr;
     float* pw = (MODE == CH_DSUM || MODE == CH_DDOT) ? wa + blk * bs : nullptr;
-    const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA) ? mu_arr[i] : 0.0f;
-    const bool scaled = MODE == CH_VDELTA && sc_arr != nullptr;
+    const float mu = (MODE == CH_SRSS || MODE == CH_VDELTA || BNB) ? mu_arr[i] : 0.0f;
+    const bool scaled = (MODE == CH_VDELTA && sc_arr != nullptr) || BNB;
     const float scl = scaled ? sc_arr[i] : 1.0f;
-    float ra[E], rb[LB ? E : 1], rc[LC ? E : 1];
+    float ra[E], rb[LB ? E : 1], rc[LC ? E : 1], rx[BNB ? E : 1];
     auto load = [&](int t) {
       const int64_t base = (int64_t)t * TILE + tid;
 #pragma unroll
@@ -363,6 +386,7 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
         ra[u] = k < nb8 ? pa[k] : 0.0f;
         if constexpr (LB) rb[u] = k < nb8 ? pb[k] : 0.0f;
         if constexpr (LC) rc[u] = k < nb8 ? pc[k] : 0.0f;
+        if constexpr (BNB) rx[u] = k < nb8 ? px[k] : 0.0f;
       }
     };
     auto store = [&](int buf, int t) {
@@ -380,6 +404,13 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
           V[buf][e] = rb[u];
           const int64_t k = (int64_t)t * TILE + tid + NT * u;
           if (k < nb8) pw[k] = d;
+        } else if constexpr (BNB) {
+          const float d = ra[u] * grad_apply(rc[u], act);  // Derivative
+          const float ds = d * scl;                          // forwardScale
+          U[buf][e] = d;
+          V[buf][e] = rb[u];
+          Mt[buf][e] = ds;
+          Qt[buf][e] = (rx[u] - mu) * ds;
         } else if constexpr (MODE == CH_SUM) {
           U[buf][e] = ra[u];
         } else if constexpr (MODE == CH_SRSS) {  // srss: vsubps (mean - a), vmulps
@@ -409,6 +440,11 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
         const float* row =
             ((MODE == CH_VDELTA && grp == 1) ? &V[t & 1][0] : &U[t & 1][0]) + l * LDT;
         const float* rowb = TWO ? &V[t & 1][0] + l * LDT : row;
+        if constexpr (BNB) {
+          if (grp == 1) row = &Mt[t & 1][0] + l * LDT;
+          if (grp == 2) row = &Qt[t & 1][0] + l * LDT;
+          if (grp >= 1) rowb = ONES;
+        }
         int q = 0;
         for (; q + 16 <= cnt; q += 16) {
           float v[16], w[16];
@@ -440,7 +476,10 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
       // srss / sVarinceDelta_avx: fold (unless quirk and no tail), tail into
       //   lane 0, hadd, hadd
       // sdot_avx2: masked-FMA tail into lanes 0..tail-1, fold, hadd, hadd
-      const bool lanes_form = MODE == CH_SRSS || (MODE == CH_VDELTA && grp == 1);
+      const bool lanes_form =
+          MODE == CH_SRSS || (MODE == CH_VDELTA && grp == 1) || (BNB && grp == 2);
+      // (BNB) tail element k's derived, scaled terms
+      auto bnb_d = [&](int k) { return pa[nb8 + k] * grad_apply(pc[nb8 + k], act); };
       if constexpr (DOTF) {
         if (tail && grp == 0) {
           float xa = l < tail ? pa[nb8 + l] : 0.0f;
@@ -451,6 +490,8 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
               pw[nb8 + l] = xa;
             }
           }
+          if constexpr (BNB)
+            if (l < tail) xa = bnb_d(l);
           acc = fmaf(xa, xb, acc);
         }
       }
@@ -461,6 +502,8 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
           if (MODE == CH_SRSS) {
             const float d = mu - pa[nb8 + k];
             x0 = x0 + d * d;
+          } else if (BNB) {
+            x0 = x0 + (px[nb8 + k] - mu) * (bnb_d(k) * scl);
           } else {
             const float d = scaled ? pa[nb8 + k] * scl : pa[nb8 + k];
             x0 = x0 + (pb[nb8 + k] - mu) * d;
@@ -475,11 +518,15 @@ __global__ __launch_bounds__(NT) void block_chains(const float* __restrict__ a,
             pw[nb8 + k] = d;
             r = r + d;
           }
+        } else if constexpr (BNB) {
+          if (grp == 1)
+            for (int k = 0; k < tail; ++k) r = r + bnb_d(k) * scl;
         } else if (!lanes_form && !DOTF) {
           for (int k = 0; k < tail; ++k) r = r + (scaled ? pa[nb8 + k] * scl : pa[nb8 + k]);
         }
         if (grp == 0) part0[blk] = r;
-        else part1[blk] = r;
+        else if (grp == 1) part1[blk] = r;
+        else if constexpr (BNB) part2[blk] = r;
       }
     }
     __syncthreads();
@@ -505,12 +552,16 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
                                                        int quirk, float* __restrict__ part0,
                                                        float* __restrict__ part1, int act,
                                                        float* wa, const float* __restrict__ c3,
-                                                       const float* __restrict__ sc_arr) {
+                                                       const float* __restrict__ sc_arr,
+                                                       const float* __restrict__ xx,
+                                                       float* __restrict__ part2) {
   // chain waves first at the SIMD issue arbiter: their dependent adds are the
   // critical path, the MFMA waves of a concurrent dW product have slack
   __builtin_amdgcn_s_setprio(3);
-  static_assert(MODE != CH_DDOT, "the specialised-wave form stages two load streams");
+  static_assert(MODE != CH_DDOT && MODE != CH_BNB, "the specialised-wave form stages two load streams");
   (void)c3;
+  (void)xx;
+  (void)part2;
   constexpr int SNT = 192, E = 32, TILE = SNT * E, NBUF = 3;
   constexpr bool TWO = MODE == CH_VDELTA || MODE == CH_DOT;
   constexpr bool LB = TWO || MODE == CH_DSUM;
@@ -779,26 +830,48 @@ __global__ void chains_finish(const float* __restrict__ part0, const float* __re
   }
 }
 
+// (BNB) per channel, over the groups in order: scale_updates += the dot
+// sums; mean_delta / var_delta as FIN_VDELTA
+__global__ void bnb_finish(const float* __restrict__ part0, const float* __restrict__ part1,
+                           const float* __restrict__ part2, int64_t groups, int64_t N,
+                           const float* __restrict__ var, float* __restrict__ dot_out,
+                           float* __restrict__ mean_delta, float* __restrict__ var_delta) {
+  const int64_t i = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (i >= N) return;
+  float d = 0.0f, m = 0.0f, v = 0.0f;
+  for (int64_t g = 0; g < groups; ++g) {
+    d = d + part0[g * N + i];
+    m = m + part1[g * N + i];
+    v = v + part2[g * N + i];
+  }
+  dot_out[i] = dot_out[i] + d;
+  const float ve = var[i] > SEPS ? var[i] : SEPS;
+  const float inv = -1.0f / sqrtf(ve);
+  mean_delta[i] = m * inv;
+  var_delta[i] = (float)((double)v * -0.5 * pow((double)ve, -1.5));
+}
+
 template <int MODE>
 hipError_t run_chains(const float* a, const float* b, const float* mu, int64_t groups, int64_t N,
                       int64_t bs, int quirk, float* part0, float* part1, hipStream_t s,
                       int act = 0, float* wa = nullptr, const float* c3 = nullptr,
-                      const float* sc = nullptr) {
+                      const float* sc = nullptr, const float* xx = nullptr,
+                      float* part2 = nullptr) {
   const int64_t nblocks = groups * N;
   const unsigned grid = (unsigned)(nblocks < (1 << 20) ? nblocks : (1 << 20));
-  if constexpr (MODE != CH_DDOT) {
+  if constexpr (MODE != CH_DDOT && MODE != CH_BNB) {
     if (bs >= 16384) {
       hipLaunchKernelGGL((block_chains_ws<MODE>), dim3(grid), dim3(256), 0, s, a, b, mu, nblocks,
-                         N, bs, quirk, part0, part1, act, wa, c3, sc);
+                         N, bs, quirk, part0, part1, act, wa, c3, sc, xx, part2);
       return hipGetLastError();
     }
   }
   if (bs >= 4096)
     hipLaunchKernelGGL((block_chains<MODE, 256, 16>), dim3(grid), dim3(256), 0, s, a, b, mu,
-                       nblocks, N, bs, quirk, part0, part1, act, wa, c3, sc);
+                       nblocks, N, bs, quirk, part0, part1, act, wa, c3, sc, xx, part2);
   else
     hipLaunchKernelGGL((block_chains<MODE, 64, 8>), dim3(grid), dim3(64), 0, s, a, b, mu, nblocks,
-                       N, bs, quirk, part0, part1, act, wa, c3, sc);
+                       N, bs, quirk, part0, part1, act, wa, c3, sc, xx, part2);
   return hipGetLastError();
 }
 
@@ -906,11 +979,12 @@ __global__ __launch_bounds__(TPB) void normalize_delta_rows(
     const float* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ var,
     const float* __restrict__ mean_delta, const float* __restrict__ var_delta,
     float* __restrict__ delta, int64_t N, int64_t bs, int bpr, float B,
-    const float* __restrict__ scales) {
+    const float* __restrict__ scales, const float* __restrict__ out, int act) {
   int64_t row, i;
   int seg;
   row_of(bpr, N, row, i, seg);
-  const bool scaled = scales != nullptr;  // (forwardScale folded in: delta * scale first)
+  // (out: Derivative folded in first, delta * f'(out); scales: forwardScale)
+  const bool scaled = scales != nullptr;
   const float scl = scaled ? scales[i] : 1.0f;
   const float md = mean_delta[i] / B;
   const float vd = 2.0f * var_delta[i] / B;
@@ -922,11 +996,13 @@ __global__ __launch_bounds__(TPB) void normalize_delta_rows(
   for (int u = 0; u < RU; ++u) {
     const int64_t j = ((int64_t)seg * RU * TPB + u * TPB + threadIdx.x) * V;
     if (j >= bs) break;
-    float d[V], xv[V];
+    float d[V], xv[V], ov[V];
     ld<V>(delta + base + j, d);
     ld<V>(x + base + j, xv);
+    if (out) ld<V>(out + base + j, ov);
 #pragma unroll
     for (int c = 0; c < V; ++c) {
+      if (out) d[c] = d[c] * grad_apply(ov[c], act);
       const float dv = scaled ? d[c] * scl : d[c];
       const float a = dv / sd;
       const float t = (xv[c] - m) * vd + md;  // sNormalizeDelta_avx order
@@ -1239,15 +1315,50 @@ hipError_t launch_normalize_delta(const float* x, const float* mean, const float
     if (v4)
       hipLaunchKernelGGL(normalize_delta_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
                          s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                         (float)(groups * bs), scales);
+                         (float)(groups * bs), scales, nullptr, 0);
     else
       hipLaunchKernelGGL(normalize_delta_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
                          s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                         (float)(groups * bs), scales);
+                         (float)(groups * bs), scales, nullptr, 0);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(normalize_delta_k, dim3(nblk(total)), dim3(TPB), 0, s, x, mean, var,
                      mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs), scales);
+  return hipGetLastError();
+}
+
+// the BN conv backward (Derivative, addDots, forwardScale, MeansAndVarsDelta,
+// normalizeDelta) as one CH_BNB chain pass + its finish + normalizeDelta with
+// the Derivative and the scale applied to each loaded term; hipErrorNotSupported
+// where it does not apply (the >= 16384-pixel planes, short blocks, planes
+// that the row form of normalizeDelta does not cover): the caller runs the
+// separate passes.  part: 3 * groups * N floats
+hipError_t launch_bn_backward_fused(float* scale_updates, const float* x_norm, float* delta,
+                                    const float* output, int act, const float* x,
+                                    const float* mean, const float* var, const float* scales,
+                                    float* mean_delta, float* var_delta, int64_t groups,
+                                    int64_t N, int64_t bs, int quirk, float* part, hipStream_t s) {
+  if (N <= 0 || groups <= 0 || bs <= 0) return hipSuccess;
+  if (bs >= 16384 || !use_chains(bs, part)) return hipErrorNotSupported;
+  const bool v4 = bs % 4 == 0 && al16(x) && al16(delta) && al16(output);
+  const int bpr = row_bpr(groups * N, bs, v4 ? 4 : 1);
+  if (!bpr) return hipErrorNotSupported;
+  float* part1 = part + groups * N;
+  float* part2 = part + 2 * groups * N;
+  if (hipError_t e = run_chains<CH_BNB>(delta, x_norm, mean, groups, N, bs, quirk, part, part1, s,
+                                        act, nullptr, output, scales, x, part2))
+    return e;
+  hipLaunchKernelGGL(bnb_finish, dim3(nblk(N)), dim3(TPB), 0, s, part, part1, part2, groups, N, var,
+                     scale_updates, mean_delta, var_delta);
+  if (hipError_t e = hipGetLastError()) return e;
+  if (v4)
+    hipLaunchKernelGGL(normalize_delta_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s,
+                       x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
+                       (float)(groups * bs), scales, output, act);
+  else
+    hipLaunchKernelGGL(normalize_delta_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s,
+                       x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
+                       (float)(groups * bs), scales, output, act);
   return hipGetLastError();
 }
 

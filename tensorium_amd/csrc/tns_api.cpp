@@ -38,6 +38,9 @@ static int64_t g_dx_fused = 1;
 static int64_t g_dx_tile = -1;
 static int64_t g_dx_conv = -1;
 static int64_t g_dw_res = -1;
+// the BN conv backward as one chain pass + normalizeDelta (launch_bn_backward_fused);
+// TNS_BN_FUSED=0 (A/B): the three-pass form
+static bool g_bn_fused = !(getenv("TNS_BN_FUSED") && getenv("TNS_BN_FUSED")[0] == '0');
 // conv backward dW with the im2col matrix generated in the staging
 // (dw_tile.hip): -1 by measured shape, -2 never, v >= 0 form v (TNS_OPT_DW_TILE)
 static int64_t g_dw_tile = -1;
@@ -1947,8 +1950,19 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
       return r;
   }
   float* part;
-  if (int r = ensure_scratch(c, SLOT_BN, 2 * batch * filters, &part)) return r;
-  if (bn.scales) {
+  if (int r = ensure_scratch(c, SLOT_BN, 3 * batch * filters, &part)) return r;
+  // batchNormBack's five passes as one chain pass over delta, output, x_norm
+  // and x (the three reductions) + normalizeDelta deriving and scaling each
+  // term as it loads it, where the chain kernels apply
+  hipError_t fe = hipErrorNotSupported;
+  if (bn.scales && g_bn_fused)
+    fe = launch_bn_backward_fused(bn.scale_updates, bn.x_norm, delta, output, activation, bn.x,
+                                  bn.mean, bn.variance, bn.scales, bn.mean_delta,
+                                  bn.variance_delta, batch, filters, i_k, (int)g_srss_quirk, part,
+                                  c->stream);
+  if (fe != hipErrorNotSupported) {
+    if (int r = hip_status(fe, "batchNormBack launch")) return r;
+  } else if (bn.scales) {
     // Derivative(): delta *= f'(output), then batchNormBack:
     // scale_updates.addDots(x_norm, delta); delta.forwardScale(scales);
     // MeansAndVarsDelta; normalizeDelta — and no bias_updates term

@@ -374,6 +374,14 @@ hipError_t launch_normalize_delta(const float* x, const float* mean, const float
 // whether launch_mean_var_delta / launch_normalize_delta can fold the BN
 // scales into their loads for planes of bs pixels (else forwardScale first)
 bool bn_folds_scale(int64_t bs);
+// the BN conv backward in one chain pass + normalizeDelta (CH_BNB);
+// hipErrorNotSupported where it does not apply (run the separate passes).
+// part: 3 * groups * N floats
+hipError_t launch_bn_backward_fused(float* scale_updates, const float* x_norm, float* delta,
+                                    const float* output, int act, const float* x,
+                                    const float* mean, const float* var, const float* scales,
+                                    float* mean_delta, float* var_delta, int64_t groups,
+                                    int64_t N, int64_t bs, int quirk, float* part, hipStream_t s);
 // the BN conv backward's Derivative + addDots in one pass where the chain
 // kernels allow (else the two passes)
 hipError_t launch_add_dots_derive(float* dst, const float* x_norm, float* delta,
