@@ -55,6 +55,7 @@ struct C1Args {
   const float* bias;
   int M, N, K, P, tiles_m, act;
   bool fuse;
+  bool add;  // C := C + product (the conv backward's 1x1 col2im: one add a pixel)
 };
 
 // BM x BN block, BK-deep k-tiles, WM x WN waves: a wave = 16 rows x 64
@@ -251,7 +252,13 @@ __global__ __launch_bounds__(G::NT) void conv1x1_kernel(C1Args p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = act_apply_cheap(v[j] + bi, p.act);
     }
-    *reinterpret_cast<floatx4*>(p.C + ((int64_t)img * p.M + m) * P + pix) = v;
+    floatx4* cp = reinterpret_cast<floatx4*>(p.C + ((int64_t)img * p.M + m) * P + pix);
+    if (p.add) {
+      const floatx4 o = *cp;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = o[j] + v[j];
+    }
+    *cp = v;
   }
 }
 
@@ -296,9 +303,38 @@ int conv1x1_pick(int64_t M, int64_t N, int64_t K, int64_t P) {
   return 3;
 }
 
+// out[c][r] = in[r][c] (rows x cols, 32 x 32 tiles through LDS): the
+// backward's transposed weights
+__global__ __launch_bounds__(256) void c1_transpose_kernel(const float* __restrict__ in,
+                                                           float* __restrict__ out, int rows,
+                                                           int cols) {
+  __shared__ float t[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    t[y][tx] = r < rows && c < cols ? in[(int64_t)r * cols + c] : 0.0f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < cols && r < rows) out[(int64_t)c * rows + r] = t[tx][y];
+  }
+}
+
+hipError_t launch_transpose(const float* in, float* out, int64_t rows, int64_t cols,
+                            hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (rows > (1 << 26) || cols > (1 << 26)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(c1_transpose_kernel,
+                     dim3((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32)), dim3(256), 0,
+                     s, in, out, (int)rows, (int)cols);
+  return hipGetLastError();
+}
+
 hipError_t launch_conv1x1(int v, const float* weights, const float* x, const float* bias,
                           float* out, int64_t batch, int64_t M, int64_t K, int64_t P, int act,
-                          hipStream_t s) {
+                          hipStream_t s, bool add) {
   if (v < 0 || v >= kNumC1) return hipErrorInvalidValue;
   const C1Form& f = kC1[v];
   const int64_t N = batch * P;
@@ -309,7 +345,7 @@ hipError_t launch_conv1x1(int v, const float* weights, const float* x, const flo
   C1Args a{};
   a.A = weights; a.X = x; a.C = out; a.bias = bias;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P;
-  a.tiles_m = (int)((M + f.bm - 1) / f.bm); a.act = act; a.fuse = bias != nullptr;
+  a.tiles_m = (int)((M + f.bm - 1) / f.bm); a.act = act; a.fuse = bias != nullptr; a.add = add;
   if ((int64_t)a.tiles_m * ((N + f.bn - 1) / f.bn) > 0x7fffffffLL) return hipErrorInvalidValue;
   return f.fn(a, s);
 }

@@ -38,6 +38,10 @@ static int64_t g_dx_fused = 1;
 static int64_t g_dx_tile = -1;
 static int64_t g_dx_conv = -1;
 static int64_t g_dw_res = -1;
+// state.delta of the 1x1 / stride-1 layers on conv1x1.hip (W^T over the delta
+// planes, the col2im add in the epilogue) where conv1x1_pick takes the shape;
+// TNS_DX_C1=0 (A/B): the TN product / conv_dx forms
+static bool g_dx_c1 = !(getenv("TNS_DX_C1") && getenv("TNS_DX_C1")[0] == '0');
 // the BN conv backward as one chain pass + normalizeDelta (launch_bn_backward_fused);
 // TNS_BN_FUSED=0 (A/B): the three-pass form
 static bool g_bn_fused = !(getenv("TNS_BN_FUSED") && getenv("TNS_BN_FUSED")[0] == '0');
@@ -2009,8 +2013,15 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // state.input.im2Col(...) — a 1x1/s1/p0 col matrix is the input itself
   const bool needs_col = kSize != 1 || stride != 1 || padding != 0 || dilation != 1;
   // state.delta of stride-1 layers without the col matrix (conv_dx.hip)
+  // state.delta of a 1x1 / stride-1 layer as a 1x1 convolution of the delta
+  // planes with W^T on conv1x1.hip, the col2im add in its epilogue (the same
+  // chains and the same add as the TN product with EPI_ADD)
+  const int dx1 = state_delta && g_dx_c1 && g_dx_fused != 2 && kSize == 1 && stride == 1 &&
+                          padding == 0 && dilation == 1
+                      ? conv1x1_pick(C, batch * i_k, filters, i_k)
+                      : -1;
   const bool fused_dx =
-      state_delta && dilation == 1 &&
+      dx1 < 0 && state_delta && dilation == 1 &&
       ((g_dx_fused == 1 && conv_dx_fused_applies(C, H, W, kSize, stride, filters, g.oh, g.ow)) ||
        (g_dx_fused == 2 && conv_dx_fused_fits(C, H, W, stride, filters, g.oh, g.ow)));
   // dW with the im2col matrix generated inside the sdot-order product
@@ -2108,7 +2119,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // scratch of the fused state.delta kernel, sized before any fork (a growth
   // inside the side-stream chain would free a buffer the main stream may use)
   float* wt = nullptr;
-  if (fused_dx || dxc >= 0)
+  if (fused_dx || dxc >= 0 || dx1 >= 0)
     if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
 
   auto run_dw = [&]() -> int {
@@ -2213,6 +2224,17 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     }
     bool done = false;
     float* col = dx_direct ? state_delta : dx_ws;
+    if (dx1 >= 0) {  // (1x1 / stride 1: dx_direct)
+      OpTimer t(c, TNS_OP_GEMM);
+      if (int r = hip_status(launch_transpose(weights, wt, filters, C, c->stream),
+                             "weights transpose launch"))
+        return r;
+      const hipError_t e = launch_conv1x1(dx1, wt, delta, nullptr, state_delta, batch, C, filters,
+                                          i_k, 0, c->stream, true);
+      if (e == hipSuccess) return TNS_OK;
+      if (e != hipErrorInvalidValue) return hip_status(e, "dX 1x1 launch");
+      // (operands off the 16-byte alignment the DMA needs: the TN product)
+    }
     if (g_dx_tile != -2) {
       const int dv = g_dx_tile >= 0 ? (int)g_dx_tile : conv_tile4_dx_pick(i_n, batch * i_k, i_m, kSize);
       if (dv >= 0) {
