@@ -805,190 +805,6 @@ __global__ __launch_bounds__(256) void block_chains_ws(const float* __restrict__
   }
 }
 
-// CH_BNB with the waves specialised (planes of >= 16384 pixels): as
-// block_chains_ws, with four LDS streams (d, x_norm, d * scale,
-// (x - mean) * d * scale) and a row of ones, two LDS buffers (a tile is
-// loaded at the top of tile t, written after the barrier that ends t into
-// the buffer tile t was read from, read in tile t+2 — the chain wave's reads
-// of a tile complete before it reaches that barrier), 16 staged floats per
-// thread and stream.  Chain lanes 0-7 / 8-15 / 16-23 as block_chains' BNB.
-__global__ __launch_bounds__(256) void bnb_chains_ws(const float* __restrict__ a,
-                                                     const float* __restrict__ xn,
-                                                     const float* __restrict__ c3,
-                                                     const float* __restrict__ xx,
-                                                     const float* __restrict__ mu_arr,
-                                                     const float* __restrict__ sc_arr,
-                                                     int64_t nblocks, int64_t N, int64_t bs,
-                                                     int quirk, int act, float* __restrict__ part0,
-                                                     float* __restrict__ part1,
-                                                     float* __restrict__ part2) {
-  __builtin_amdgcn_s_setprio(3);
-  constexpr int SNT = 192, E = 16, TILE = SNT * E, NBUF = 2;
-  constexpr int LDT = TILE / 8 + 72;  // (rows: 8 mod 32, 72 floats of slack)
-  __shared__ __attribute__((aligned(16))) float U[NBUF][8 * LDT];
-  __shared__ __attribute__((aligned(16))) float V[NBUF][8 * LDT];
-  __shared__ __attribute__((aligned(16))) float Mt[NBUF][8 * LDT];
-  __shared__ __attribute__((aligned(16))) float Qt[NBUF][8 * LDT];
-  __shared__ __attribute__((aligned(16))) float ONES[LDT];
-  const int tid = threadIdx.x;
-  const bool chainwave = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;
-  const int st = tid - 64;
-  const int l = tid & 7, grp = tid >> 3;
-  const bool chain = grp <= 2;
-  const int64_t nb8 = (bs >> 3) << 3;
-  const int ntile = (int)((nb8 + TILE - 1) / TILE);
-  const int tail = (int)(bs & 7);
-  for (int q = tid; q < LDT; q += 256) ONES[q] = 1.0f;  // (published by the first barrier)
-  for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
-    const int64_t i = blk % N;
-    const float* pa = a + blk * bs;
-    const float* pb = xn + blk * bs;
-    const float* pc = c3 + blk * bs;
-    const float* px = xx + blk * bs;
-    const float mu = mu_arr[i], scl = sc_arr[i];
-    float acc = 0.0f;
-    if (!chainwave) {
-      const bool v4 = ((reinterpret_cast<uintptr_t>(pa) | reinterpret_cast<uintptr_t>(pb) |
-                        reinterpret_cast<uintptr_t>(pc) | reinterpret_cast<uintptr_t>(px)) & 15) == 0;
-      float ra[E], rb[E], rc[E], rx[E];
-      auto load = [&](int t) {
-        const int64_t t0 = (int64_t)t * TILE;
-        if (v4) {
-#pragma unroll
-          for (int u = 0; u < E / 4; ++u) {
-            const int64_t k = t0 + 4 * (st + SNT * u);
-            const bool in = k < nb8;
-            const float4 z = {0, 0, 0, 0};
-            const float4 qa = in ? *reinterpret_cast<const float4*>(pa + k) : z;
-            const float4 qb = in ? *reinterpret_cast<const float4*>(pb + k) : z;
-            const float4 qc = in ? *reinterpret_cast<const float4*>(pc + k) : z;
-            const float4 qx = in ? *reinterpret_cast<const float4*>(px + k) : z;
-            ra[4 * u] = qa.x; ra[4 * u + 1] = qa.y; ra[4 * u + 2] = qa.z; ra[4 * u + 3] = qa.w;
-            rb[4 * u] = qb.x; rb[4 * u + 1] = qb.y; rb[4 * u + 2] = qb.z; rb[4 * u + 3] = qb.w;
-            rc[4 * u] = qc.x; rc[4 * u + 1] = qc.y; rc[4 * u + 2] = qc.z; rc[4 * u + 3] = qc.w;
-            rx[4 * u] = qx.x; rx[4 * u + 1] = qx.y; rx[4 * u + 2] = qx.z; rx[4 * u + 3] = qx.w;
-          }
-        } else {
-#pragma unroll
-          for (int u = 0; u < E / 4; ++u)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              const int64_t k = t0 + 4 * (st + SNT * u) + c;
-              const bool in = k < nb8;
-              ra[4 * u + c] = in ? pa[k] : 0.0f;
-              rb[4 * u + c] = in ? pb[k] : 0.0f;
-              rc[4 * u + c] = in ? pc[k] : 0.0f;
-              rx[4 * u + c] = in ? px[k] : 0.0f;
-            }
-        }
-      };
-      auto store = [&](int buf) {
-#pragma unroll
-        for (int u = 0; u < E / 4; ++u)
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int ee = 4 * (st + SNT * u) + c;
-            const int e = (ee & 7) * LDT + (ee >> 3);
-            const float d = ra[4 * u + c] * grad_apply(rc[4 * u + c], act);  // Derivative
-            const float ds = d * scl;                                          // forwardScale
-            U[buf][e] = d;
-            V[buf][e] = rb[4 * u + c];
-            Mt[buf][e] = ds;
-            Qt[buf][e] = (rx[4 * u + c] - mu) * ds;
-          }
-      };
-      for (int t = 0; t < 2 && t < ntile; ++t) {
-        load(t);
-        store(t);
-      }
-      __syncthreads();
-      for (int t = 0; t < ntile; ++t) {
-        const bool more = t + 2 < ntile;
-        if (more) load(t + 2);
-        __syncthreads();
-        if (more) store(t % NBUF);
-      }
-    } else {
-      __syncthreads();
-      for (int t = 0; t < ntile; ++t) {
-        if (chain) {
-          const int64_t rem = nb8 - (int64_t)t * TILE;
-          const int cnt = (int)((rem < TILE ? rem : TILE) >> 3);
-          const int buf = t % NBUF;
-          const float* row = (grp == 0 ? &U[buf][0] : grp == 1 ? &Mt[buf][0] : &Qt[buf][0]) + l * LDT;
-          const float* rowb = grp == 0 ? &V[buf][0] + l * LDT : ONES;
-          // (block_chains_ws' CH_DOT ring: two sets of 8 reads, lgkmcnt(8))
-          typedef float f4 __attribute__((ext_vector_type(4)));
-          const unsigned ra_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)row;
-          const unsigned rb_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) const float*)rowb;
-          auto rd = [&](int q, f4 (&v)[4], f4 (&w)[4]) {
-            const unsigned aa = ra_lds + 4u * (unsigned)q, bb = rb_lds + 4u * (unsigned)q;
-            asm volatile("ds_read_b128 %0, %1" : "=v"(v[0]) : "v"(aa));
-            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(v[1]) : "v"(aa));
-            asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(v[2]) : "v"(aa));
-            asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(v[3]) : "v"(aa));
-            asm volatile("ds_read_b128 %0, %1" : "=v"(w[0]) : "v"(bb));
-            asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(w[1]) : "v"(bb));
-            asm volatile("ds_read_b128 %0, %1 offset:32" : "=v"(w[2]) : "v"(bb));
-            asm volatile("ds_read_b128 %0, %1 offset:48" : "=v"(w[3]) : "v"(bb));
-          };
-          auto wait8 = [&](f4 (&v)[4], f4 (&w)[4]) {
-            asm volatile("s_waitcnt lgkmcnt(8)"
-                         : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(w[0]), "+v"(w[1]),
-                           "+v"(w[2]), "+v"(w[3]));
-          };
-          auto fma16 = [&](const f4 (&v)[4], const f4 (&w)[4]) {
-#pragma unroll
-            for (int z = 0; z < 16; ++z) acc = fmaf(v[z >> 2][z & 3], w[z >> 2][z & 3], acc);
-          };
-          f4 va[4], wa[4], vb[4], wb[4];
-          const int full = cnt - cnt % 32;
-          rd(0, va, wa);
-          rd(16, vb, wb);
-          for (int q = 0; q < full; q += 32) {
-            wait8(va, wa);
-            fma16(va, wa);
-            rd(q + 32, va, wa);
-            wait8(vb, wb);
-            fma16(vb, wb);
-            rd(q + 48, vb, wb);
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)"
-                       : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(va[3]), "+v"(wa[0]),
-                         "+v"(wa[1]), "+v"(wa[2]), "+v"(wa[3]), "+v"(vb[0]), "+v"(vb[1]),
-                         "+v"(vb[2]), "+v"(vb[3]), "+v"(wb[0]), "+v"(wb[1]), "+v"(wb[2]),
-                         "+v"(wb[3]));
-          for (int q = full; q < cnt; ++q) acc = fmaf(row[q], rowb[q], acc);
-        }
-        __syncthreads();
-      }
-    }
-    if (tid < 64) {  // the lane-order epilogues (block_chains' BNB)
-      auto bnb_d = [&](int k) { return pa[nb8 + k] * grad_apply(pc[nb8 + k], act); };
-      if (tail && grp == 0) {
-        const float xa = l < tail ? bnb_d(l) : 0.0f;
-        const float xb = l < tail ? pb[nb8 + l] : 0.0f;
-        acc = fmaf(xa, xb, acc);
-      }
-      const bool lanes_form = grp == 2;
-      const float up = __shfl_down(acc, 4, 8);
-      float x0 = (lanes_form && tail == 0 && quirk) ? acc : acc + up;
-      if (lanes_form && l == 0)
-        for (int k = 0; k < tail; ++k) x0 = x0 + (px[nb8 + k] - mu) * (bnb_d(k) * scl);
-      const float h = x0 + __shfl_down(x0, 1, 8);
-      float r = h + __shfl_down(h, 2, 8);
-      if (l == 0 && chain) {
-        if (grp == 1)
-          for (int k = 0; k < tail; ++k) r = r + bnb_d(k) * scl;
-        if (grp == 0) part0[blk] = r;
-        else if (grp == 1) part1[blk] = r;
-        else part2[blk] = r;
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // per-channel passes: block results added over the groups in order
 enum FinMode { FIN_MEAN = 0, FIN_VAR = 1, FIN_VDELTA = 2, FIN_ADD = 3 };
 template <int MODE>
@@ -1524,24 +1340,19 @@ hipError_t launch_bn_backward_fused(float* scale_updates, const float* x_norm, f
                                     float* mean_delta, float* var_delta, int64_t groups,
                                     int64_t N, int64_t bs, int quirk, float* part, hipStream_t s) {
   if (N <= 0 || groups <= 0 || bs <= 0) return hipSuccess;
-  if (!use_chains(bs, part)) return hipErrorNotSupported;
+  // (the >= 16384-pixel planes keep the separate passes: a specialised-wave
+  // form of this pass with four LDS streams was bit-exact and no faster —
+  // YOLOv3 training backward 17.22 ms without it, 17.27 with it,
+  // profiles/r06_bn_fused_ws.json)
+  if (bs >= 16384 || !use_chains(bs, part)) return hipErrorNotSupported;
   const bool v4 = bs % 4 == 0 && al16(x) && al16(delta) && al16(output);
   const int bpr = row_bpr(groups * N, bs, v4 ? 4 : 1);
   if (!bpr) return hipErrorNotSupported;
   float* part1 = part + groups * N;
   float* part2 = part + 2 * groups * N;
-  static const bool ws_off = getenv("TNS_BN_WS") && getenv("TNS_BN_WS")[0] == '0';
-  if (bs >= 16384 && ws_off) return hipErrorNotSupported;  // (A/B: separate passes there)
-  if (bs >= 16384) {
-    const int64_t nblocks = groups * N;
-    const unsigned grid = (unsigned)(nblocks < (1 << 20) ? nblocks : (1 << 20));
-    hipLaunchKernelGGL(bnb_chains_ws, dim3(grid), dim3(256), 0, s, delta, x_norm, output, x, mean,
-                       scales, nblocks, N, bs, quirk, act, part, part1, part2);
-    if (hipError_t e = hipGetLastError()) return e;
-  } else if (hipError_t e = run_chains<CH_BNB>(delta, x_norm, mean, groups, N, bs, quirk, part,
-                                               part1, s, act, nullptr, output, scales, x, part2)) {
+  if (hipError_t e = run_chains<CH_BNB>(delta, x_norm, mean, groups, N, bs, quirk, part, part1, s,
+                                        act, nullptr, output, scales, x, part2))
     return e;
-  }
   hipLaunchKernelGGL(bnb_finish, dim3(nblk(N)), dim3(TPB), 0, s, part, part1, part2, groups, N, var,
                      scale_updates, mean_delta, var_delta);
   if (hipError_t e = hipGetLastError()) return e;
