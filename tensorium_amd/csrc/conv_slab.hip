@@ -140,6 +140,69 @@ __global__ __launch_bounds__(256) void slab_fill_kernel(SlabFillArgs a) {
     *reinterpret_cast<floatx4*>(dst + q * BN * 4) = floatx4{v[q], v[4 + q], v[8 + q], v[12 + q]};
 }
 
+// The same fill with the (column tile, k-tile, group) of a block uniform:
+// one block of BN (rounded up to whole waves) threads per (ct, t, g), a
+// thread one column — so the 16 k's (channel, tap) walk and the taps' byte
+// offsets are scalar, and a value costs the lane its window bit test, one
+// address add and its load (the per-lane form selected each tap's offset
+// out of nine registers: ~25 VALU instructions a value)
+template <int KS, int BK, int BN>
+__global__ __launch_bounds__((BN + 63) / 64 * 64) void slab_fill_u_kernel(SlabFillArgs a) {
+  constexpr int NG = BK / 16, KK = KS * KS;
+  const int c = threadIdx.x;
+  if (c >= BN) return;
+  const int64_t r1 = blockIdx.x;  // (ct * KT + t) * NG + g
+  const int g = (int)(r1 % NG);
+  const int64_t r2 = r1 / NG;
+  const int t = (int)(r2 % a.KT), ct = (int)(r2 / a.KT);
+  const int n = ct * BN + c;
+  float v[16];
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.x), 0, a.bytes, 0x00020000);
+  {
+    const int nn = n < a.N ? n : a.N - 1;  // (past N: any column, stored as 0)
+    const int img = slab_div(nn, a.ohw, a.inv_ohw), pix = nn - img * a.ohw;
+    const int oy = slab_div(pix, a.ow, a.inv_ow), ox = pix - oy * a.ow;
+    const int iy0 = oy * a.stride - a.pad, ix0 = ox * a.stride - a.pad;
+    const int HW = a.H * a.W;
+    unsigned mask = 0;
+#pragma unroll
+    for (int kr = 0; kr < KS; ++kr)
+#pragma unroll
+      for (int kc = 0; kc < KS; ++kc) {
+        const int iy = iy0 + kr * a.dil, ix = ix0 + kc * a.dil;
+        mask |= (unsigned)(((unsigned)iy < (unsigned)a.H) & ((unsigned)ix < (unsigned)a.W))
+                << (kr * KS + kc);
+      }
+    if (n >= a.N) mask = 0;
+    const unsigned base = 4u * (unsigned)(img * (int)a.strideX + iy0 * a.W + ix0);
+    // (block-uniform from here: k0, the channel / tap walk, the tap offsets)
+    const int k0 = __builtin_amdgcn_readfirstlane(t * BK + 16 * g);
+    int ch = k0 / KK, tap = k0 - ch * KK;
+    int kr = tap / KS, kc = tap - kr * KS;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const unsigned uoff = 4u * (unsigned)(ch * HW + kr * a.dil * a.W + kc * a.dil);
+      const unsigned o = ((mask >> tap) & 1u) ? base + uoff : 0x80000000u;
+      v[e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, o, 0, 0));
+      ++tap;
+      if (++kc == KS) {
+        kc = 0;
+        ++kr;
+      }
+      if (tap == KK) {
+        tap = 0;
+        kr = 0;
+        ++ch;
+      }
+    }
+  }
+  float* dst = a.slab + ((r2 * NG + g) * 4 * BN + c) * 4;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<floatx4*>(dst + q * BN * 4) = floatx4{v[q], v[4 + q], v[8 + q], v[12 + q]};
+}
+
 struct SlabGemmArgs {
   const float* A;  // weights [M][K]
   const float* slab;
@@ -413,6 +476,20 @@ hipError_t launch_slab_gemm(const SlabGemmArgs& a, hipStream_t s) {
 
 template <int BK, int BN>
 hipError_t launch_slab_fill(const SlabFillArgs& a, int ks, hipStream_t s) {
+#ifndef TNS_SLAB_FILL_LANE  // (A/B side builds: the per-lane form)
+  {
+    constexpr int NT = (BN + 63) / 64 * 64;
+    const int64_t nb = a.units / BN;  // (ct, t, g) triples
+    if (nb > 0x7fffffffLL) return hipErrorInvalidValue;
+    if (ks == 3)
+      hipLaunchKernelGGL((slab_fill_u_kernel<3, BK, BN>), dim3((unsigned)nb), dim3(NT), 0, s, a);
+    else if (ks == 1)
+      hipLaunchKernelGGL((slab_fill_u_kernel<1, BK, BN>), dim3((unsigned)nb), dim3(NT), 0, s, a);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
+#endif
   const unsigned blocks = (unsigned)((a.units + 255) / 256);
   if (ks == 3)
     hipLaunchKernelGGL((slab_fill_kernel<3, BK, BN>), dim3(blocks), dim3(256), 0, s, a);
