@@ -56,7 +56,6 @@ struct C1Args {
   int M, N, K, P, tiles_m, act;
   bool fuse;
   bool add;  // C := C + product (the conv backward's 1x1 col2im: one add a pixel)
-  bool at;   // A given k-major ([K][M]: the conv backward's W^T read from W)
 };
 
 // BM x BN block, BK-deep k-tiles, WM x WN waves: a wave = 16 rows x 64
@@ -139,31 +138,7 @@ __global__ __launch_bounds__(G::NT) void conv1x1_kernel(C1Args p) {
   }
   const float* a_row0 = p.A + (int64_t)m0 * K;
   floatx4 ra[AU];
-  // (at) the unit's four k as four dword loads down W's rows (column m)
-  float rt[AU][4];
-  unsigned at_off[AU];
-#pragma unroll
-  for (int u = 0; u < AU; ++u) {
-    const int idx = tid + G::NT * u;
-    const int lo = idx & 7, rest = idx >> 3;
-    const int m = rest % BM, kq4 = lo + 8 * (rest / BM);
-    const int mr = m0 + m < p.M ? m0 + m : p.M - 1;
-    at_off[u] = 4u * (unsigned)(4 * kq4 * p.M + mr);
-  }
-  const unsigned at_row = 4u * (unsigned)p.M;  // (bytes between consecutive k)
   auto load_a = [&](int t) {
-    if (p.at) {  // (launch-uniform)
-      const float* sb = p.A + (int64_t)t * BK * p.M;
-#pragma unroll
-      for (int u = 0; u < AU; ++u)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          asm volatile("global_load_dword %0, %1, %2"
-                       : "=v"(rt[u][c])
-                       : "v"(at_off[u] + (unsigned)c * at_row), "s"(sb)
-                       : "memory");
-      return;
-    }
     const float* sb = a_row0 + t * BK;
 #pragma unroll
     for (int u = 0; u < AU; ++u)
@@ -171,15 +146,6 @@ __global__ __launch_bounds__(G::NT) void conv1x1_kernel(C1Args p) {
   };
   auto store_a = [&](int st) {
     float* as = smem + st * STAGE;
-    if (p.at) {
-#pragma unroll
-      for (int u = 0; u < AU; ++u) {
-        asm volatile("" : "+v"(rt[u][0]), "+v"(rt[u][1]), "+v"(rt[u][2]), "+v"(rt[u][3]));
-#pragma unroll
-        for (int c = 0; c < 4; ++c) as[a_dst[u] + c * BM * 4] = rt[u][c];
-      }
-      return;
-    }
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
       asm volatile("" : "+v"(ra[u]));
@@ -337,9 +303,38 @@ int conv1x1_pick(int64_t M, int64_t N, int64_t K, int64_t P) {
   return 3;
 }
 
+// out[c][r] = in[r][c] (rows x cols, 32 x 32 tiles through LDS): the
+// backward's transposed weights
+__global__ __launch_bounds__(256) void c1_transpose_kernel(const float* __restrict__ in,
+                                                           float* __restrict__ out, int rows,
+                                                           int cols) {
+  __shared__ float t[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = ty; y < 32; y += 8) {
+    const int r = r0 + y, c = c0 + tx;
+    t[y][tx] = r < rows && c < cols ? in[(int64_t)r * cols + c] : 0.0f;
+  }
+  __syncthreads();
+  for (int y = ty; y < 32; y += 8) {
+    const int c = c0 + y, r = r0 + tx;
+    if (c < cols && r < rows) out[(int64_t)c * rows + r] = t[tx][y];
+  }
+}
+
+hipError_t launch_transpose(const float* in, float* out, int64_t rows, int64_t cols,
+                            hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (rows > (1 << 26) || cols > (1 << 26)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(c1_transpose_kernel,
+                     dim3((unsigned)((cols + 31) / 32), (unsigned)((rows + 31) / 32)), dim3(256), 0,
+                     s, in, out, (int)rows, (int)cols);
+  return hipGetLastError();
+}
+
 hipError_t launch_conv1x1(int v, const float* weights, const float* x, const float* bias,
                           float* out, int64_t batch, int64_t M, int64_t K, int64_t P, int act,
-                          hipStream_t s, bool add, bool at) {
+                          hipStream_t s, bool add) {
   if (v < 0 || v >= kNumC1) return hipErrorInvalidValue;
   const C1Form& f = kC1[v];
   const int64_t N = batch * P;
@@ -351,7 +346,6 @@ hipError_t launch_conv1x1(int v, const float* weights, const float* x, const flo
   a.A = weights; a.X = x; a.C = out; a.bias = bias;
   a.M = (int)M; a.N = (int)N; a.K = (int)K; a.P = (int)P;
   a.tiles_m = (int)((M + f.bm - 1) / f.bm); a.act = act; a.fuse = bias != nullptr; a.add = add;
-  a.at = at;
   if ((int64_t)a.tiles_m * ((N + f.bn - 1) / f.bn) > 0x7fffffffLL) return hipErrorInvalidValue;
   return f.fn(a, s);
 }

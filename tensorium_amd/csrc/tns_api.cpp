@@ -2119,7 +2119,7 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
   // scratch of the fused state.delta kernel, sized before any fork (a growth
   // inside the side-stream chain would free a buffer the main stream may use)
   float* wt = nullptr;
-  if (fused_dx || dxc >= 0)
+  if (fused_dx || dxc >= 0 || dx1 >= 0)
     if (int r = ensure_scratch(c, SLOT_WT, filters * C * kSize * kSize, &wt)) return r;
 
   auto run_dw = [&]() -> int {
@@ -2224,10 +2224,13 @@ int conv_backward_impl(tns_ctx* c, int64_t batch, int64_t C, int64_t H, int64_t 
     }
     bool done = false;
     float* col = dx_direct ? state_delta : dx_ws;
-    if (dx1 >= 0) {  // (1x1 / stride 1: dx_direct; W^T read from W's rows)
+    if (dx1 >= 0) {  // (1x1 / stride 1: dx_direct)
       OpTimer t(c, TNS_OP_GEMM);
-      const hipError_t e = launch_conv1x1(dx1, weights, delta, nullptr, state_delta, batch, C,
-                                          filters, i_k, 0, c->stream, true, true);
+      if (int r = hip_status(launch_transpose(weights, wt, filters, C, c->stream),
+                             "weights transpose launch"))
+        return r;
+      const hipError_t e = launch_conv1x1(dx1, wt, delta, nullptr, state_delta, batch, C, filters,
+                                          i_k, 0, c->stream, true);
       if (e == hipSuccess) return TNS_OK;
       if (e != hipErrorInvalidValue) return hip_status(e, "dX 1x1 launch");
       // (operands off the 16-byte alignment the DMA needs: the TN product)

@@ -149,7 +149,10 @@ const char* conv1x1_name(int v);
 int conv1x1_pick(int64_t M, int64_t N, int64_t K, int64_t P);
 hipError_t launch_conv1x1(int v, const float* weights, const float* x, const float* bias,
                           float* out, int64_t batch, int64_t M, int64_t K, int64_t P, int act,
-                          hipStream_t s, bool add = false, bool at = false);
+                          hipStream_t s, bool add = false);
+// out[c][r] = in[r][c] (rows x cols)
+hipError_t launch_transpose(const float* in, float* out, int64_t rows, int64_t cols,
+                            hipStream_t s);
 int conv_slab_count();
 const char* conv_slab_name(int v);
 int conv_slab_pick(int64_t M, int64_t N, int64_t K, int64_t ks);
