@@ -238,7 +238,8 @@ __global__ void normalize_delta_k(const float* __restrict__ x, const float* __re
                                   const float* __restrict__ mean_delta,
                                   const float* __restrict__ var_delta, float* __restrict__ delta,
                                   int64_t total, int64_t N, int64_t bs, float B,
-                                  const float* __restrict__ scales) {
+                                  const float* __restrict__ scales,
+                                  const float* __restrict__ out, int act) {
   for (int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x; e < total;
        e += (int64_t)gridDim.x * TPB) {
     const int64_t i = (e / bs) % N;
@@ -246,7 +247,9 @@ __global__ void normalize_delta_k(const float* __restrict__ x, const float* __re
     const float vd = 2.0f * var_delta[i] / B;
     const float ve = var[i] > SEPS ? var[i] : SEPS;
     const float sd = sqrtf(ve);
-    const float a = (scales ? delta[e] * scales[i] : delta[e]) / sd;
+    float d = delta[e];
+    if (out) d = d * grad_apply(out[e], act);  // (Derivative folded in)
+    const float a = (scales ? d * scales[i] : d) / sd;
     const float t = (x[e] - mean[i]) * vd + md;  // sNormalizeDelta_avx order
     delta[e] = a + t;
   }
@@ -976,20 +979,58 @@ __device__ __forceinline__ void st(float* p, const float (&v)[V]) {
     *p = v[0];
 }
 
-template <int V>
+// (FIN: the CH_BNB finish folded in — each block sums its channel's group
+// partials in order (bnb_finish's arithmetic) for its mean / variance
+// deltas, and the channel's first block stores them and adds the dot sums
+// to scale_updates: one launch less per layer)
+struct BnbFin {
+  const float *p0, *p1, *p2;
+  int64_t groups;
+  float *dot_out, *md_out, *vd_out;
+};
+template <int V, bool FIN = false>
 __global__ __launch_bounds__(TPB) void normalize_delta_rows(
     const float* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ var,
     const float* __restrict__ mean_delta, const float* __restrict__ var_delta,
     float* __restrict__ delta, int64_t N, int64_t bs, int bpr, float B,
-    const float* __restrict__ scales, const float* __restrict__ out, int act) {
+    const float* __restrict__ scales, const float* __restrict__ out, int act, BnbFin fin) {
   int64_t row, i;
   int seg;
   row_of(bpr, N, row, i, seg);
   // (out: Derivative folded in first, delta * f'(out); scales: forwardScale)
   const bool scaled = scales != nullptr;
   const float scl = scaled ? scales[i] : 1.0f;
-  const float md = mean_delta[i] / B;
-  const float vd = 2.0f * var_delta[i] / B;
+  float mdi, vdi;
+  if constexpr (FIN) {
+    __shared__ float sh[2];
+    if (threadIdx.x == 0) {
+      float d = 0.0f, m = 0.0f, v = 0.0f;
+      for (int64_t g = 0; g < fin.groups; ++g) {
+        d = d + fin.p0[g * N + i];
+        m = m + fin.p1[g * N + i];
+        v = v + fin.p2[g * N + i];
+      }
+      const float ve = var[i] > SEPS ? var[i] : SEPS;
+      const float inv = -1.0f / sqrtf(ve);
+      const float mdv = m * inv;
+      const float vdv = (float)((double)v * -0.5 * pow((double)ve, -1.5));
+      if (row < N && seg == 0) {  // (group 0's first block of the channel)
+        fin.dot_out[i] = fin.dot_out[i] + d;
+        fin.md_out[i] = mdv;
+        fin.vd_out[i] = vdv;
+      }
+      sh[0] = mdv;
+      sh[1] = vdv;
+    }
+    __syncthreads();
+    mdi = sh[0];
+    vdi = sh[1];
+  } else {
+    mdi = mean_delta[i];
+    vdi = var_delta[i];
+  }
+  const float md = mdi / B;
+  const float vd = 2.0f * vdi / B;
   const float ve = var[i] > SEPS ? var[i] : SEPS;
   const float sd = sqrtf(ve);
   const float m = mean[i];
@@ -1317,15 +1358,16 @@ hipError_t launch_normalize_delta(const float* x, const float* mean, const float
     if (v4)
       hipLaunchKernelGGL(normalize_delta_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
                          s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                         (float)(groups * bs), scales, nullptr, 0);
+                         (float)(groups * bs), scales, nullptr, 0, BnbFin{});
     else
       hipLaunchKernelGGL(normalize_delta_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0,
                          s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                         (float)(groups * bs), scales, nullptr, 0);
+                         (float)(groups * bs), scales, nullptr, 0, BnbFin{});
     return hipGetLastError();
   }
   hipLaunchKernelGGL(normalize_delta_k, dim3(nblk(total)), dim3(TPB), 0, s, x, mean, var,
-                     mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs), scales);
+                     mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs), scales,
+                     nullptr, 0);
   return hipGetLastError();
 }
 
@@ -1347,23 +1389,30 @@ hipError_t launch_bn_backward_fused(float* scale_updates, const float* x_norm, f
   if (bs >= 16384 || !use_chains(bs, part)) return hipErrorNotSupported;
   const bool v4 = bs % 4 == 0 && al16(x) && al16(delta) && al16(output);
   const int bpr = row_bpr(groups * N, bs, v4 ? 4 : 1);
-  if (!bpr) return hipErrorNotSupported;
   float* part1 = part + groups * N;
   float* part2 = part + 2 * groups * N;
   if (hipError_t e = run_chains<CH_BNB>(delta, x_norm, mean, groups, N, bs, quirk, part, part1, s,
                                         act, nullptr, output, scales, x, part2))
     return e;
-  hipLaunchKernelGGL(bnb_finish, dim3(nblk(N)), dim3(TPB), 0, s, part, part1, part2, groups, N, var,
-                     scale_updates, mean_delta, var_delta);
-  if (hipError_t e = hipGetLastError()) return e;
+  if (!bpr) {  // (short planes: the finish, then the element form of normalizeDelta)
+    hipLaunchKernelGGL(bnb_finish, dim3(nblk(N)), dim3(TPB), 0, s, part, part1, part2, groups, N,
+                       var, scale_updates, mean_delta, var_delta);
+    if (hipError_t e = hipGetLastError()) return e;
+    const int64_t total = groups * N * bs;
+    hipLaunchKernelGGL(normalize_delta_k, dim3(nblk(total)), dim3(TPB), 0, s, x, mean, var,
+                       mean_delta, var_delta, delta, total, N, bs, (float)(groups * bs), scales,
+                       output, act);
+    return hipGetLastError();
+  }
+  const BnbFin fin{part, part1, part2, groups, scale_updates, mean_delta, var_delta};
   if (v4)
-    hipLaunchKernelGGL(normalize_delta_rows<4>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s,
-                       x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                       (float)(groups * bs), scales, output, act);
+    hipLaunchKernelGGL((normalize_delta_rows<4, true>), dim3((unsigned)(groups * N * bpr)), dim3(TPB),
+                       0, s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
+                       (float)(groups * bs), scales, output, act, fin);
   else
-    hipLaunchKernelGGL(normalize_delta_rows<1>, dim3((unsigned)(groups * N * bpr)), dim3(TPB), 0, s,
-                       x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
-                       (float)(groups * bs), scales, output, act);
+    hipLaunchKernelGGL((normalize_delta_rows<1, true>), dim3((unsigned)(groups * N * bpr)), dim3(TPB),
+                       0, s, x, mean, var, mean_delta, var_delta, delta, N, bs, bpr,
+                       (float)(groups * bs), scales, output, act, fin);
   return hipGetLastError();
 }
 
