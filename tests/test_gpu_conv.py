@@ -746,7 +746,12 @@ BN_CASES = [(2, 3, 17, 8, 3, 1, 1, 9, 1), (3, 5, 12, 7, 3, 2, 1, 9, 1), (2, 16, 
             (2, 6, 13, 33, 3, 1, 1, 0, 1), (2, 4, 15, 6, 3, 1, 1, 9, 2),
             # 65^2 = 4225-pixel planes: the 256-thread chain form with a tail;
             # 129^2 = 16641: the specialised-wave form with a tail
-            (1, 2, 65, 3, 3, 1, 1, 9, 1), (1, 1, 129, 2, 3, 1, 1, 9, 1)]
+            (1, 2, 65, 3, 3, 1, 1, 9, 1), (1, 1, 129, 2, 3, 1, 1, 9, 1),
+            # the fused batchNormBack's edges: 16^2 = 256 pixels (the first
+            # plane past the short-plane finish), 127^2 = 16129 (the largest
+            # fused plane), 128^2 = 16384 (the first on the separate passes)
+            (2, 3, 16, 5, 3, 1, 1, 9, 1), (1, 1, 127, 2, 3, 1, 1, 9, 1),
+            (1, 1, 128, 2, 3, 1, 1, 9, 1)]
 
 
 @pytest.mark.parametrize("quirk", [0, 1])
