@@ -33,6 +33,7 @@
 // The rearranged delta (rows = filters) and col (rows = (c, kr, kc), or the
 // input planes themselves for a 1x1 / stride-1 layer) are written by one pass
 // each over their sources (reads coalesced, 32-byte write sectors).
+#include <cstdlib>
 #include <algorithm>
 
 #include "tns_internal.hpp"
@@ -361,6 +362,52 @@ __global__ __launch_bounds__(256) void dw_res_accumulate_kernel(float* __restric
         dot = ((q[0] + q[4 * mn]) + (q[mn] + q[5 * mn])) +
               ((q[2 * mn] + q[6 * mn]) + (q[3 * mn] + q[7 * mn]));
       c = c + alpha * dot;
+    }
+    C[o] = c;
+  }
+}
+
+// float4 form of the same (mn % 4 == 0, 16-byte aligned planes), per element
+// the same operations in the same order; the G group planes of 8 / G images
+// are loaded before the adds so eight 16-byte reads a lane are in flight
+// (the scalar form holds one 4-byte read a lane: latency-bound near 1.5 TB/s)
+template <int G>
+__global__ __launch_bounds__(256) void dw_res_accumulate4_kernel(float4* __restrict__ C,
+                                                                 const float4* __restrict__ P,
+                                                                 int64_t mn4, int64_t strideP4,
+                                                                 int batch, float alpha) {
+  constexpr int U = 8 / G;  // images per load group
+  for (int64_t o = blockIdx.x * 256LL + threadIdx.x; o < mn4; o += (int64_t)gridDim.x * 256) {
+    float4 c = C[o];
+    for (int b0 = 0; b0 < batch; b0 += U) {
+      float4 v[U][G];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (b0 + u < batch) {
+#pragma unroll
+          for (int g = 0; g < G; ++g) v[u][g] = P[(b0 + u) * strideP4 + g * mn4 + o];
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (b0 + u < batch) {
+          const float4* q = v[u];
+          float4 dot;
+#define TNS_ACC_DOT(f)                                                                           \
+  if constexpr (G == 1)                                                                          \
+    dot.f = q[0].f;                                                                              \
+  else if constexpr (G == 2)                                                                     \
+    dot.f = q[0].f + q[1].f;                                                                     \
+  else if constexpr (G == 4)                                                                     \
+    dot.f = (q[0].f + q[1].f) + (q[2].f + q[3].f);                                               \
+  else                                                                                           \
+    dot.f = ((q[0].f + q[4].f) + (q[1].f + q[5].f)) + ((q[2].f + q[6].f) + (q[3].f + q[7].f)); \
+  c.f = c.f + alpha * dot.f;
+          TNS_ACC_DOT(x)
+          TNS_ACC_DOT(y)
+          TNS_ACC_DOT(z)
+          TNS_ACC_DOT(w)
+#undef TNS_ACC_DOT
+        }
     }
     C[o] = c;
   }
@@ -865,6 +912,26 @@ hipError_t launch_dw_res(int v, const DwResArgs& d, hipStream_t s) {
   if (hipError_t e = f.fn(a, d.batch, s); e != hipSuccess) return e;
   if (f.fold_images) return hipSuccess;  // (weight_updates written by the product)
   const int64_t mn = d.M * d.N;
+  // (TNS_ACC4=0: the scalar form, for A/B runs)
+  static const bool acc4 = !(getenv("TNS_ACC4") && getenv("TNS_ACC4")[0] == '0');
+  if (acc4 && mn % 4 == 0 && !(reinterpret_cast<uintptr_t>(d.weight_updates) & 15) &&
+      !(reinterpret_cast<uintptr_t>(d.part) & 15)) {
+    const int64_t mn4 = mn / 4;
+    auto go = [&](auto gc) {
+      constexpr int Gv = decltype(gc)::value;
+      hipLaunchKernelGGL((dw_res_accumulate4_kernel<Gv>), dim3(blocks_for(mn4)), dim3(256), 0, s,
+                         reinterpret_cast<float4*>(d.weight_updates),
+                         reinterpret_cast<const float4*>(d.part), mn4, a.strideP / 4,
+                         (int)d.batch, d.alpha);
+    };
+    switch (a.G) {
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 4: go(std::integral_constant<int, 4>{}); break;
+      default: go(std::integral_constant<int, 8>{}); break;
+    }
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(dw_res_accumulate_kernel, dim3(blocks_for(mn)), dim3(256), 0, s,
                      d.weight_updates, d.part, mn, a.G, a.strideP, (int)d.batch, d.alpha);
   return hipGetLastError();
