@@ -642,7 +642,8 @@ int tns_hip_gemm_variant(tns_ctx* ctx, int32_t variant, uint8_t transA, uint8_t 
  * at the default instead of the highest); TNS_BN_FUSED=0 — batchNormBack as
  * its separate passes instead of the one chain pass + normalizeDelta;
  * TNS_DX_C1=0 — the 1x1 layers' state.delta on the TN product / conv_dx forms
- * instead of conv1x1's W^T product. */
+ * instead of conv1x1's W^T product; TNS_ACC4=0 — the dW accumulate pass in
+ * its scalar form. */
 enum { TNS_OPT_STRICT_BETA0 = 0, TNS_OPT_CONV_VARIANT = 1, TNS_OPT_CONV_PAD = 2,
        TNS_OPT_NT_SDOT = 3, TNS_OPT_SRSS_QUIRK = 4, TNS_OPT_TT_EXACT = 5,
        TNS_OPT_SDOT_FORM = 6, TNS_OPT_DX_FUSED = 7, TNS_OPT_DX_TILE = 8,
